@@ -1,0 +1,341 @@
+"""Device-resident retrieval engines over the C ABI (include/classmate_hip.h).
+
+``DenseIndex`` (cosine k-NN, K1), ``BM25Index`` (postings + BM25, K2/K3/K7)
+and the fusion / pooling ops (K4 MMR, K5 RRF, K6 mean-pool).  Two call styles:
+
+* host arrays (numpy) — used by the drop-in classes in ``classmate_hip.retrieval``;
+* device tensors (torch) on torch's current HIP stream — used by the batched
+  pipeline and ``bench.py`` (inputs resident in HBM, graph-capturable).
+
+Rows are the integer positions the stores assign; string ids / documents /
+metadata stay on the host (classmate_hip.retrieval).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from typing import Optional, Sequence
+
+import numpy as np
+
+from . import _lib as L
+
+try:
+    import torch
+except Exception:  # pragma: no cover
+    torch = None
+
+
+def default_device() -> int:
+    env = os.environ.get("CM_DEVICE")
+    if env:
+        return int(env)
+    if torch is not None and torch.cuda.is_available():
+        return torch.cuda.current_device()
+    return 0
+
+
+def _stream(device: int):
+    if torch is None:
+        return None
+    return C.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def _c(a, dtype):
+    return np.ascontiguousarray(a, dtype=dtype)
+
+
+class DenseIndex:
+    """HBM-resident fp32 corpus + exact cosine top-k (replaces Chroma's HNSW)."""
+
+    def __init__(self, dim: int, device: Optional[int] = None, capacity: int = 0):
+        self.device = default_device() if device is None else int(device)
+        h = C.c_void_p()
+        L.check(L.fn["cm_dense_create"](self.device, int(dim), int(capacity), C.byref(h)), "cm_dense_create")
+        self._h = h
+        self.dim = int(dim)
+        self._ws = None
+
+    # -- lifecycle -------------------------------------------------------
+    def close(self):
+        if getattr(self, "_h", None):
+            L.fn["cm_dense_destroy"](self._h)
+            self._h = None
+
+    def __del__(self):  # pragma: no cover - interpreter shutdown order
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- mutation --------------------------------------------------------
+    def reserve(self, capacity: int):
+        L.check(L.fn["cm_dense_reserve"](self._h, int(capacity)), "cm_dense_reserve")
+
+    def upsert(self, vecs: np.ndarray, rows: np.ndarray):
+        v = _c(vecs, np.float32)
+        r = _c(rows, np.int64)
+        if v.ndim != 2 or v.shape[1] != self.dim or v.shape[0] != r.shape[0]:
+            raise ValueError(f"expected ({r.shape[0]}, {self.dim}) embeddings, got {v.shape}")
+        L.check(L.fn["cm_dense_upsert"](self._h, L.ptr(v), L.ptr(r), int(r.shape[0])), "cm_dense_upsert")
+
+    def upsert_dev(self, vecs, row0: int):
+        """vecs: contiguous float32 device tensor (n, dim) -> rows [row0, row0+n)."""
+        assert vecs.is_cuda and vecs.dtype == torch.float32 and vecs.is_contiguous() and vecs.shape[1] == self.dim
+        L.check(L.fn["cm_dense_upsert_dev"](self._h, L.ptr(vecs), int(row0), int(vecs.shape[0]),
+                                            _stream(self.device)), "cm_dense_upsert_dev")
+
+    def delete(self, rows):
+        r = _c(rows, np.int64)
+        L.check(L.fn["cm_dense_delete"](self._h, L.ptr(r), int(r.shape[0])), "cm_dense_delete")
+
+    def reset(self):
+        L.check(L.fn["cm_dense_reset"](self._h), "cm_dense_reset")
+
+    # -- queries ---------------------------------------------------------
+    @property
+    def size(self) -> int:
+        return int(L.fn["cm_dense_size"](self._h))
+
+    def live_count(self) -> int:
+        n = int(L.fn["cm_dense_live_count"](self._h))
+        if n < 0:
+            raise RuntimeError(L.last_error())
+        return n
+
+    def search(self, q: np.ndarray, k: int, allow_bits: Optional[np.ndarray] = None, return_vectors: bool = False):
+        """q: (nq, dim) -> dist (nq,k) f32, rows (nq,k) i64 (-1 pad)[, vecs (nq,k,dim)]."""
+        qq = _c(np.atleast_2d(q), np.float32)
+        if qq.shape[1] != self.dim:
+            raise ValueError(f"query dim {qq.shape[1]} != index dim {self.dim}")
+        nq = qq.shape[0]
+        dist = np.empty((nq, k), np.float32)
+        rows = np.empty((nq, k), np.int64)
+        vecs = np.empty((nq, k, self.dim), np.float32) if return_vectors else None
+        ab = None
+        if allow_bits is not None:
+            ab = _c(allow_bits, np.uint32)
+            need = (self.size + 31) // 32
+            if ab.shape[0] < need:
+                raise ValueError(f"allow bitmap has {ab.shape[0]} words, need {need}")
+        L.check(L.fn["cm_dense_search"](self._h, L.ptr(qq), nq, int(k), L.ptr(ab), L.ptr(dist), L.ptr(rows),
+                                        L.ptr(vecs)), "cm_dense_search")
+        return (dist, rows, vecs) if return_vectors else (dist, rows)
+
+    def workspace_bytes(self, nq: int, k: int) -> int:
+        n = int(L.fn["cm_dense_search_workspace"](self._h, int(nq), int(k)))
+        if n < 0:
+            raise ValueError("bad (nq, k) for dense search")
+        return n
+
+    def search_dev(self, q, k: int, allow=None, out=None, workspace=None):
+        """q: (nq, dim) float32 device tensor. Returns (dist f32 (nq,k), rows i64 (nq,k)) device tensors."""
+        nq = q.shape[0]
+        dev = q.device
+        wsb = self.workspace_bytes(nq, k)
+        if workspace is None:
+            if self._ws is None or self._ws.numel() < wsb:
+                self._ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
+            workspace = self._ws
+        if out is None:
+            out = (torch.empty((nq, k), dtype=torch.float32, device=dev),
+                   torch.empty((nq, k), dtype=torch.int64, device=dev))
+        L.check(L.fn["cm_dense_search_dev"](self._h, L.ptr(q), nq, int(k), L.ptr(allow), L.ptr(out[0]),
+                                            L.ptr(out[1]), L.ptr(workspace), int(workspace.numel()),
+                                            _stream(self.device)), "cm_dense_search_dev")
+        return out
+
+    def gather_dev(self, rows, out=None):
+        n = rows.numel()
+        if out is None:
+            out = torch.empty((n, self.dim), dtype=torch.float32, device=rows.device)
+        L.check(L.fn["cm_dense_gather_dev"](self._h, L.ptr(rows), n, L.ptr(out), _stream(self.device)),
+                "cm_dense_gather_dev")
+        return out
+
+
+class BM25Index:
+    """HBM-resident postings + BM25 Okapi with rank_bm25 0.2.x semantics."""
+
+    def __init__(self, device: Optional[int] = None):
+        self.device = default_device() if device is None else int(device)
+        h = C.c_void_p()
+        L.check(L.fn["cm_bm25_create"](self.device, C.byref(h)), "cm_bm25_create")
+        self._h = h
+        self.vocab = 0
+        self._ws = None
+
+    def close(self):
+        if getattr(self, "_h", None):
+            L.fn["cm_bm25_destroy"](self._h)
+            self._h = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def build(self, term_ids: np.ndarray, doc_off: np.ndarray, vocab: int, live: Optional[np.ndarray] = None):
+        t = _c(term_ids, np.int32)
+        o = _c(doc_off, np.int64)
+        lv = None if live is None else _c(live, np.uint8)
+        L.check(L.fn["cm_bm25_build"](self._h, L.ptr(t), L.ptr(o), int(o.shape[0] - 1), int(vocab), L.ptr(lv)),
+                "cm_bm25_build")
+        self.vocab = int(vocab)
+
+    def build_dev(self, term_ids, doc_off, vocab: int):
+        assert term_ids.dtype == torch.int32 and doc_off.dtype == torch.int64
+        L.check(L.fn["cm_bm25_build_dev"](self._h, L.ptr(term_ids), L.ptr(doc_off), int(doc_off.numel() - 1),
+                                          int(term_ids.numel()), int(vocab), _stream(self.device)),
+                "cm_bm25_build_dev")
+        self.vocab = int(vocab)
+
+    @property
+    def num_docs(self) -> int:
+        return int(L.fn["cm_bm25_num_docs"](self._h))
+
+    @property
+    def num_postings(self) -> int:
+        return int(L.fn["cm_bm25_num_postings"](self._h))
+
+    def stats(self):
+        n, s = C.c_int64(), C.c_int64()
+        a, e = C.c_double(), C.c_double()
+        L.check(L.fn["cm_bm25_stats"](self._h, C.byref(n), C.byref(s), C.byref(a), C.byref(e)), "cm_bm25_stats")
+        return dict(n_live=n.value, sum_len=s.value, avgdl=a.value, eps=e.value)
+
+    def search(self, queries: Sequence[Sequence[int]], k: int, allow_bits: Optional[np.ndarray] = None):
+        """queries: per query a list of term ids (-1 unknown). -> scores f64 (nq,k), rows i64, n i32."""
+        nq = len(queries)
+        off = np.zeros(nq + 1, np.int32)
+        for i, q in enumerate(queries):
+            off[i + 1] = off[i] + len(q)
+        flat = np.concatenate([np.asarray(q, np.int32) for q in queries]) if off[-1] else np.zeros(1, np.int32)
+        flat = _c(flat, np.int32)
+        scores = np.empty((nq, k), np.float64)
+        rows = np.empty((nq, k), np.int64)
+        nvalid = np.empty(nq, np.int32)
+        ab = None if allow_bits is None else _c(allow_bits, np.uint32)
+        L.check(L.fn["cm_bm25_search"](self._h, L.ptr(flat), L.ptr(off), nq, int(k), L.ptr(ab), L.ptr(scores),
+                                       L.ptr(rows), L.ptr(nvalid)), "cm_bm25_search")
+        return scores, rows, nvalid
+
+    def workspace_bytes(self, nq: int, total_terms: int, k: int) -> int:
+        n = int(L.fn["cm_bm25_search_workspace"](self._h, int(nq), int(total_terms), int(k)))
+        if n < 0:
+            raise ValueError("bad BM25 workspace request")
+        return n
+
+    def search_dev(self, q_terms, q_off, k: int, out=None, workspace=None):
+        """Unfiltered device search: q_terms int32 (T,), q_off int32 (nq+1,) device tensors."""
+        nq = q_off.numel() - 1
+        total = q_terms.numel()
+        wsb = self.workspace_bytes(nq, total, k)
+        if workspace is None:
+            if self._ws is None or self._ws.numel() < wsb:
+                self._ws = torch.empty(wsb, dtype=torch.uint8, device=q_terms.device)
+            workspace = self._ws
+        if out is None:
+            out = (torch.empty((nq, k), dtype=torch.float64, device=q_terms.device),
+                   torch.empty((nq, k), dtype=torch.int64, device=q_terms.device))
+        L.check(L.fn["cm_bm25_search_dev"](self._h, L.ptr(q_terms), L.ptr(q_off), nq, total, int(k), L.ptr(out[0]),
+                                           L.ptr(out[1]), L.ptr(workspace), int(workspace.numel()),
+                                           _stream(self.device)), "cm_bm25_search_dev")
+        return out
+
+
+# ---------------------------------------------------------------------------
+# Fusion and pooling ops
+# ---------------------------------------------------------------------------
+def mmr_order_batch(q: np.ndarray, cands: np.ndarray, k: int, lambd: float = 0.5,
+                    n_valid: Optional[np.ndarray] = None) -> np.ndarray:
+    """_mmr_order for nq queries on device. q (nq,d), cands (nq,P,d) -> (nq,k) int32 (-1 pad)."""
+    qq = _c(np.atleast_2d(q), np.float32)
+    cc = _c(cands, np.float32)
+    nq, pool, dim = cc.shape
+    out = np.empty((nq, k), np.int32)
+    nv = None if n_valid is None else _c(n_valid, np.int32)
+    L.check(L.fn["cm_mmr"](L.ptr(qq), L.ptr(cc), L.ptr(nv), nq, pool, dim, int(k), float(lambd), L.ptr(out)),
+            "cm_mmr")
+    return out
+
+
+def mmr_dev(q, cands, k: int, lambd: float = 0.5, n_valid=None, out=None):
+    nq, pool, dim = cands.shape
+    if out is None:
+        out = torch.empty((nq, k), dtype=torch.int32, device=q.device)
+    L.check(L.fn["cm_mmr_dev"](L.ptr(q), L.ptr(cands), L.ptr(n_valid), nq, pool, dim, int(k), float(lambd),
+                               L.ptr(out), _stream(q.device.index)), "cm_mmr_dev")
+    return out
+
+
+def rrf_fuse_keys(lists: Sequence[Sequence[int]], weights: Optional[Sequence[float]], rrf_k: int):
+    """rrf_fuse over int keys on device -> (keys in first-appearance order, scores)."""
+    nl = len(lists)
+    off = np.zeros(nl + 1, np.int32)
+    for i, l in enumerate(lists):
+        off[i + 1] = off[i] + len(l)
+    total = int(off[-1])
+    keys = np.asarray([x for l in lists for x in l] or [0], np.int64)
+    w = None if weights is None else _c([float(x) for x in weights], np.float64)
+    out_k = np.empty(max(total, 1), np.int64)
+    out_s = np.empty(max(total, 1), np.float64)
+    n = C.c_int32(0)
+    L.check(L.fn["cm_rrf_fuse"](L.ptr(keys), L.ptr(off), nl, L.ptr(w), int(rrf_k), L.ptr(out_k), L.ptr(out_s),
+                                C.byref(n)), "cm_rrf_fuse")
+    return out_k[:n.value], out_s[:n.value]
+
+
+def rrf_merge(vkeys, vdist, vn, bkeys, bscore, bn, *, w_vec: float, w_bm25: float, rrf_k: int, top_k: int):
+    """Batched HybridRetriever merge on device (host arrays in/out)."""
+    vkeys = _c(vkeys, np.int64)
+    nq = vkeys.shape[0]
+    kv = vkeys.shape[1]
+    bkeys = _c(bkeys, np.int64).reshape(nq, -1)
+    kb = bkeys.shape[1]
+    vdist = _c(vdist, np.float32).reshape(nq, kv)
+    bscore = _c(bscore, np.float64).reshape(nq, kb)
+    vn = _c(vn, np.int32)
+    bn = _c(bn, np.int32)
+    ok = np.empty((nq, top_k), np.int64)
+    of = np.empty((nq, top_k), np.float64)
+    ov = np.empty((nq, top_k), np.float32)
+    ob = np.empty((nq, top_k), np.float64)
+    ofl = np.empty((nq, top_k), np.int32)
+    on = np.empty(nq, np.int32)
+    L.check(L.fn["cm_rrf_merge"](L.ptr(vkeys), L.ptr(vdist), L.ptr(vn), kv, L.ptr(bkeys), L.ptr(bscore), L.ptr(bn), kb,
+                                 nq, float(w_vec), float(w_bm25), int(rrf_k), int(top_k), L.ptr(ok), L.ptr(of),
+                                 L.ptr(ov), L.ptr(ob), L.ptr(ofl), L.ptr(on)), "cm_rrf_merge")
+    return ok, of, ov, ob, ofl, on
+
+
+def rrf_merge_dev(vkeys, vdist, vn, bkeys, bscore, bn, *, w_vec, w_bm25, rrf_k, top_k, out=None):
+    nq, kv = vkeys.shape
+    kb = bkeys.shape[1]
+    dev = vkeys.device
+    if out is None:
+        out = (torch.empty((nq, top_k), dtype=torch.int64, device=dev),
+               torch.empty((nq, top_k), dtype=torch.float64, device=dev),
+               torch.empty((nq, top_k), dtype=torch.float32, device=dev),
+               torch.empty((nq, top_k), dtype=torch.float64, device=dev),
+               torch.empty((nq, top_k), dtype=torch.int32, device=dev),
+               torch.empty((nq,), dtype=torch.int32, device=dev))
+    L.check(L.fn["cm_rrf_merge_dev"](L.ptr(vkeys), L.ptr(vdist), L.ptr(vn), kv, L.ptr(bkeys), L.ptr(bscore),
+                                     L.ptr(bn), kb, nq, float(w_vec), float(w_bm25), int(rrf_k), int(top_k),
+                                     *[L.ptr(t) for t in out], _stream(dev.index)), "cm_rrf_merge_dev")
+    return out
+
+
+def meanpool_l2norm(hidden, mask, normalize: bool = True, out=None):
+    """hidden (B,S,D) f32/bf16/f16 device, mask (B,S) int32/int64 -> (B,D) f32 (K6)."""
+    B, S, D = hidden.shape
+    hd = {torch.float32: L.CM_DTYPE_F32, torch.bfloat16: L.CM_DTYPE_BF16, torch.float16: L.CM_DTYPE_F16}[hidden.dtype]
+    md = {torch.int32: L.CM_DTYPE_I32, torch.int64: L.CM_DTYPE_I64}[mask.dtype]
+    hidden = hidden.contiguous()
+    mask = mask.contiguous()
+    if out is None:
+        out = torch.empty((B, D), dtype=torch.float32, device=hidden.device)
+    L.check(L.fn["cm_meanpool_l2norm"](L.ptr(hidden), hd, L.ptr(mask), md, B, S, D, int(bool(normalize)),
+                                       L.ptr(out), _stream(hidden.device.index)), "cm_meanpool_l2norm")
+    return out

@@ -1,0 +1,289 @@
+"""Metadata where-filters evaluated into row bitmaps for the device kernels.
+
+Two semantics, both from the reference:
+
+* Chroma ``where`` (what ``build_where_filter``, rag/retrieval/vector_chroma.py:45-78,
+  produces): typed equality per key (bool True != int 1), ``$and``/``$or``,
+  ``$eq``/``$ne``/``$in``/``$nin``; a row lacking the key never matches.
+* BM25 ``_matches_filter`` (rag/retrieval/bm25.py:79-107): Python equality of
+  ``meta.get(f)`` for the six simple fields *whenever the key is present in
+  where, even when its value is None* (quirk Q4), ``tags: {"$contains": ...}``
+  over a ``tags`` list (returning before the simple fields are looked at), and
+  ``$and`` recursion (ignoring sibling keys).
+
+Metadata is kept column-wise (per key an int32 code array + value->code dicts)
+so a filter over N rows is a few vectorised numpy compares, and the resulting
+boolean mask is packed into the uint32 bitmap the kernels read.
+"""
+from __future__ import annotations
+
+import re
+from typing import Any, Dict, List, Mapping, Optional
+
+import numpy as np
+
+SIMPLE_FIELDS = ("course", "unit", "language", "doc_type", "author", "semester")
+_MISSING = -1
+_UNHASHABLE = -2
+
+
+def _slug_tag(t: str) -> str:
+    s = re.sub(r"[^a-z0-9]+", "_", (t or "").lower().strip())
+    return s.strip("_")
+
+
+def _parse_tags(obj) -> List[str]:
+    if not obj:
+        return []
+    vals = [str(x) for x in obj] if isinstance(obj, (list, tuple)) else str(obj).split(",")
+    return [v.strip() for v in vals if v.strip()]
+
+
+def build_where_filter(meta_like: Mapping[str, Any]) -> Optional[Dict[str, Any]]:
+    """Chroma where from CLI-style filters (vector_chroma.py:45-78)."""
+    if not meta_like:
+        return None
+    clauses: List[Dict[str, Any]] = []
+    for f in SIMPLE_FIELDS:
+        v = meta_like.get(f)
+        if v is None:
+            continue
+        if isinstance(v, str):
+            v = v.strip()
+            if not v or (f == "doc_type" and v.lower() == "other"):
+                continue
+        clauses.append({f: v})
+    for t in _parse_tags(meta_like.get("tags")):
+        slug = _slug_tag(t)
+        if slug:
+            clauses.append({f"tag_{slug}": True})
+    if not clauses:
+        return None
+    return clauses[0] if len(clauses) == 1 else {"$and": clauses}
+
+
+def pack_bits(mask: np.ndarray) -> np.ndarray:
+    """bool[n] -> uint32[ceil(n/32)], bit (r & 31) of word r >> 5 (little-endian)."""
+    n = mask.shape[0]
+    b = np.packbits(mask.astype(np.uint8), bitorder="little")
+    pad = (-b.shape[0]) % 4
+    if pad:
+        b = np.concatenate([b, np.zeros(pad, np.uint8)])
+    words = b.view("<u4").astype(np.uint32)
+    need = (n + 31) // 32
+    if words.shape[0] < need:
+        words = np.concatenate([words, np.zeros(need - words.shape[0], np.uint32)])
+    return words[:max(need, 1)] if need else np.zeros(1, np.uint32)
+
+
+def _typed(v):
+    return (type(v).__name__, v)
+
+
+class _Column:
+    __slots__ = ("py", "ty", "py_map", "ty_map")
+
+    def __init__(self, cap: int):
+        self.py = np.full(cap, _MISSING, np.int32)
+        self.ty = np.full(cap, _MISSING, np.int32)
+        self.py_map: Dict[Any, int] = {}
+        self.ty_map: Dict[Any, int] = {}
+
+    def grow(self, cap: int):
+        if cap > self.py.shape[0]:
+            for name in ("py", "ty"):
+                old = getattr(self, name)
+                new = np.full(cap, _MISSING, np.int32)
+                new[: old.shape[0]] = old
+                setattr(self, name, new)
+
+
+class MetaIndex:
+    """Row-aligned metadata with vectorised where-evaluation."""
+
+    def __init__(self):
+        self.metas: List[Optional[Mapping[str, Any]]] = []
+        self.live = np.zeros(0, bool)
+        self.cols: Dict[str, _Column] = {}
+        self.tags: Dict[Any, set] = {}
+        self._cap = 0
+
+    def __len__(self):
+        return len(self.metas)
+
+    def _ensure(self, n: int):
+        if n > self._cap:
+            cap = max(n, 2 * self._cap, 1024)
+            live = np.zeros(cap, bool)
+            live[: self.live.shape[0]] = self.live
+            self.live = live
+            for c in self.cols.values():
+                c.grow(cap)
+            self._cap = cap
+        while len(self.metas) < n:
+            self.metas.append(None)
+
+    def set(self, row: int, meta: Optional[Mapping[str, Any]]):
+        self._ensure(row + 1)
+        if self.live[row]:
+            self.remove(row)
+        self.metas[row] = meta
+        self.live[row] = True
+        for key, v in (meta or {}).items():
+            col = self.cols.get(key)
+            if col is None:
+                col = self.cols[key] = _Column(self._cap)
+            try:
+                col.py[row] = col.py_map.setdefault(v, len(col.py_map))
+                col.ty[row] = col.ty_map.setdefault(_typed(v), len(col.ty_map))
+            except TypeError:  # unhashable value: evaluated row by row
+                col.py[row] = col.ty[row] = _UNHASHABLE
+        tags = (meta or {}).get("tags")
+        if isinstance(tags, (list, tuple, set)):
+            for t in tags:
+                try:
+                    self.tags.setdefault(t, set()).add(row)
+                except TypeError:
+                    pass
+
+    def remove(self, row: int):
+        if row >= len(self.metas) or not self.live[row]:
+            return
+        meta = self.metas[row] or {}
+        for key in meta:
+            col = self.cols.get(key)
+            if col is not None:
+                col.py[row] = col.ty[row] = _MISSING
+        tags = meta.get("tags")
+        if isinstance(tags, (list, tuple, set)):
+            for t in tags:
+                try:
+                    self.tags.get(t, set()).discard(row)
+                except TypeError:
+                    pass
+        self.metas[row] = None
+        self.live[row] = False
+
+    # ---- evaluation helpers --------------------------------------------
+    def _n(self):
+        return len(self.metas)
+
+    def _slow(self, pred) -> np.ndarray:
+        return np.array([bool(self.live[r]) and pred(self.metas[r] or {}) for r in range(self._n())], bool)
+
+    def _eq_py(self, key: str, value) -> np.ndarray:
+        """rows with meta.get(key) == value (Python equality; missing key == None)."""
+        n = self._n()
+        col = self.cols.get(key)
+        if col is None:
+            m = np.ones(n, bool) if value is None else np.zeros(n, bool)
+            return m & self.live[:n]
+        codes = col.py[:n]
+        try:
+            c = col.py_map.get(value, None)
+        except TypeError:
+            return self._slow(lambda meta: meta.get(key) == value)
+        m = (codes == c) if c is not None else np.zeros(n, bool)
+        if value is None:
+            m = m | (codes == _MISSING)
+        if (codes == _UNHASHABLE).any():
+            odd = np.nonzero(codes == _UNHASHABLE)[0]
+            for r in odd:
+                m[r] = (self.metas[r] or {}).get(key) == value
+        return m & self.live[:n]
+
+    def _eq_typed(self, key: str, value) -> np.ndarray:
+        n = self._n()
+        col = self.cols.get(key)
+        if col is None:
+            return np.zeros(n, bool)
+        try:
+            c = col.ty_map.get(_typed(value), None)
+        except TypeError:
+            return np.zeros(n, bool)
+        if c is None:
+            return np.zeros(n, bool)
+        return (col.ty[:n] == c) & self.live[:n]
+
+    def _has(self, key: str) -> np.ndarray:
+        n = self._n()
+        col = self.cols.get(key)
+        if col is None:
+            return np.zeros(n, bool)
+        return (col.ty[:n] != _MISSING) & self.live[:n]
+
+    # ---- public: BM25 semantics (bm25.py:79-107) ----------------------
+    def bm25_mask(self, where: Optional[Mapping[str, Any]]) -> np.ndarray:
+        n = self._n()
+        if not where:
+            return self.live[:n].copy()
+        if "$and" in where:
+            m = self.live[:n].copy()
+            for clause in where["$and"]:
+                m &= self.bm25_mask(clause)
+            return m
+        if "tags" in where and isinstance(where["tags"], dict) and "$contains" in where["tags"]:
+            t = where["tags"]["$contains"]
+            if not t:
+                return self.live[:n].copy()
+            want = {t} if isinstance(t, str) else set(t)
+            m = self.live[:n].copy()
+            for tag in want:
+                rows = np.fromiter(self.tags.get(tag, ()), np.int64)
+                hit = np.zeros(n, bool)
+                hit[rows] = True
+                m &= hit
+            return m
+        m = self.live[:n].copy()
+        for f in SIMPLE_FIELDS:
+            if f in where:
+                m &= self._eq_py(f, where[f])
+        return m
+
+    # ---- public: Chroma semantics ---------------------------------------
+    def chroma_mask(self, where: Optional[Mapping[str, Any]]) -> np.ndarray:
+        n = self._n()
+        m = self.live[:n].copy()
+        if not where:
+            return m
+        for key, cond in where.items():
+            if key == "$and":
+                for c in cond:
+                    m &= self.chroma_mask(c)
+            elif key == "$or":
+                acc = np.zeros(n, bool)
+                for c in cond:
+                    acc |= self.chroma_mask(c)
+                m &= acc
+            elif isinstance(cond, dict):
+                if len(cond) != 1:
+                    raise ValueError(f"Expected operator expression with one operator, got {cond}")
+                (op, arg), = cond.items()
+                if op == "$eq":
+                    m &= self._eq_typed(key, arg)
+                elif op == "$ne":
+                    m &= self._has(key) & ~self._eq_typed(key, arg)
+                elif op == "$in":
+                    acc = np.zeros(n, bool)
+                    for a in arg:
+                        acc |= self._eq_typed(key, a)
+                    m &= acc
+                elif op == "$nin":
+                    acc = self._has(key)
+                    for a in arg:
+                        acc &= ~self._eq_typed(key, a)
+                    m &= acc
+                elif op in ("$gt", "$gte", "$lt", "$lte"):
+                    m &= self._slow(lambda meta, k=key, o=op, a=arg: _cmp(meta, k, o, a))
+                else:
+                    raise ValueError(f"Unsupported where operator {op}")
+            else:
+                m &= self._eq_typed(key, cond)
+        return m
+
+
+def _cmp(meta, key, op, arg) -> bool:
+    if key not in meta or not isinstance(meta[key], (int, float)) or isinstance(meta[key], bool):
+        return False
+    v = meta[key]
+    return {"$gt": v > arg, "$gte": v >= arg, "$lt": v < arg, "$lte": v <= arg}[op]

@@ -1,0 +1,938 @@
+// BM25 Okapi over HBM-resident postings (replaces BM25Store.search,
+// rag/retrieval/bm25.py:175-212, and rank_bm25.BM25Okapi it rebuilds per query).
+// See DESIGN.md §K2/K3/K7.
+//
+// Exactness contract (bit-identical fp64 scores to rank_bm25 0.2.x):
+//   contribution(q, d) = idf_q * ((tf*2.5) / (tf + K_d)),
+//   K_d = 1.5 * (0.25 + (0.75*dl_d) / avgdl)        [numpy op order, no FMA]
+//   score_d = sum over query tokens in order, duplicates included.
+// This file is compiled with -ffp-contract=off.  idf values are computed on
+// the host with glibc log() (the same libm call CPython's math.log makes),
+// including the epsilon floor whose average is summed in the reference's
+// dict (first-occurrence) order.
+//
+// Layout in HBM (per handle): CSR by term, postings sorted by doc row:
+//   term_off [V+1] i64, post_doc [P] i32, post_tf [P] u16, post_pos [P] u32
+//   (first position of the term in the doc: orders terms by first occurrence),
+//   dl [N] i32, live [ceil(N/32)] u32, idf [V] f64 (unfiltered statistics).
+//
+// Search (K2): grid = (doc ranges of R rows) x (query groups).  A workgroup
+// stages K_d for its range in LDS (fp64), then for each query of its group
+// accumulates term contributions into an LDS fp64 score tile, term by term
+// (barrier between terms keeps the reference's summation order), and selects
+// the range's top-k (score desc, row asc) over *all* candidate rows — zero
+// scores included, which reproduces the reference's zero-score padding.
+// A tournament kernel merges the sorted per-range lists.
+#include "cm_common.h"
+
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <cmath>
+#include <numeric>
+#include <vector>
+
+namespace cm {
+
+constexpr int kRange = 4096;       // docs per K2 workgroup
+constexpr int kBmThreads = 256;
+constexpr int kSlots = kRange / kBmThreads;  // 16 slots per thread
+constexpr int kQG = 8;             // queries per K2 workgroup
+
+struct PairKey {  // (k, r) lexicographic; smaller is better
+  uint64_t k;
+  uint32_t r;
+};
+__device__ inline bool pk_less(uint64_t ka, uint32_t ra, uint64_t kb, uint32_t rb) {
+  return ka < kb || (ka == kb && ra < rb);
+}
+
+// Block-wide argmin of (key,row) over kBmThreads threads. Returns in all threads.
+__device__ inline PairKey block_min_pair(uint64_t key, uint32_t row, uint64_t *sk, uint32_t *sr) {
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint64_t ok = __shfl_xor(key, o);
+    const uint32_t orr = __shfl_xor(row, o);
+    if (pk_less(ok, orr, key, row)) {
+      key = ok;
+      row = orr;
+    }
+  }
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    sk[w] = key;
+    sr[w] = row;
+  }
+  __syncthreads();
+  PairKey best{sk[0], sr[0]};
+  const int nw = blockDim.x >> 6;
+  for (int i = 1; i < nw; ++i)
+    if (pk_less(sk[i], sr[i], best.k, best.r)) best = PairKey{sk[i], sr[i]};
+  __syncthreads();
+  return best;
+}
+
+__device__ inline uint64_t score_key(double s) {
+  s = s + 0.0;  // -0.0 -> +0.0 (Python compares them equal)
+  return ~f64_order(s);  // ascending key == descending score
+}
+
+// q_idf[i] = idf[t] for known terms, 0 otherwise (unfiltered statistics).
+__global__ void bm25_qidf_kernel(const int32_t *__restrict__ q_terms, int n, const double *__restrict__ idf,
+                                 int32_t vocab, double *__restrict__ q_idf) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int32_t t = q_terms[i];
+  q_idf[i] = (t >= 0 && t < vocab) ? idf[t] : 0.0;
+}
+
+// bounds[i*(nr+1)+r] = first posting of term q_terms[i] with doc >= r*kRange.
+__global__ void bm25_bounds_kernel(const int32_t *__restrict__ q_terms, int n_terms, int32_t vocab, int nr,
+                                   const int64_t *__restrict__ term_off, const int32_t *__restrict__ post_doc,
+                                   int64_t *__restrict__ bounds) {
+  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t per = nr + 1;
+  if (gid >= (int64_t)n_terms * per) return;
+  const int i = (int)(gid / per);
+  const int r = (int)(gid - (int64_t)i * per);
+  const int32_t t = q_terms[i];
+  if (t < 0 || t >= vocab) {
+    bounds[gid] = 0;
+    return;
+  }
+  int64_t lo = term_off[t], hi = term_off[t + 1];
+  if (r == nr) {
+    bounds[gid] = hi;
+    return;
+  }
+  const int32_t target = r * kRange;
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (post_doc[mid] < target) lo = mid + 1;
+    else hi = mid;
+  }
+  bounds[gid] = lo;
+}
+
+template <typename TF>
+__global__ void __launch_bounds__(kBmThreads)
+    bm25_range_kernel(const int32_t *__restrict__ q_off, int nq, const double *__restrict__ q_idf,
+                      const int64_t *__restrict__ bounds, int nr, const int32_t *__restrict__ post_doc,
+                      const TF *__restrict__ post_tf, const int32_t *__restrict__ dl, const uint32_t *__restrict__ live,
+                      const uint32_t *__restrict__ allow, int64_t ndocs, double avgdl, int k,
+                      uint64_t *__restrict__ cand_key, uint32_t *__restrict__ cand_row) {
+  __shared__ double score[kRange];
+  __shared__ double kd[kRange];
+  __shared__ uint32_t okbits[kRange / 32];
+  __shared__ uint64_t sk[4];
+  __shared__ uint32_t sr[4];
+  const int r = blockIdx.x;
+  const int64_t d0 = (int64_t)r * kRange;
+  const int tid = threadIdx.x;
+  for (int s = tid; s < kRange; s += kBmThreads) {
+    const int64_t d = d0 + s;
+    double v = 0.0;
+    if (d < ndocs) {
+      double t = 0.75 * (double)dl[d];
+      t = t / avgdl;
+      t = 0.25 + t;
+      v = 1.5 * t;
+    }
+    kd[s] = v;
+  }
+  for (int w = tid; w < kRange / 32; w += kBmThreads) {
+    const int64_t gw = d0 / 32 + w;
+    uint32_t b = 0;
+    if (gw * 32 < ndocs) {
+      b = live[gw] & (allow ? allow[gw] : 0xffffffffu);
+      const int64_t rem = ndocs - gw * 32;
+      if (rem < 32) b &= (1u << rem) - 1u;
+    }
+    okbits[w] = b;
+  }
+  const int q_begin = blockIdx.y * kQG;
+  const int q_end = min(q_begin + kQG, nq);
+  for (int qi = q_begin; qi < q_end; ++qi) {
+    for (int s = tid; s < kRange; s += kBmThreads) score[s] = 0.0;
+    __syncthreads();
+    const int t0 = q_off[qi], t1 = q_off[qi + 1];
+    for (int i = t0; i < t1; ++i) {  // query tokens in order (duplicates twice)
+      const double idf = q_idf[i];
+      const int64_t lo = bounds[(int64_t)i * (nr + 1) + r];
+      const int64_t hi = bounds[(int64_t)i * (nr + 1) + r + 1];
+      for (int64_t p = lo + tid; p < hi; p += kBmThreads) {
+        const int s = post_doc[p] - (int32_t)d0;
+        const double tf = (double)post_tf[p];
+        const double num = tf * 2.5;
+        const double den = tf + kd[s];
+        const double c = idf * (num / den);
+        score[s] = score[s] + c;
+      }
+      __syncthreads();
+    }
+    // top-k of this range: (score desc, row asc) over candidate rows.
+    uint32_t taken = 0;
+    const uint32_t myw = okbits[(tid * kSlots) >> 5] >> ((tid * kSlots) & 31);
+    auto local_best = [&](uint64_t &bk, uint32_t &br) {
+      bk = kEmptyKey;
+      br = 0xffffffffu;
+#pragma unroll
+      for (int u = 0; u < kSlots; ++u) {
+        if (((myw >> u) & 1u) && !((taken >> u) & 1u)) {
+          const uint64_t key = score_key(score[tid * kSlots + u]);
+          if (key < bk) {  // rows ascending within the thread: first wins ties
+            bk = key;
+            br = (uint32_t)(d0 + tid * kSlots + u);
+          }
+        }
+      }
+    };
+    uint64_t bk;
+    uint32_t br;
+    local_best(bk, br);
+    for (int i = 0; i < k; ++i) {
+      const PairKey best = block_min_pair(bk, br, sk, sr);
+      if (tid == 0) {
+        const int64_t o = ((int64_t)qi * nr + r) * k + i;
+        cand_key[o] = best.k;
+        cand_row[o] = best.r;
+      }
+      if (best.r != 0xffffffffu && br == best.r && bk == best.k) {
+        taken |= 1u << (best.r - (uint32_t)d0 - tid * kSlots);
+        local_best(bk, br);
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// Tournament merge of nr sorted per-range lists per query.
+__global__ void __launch_bounds__(kBmThreads) bm25_merge_kernel(const uint64_t *__restrict__ cand_key,
+                                                                const uint32_t *__restrict__ cand_row, int nr, int k,
+                                                                double *__restrict__ out_score,
+                                                                int64_t *__restrict__ out_row) {
+  const int qi = blockIdx.x;
+  __shared__ uint64_t sk[4];
+  __shared__ uint32_t sr[4];
+  constexpr int kPer = 16;  // nr <= 4096 lists
+  int head[kPer];
+  uint64_t hk[kPer];
+  uint32_t hr[kPer];
+  const int64_t base = (int64_t)qi * nr * k;
+#pragma unroll
+  for (int s = 0; s < kPer; ++s) {
+    const int l = threadIdx.x + kBmThreads * s;
+    head[s] = 0;
+    hk[s] = kEmptyKey;
+    hr[s] = 0xffffffffu;
+    if (l < nr) {
+      hk[s] = cand_key[base + (int64_t)l * k];
+      hr[s] = cand_row[base + (int64_t)l * k];
+    }
+  }
+  for (int i = 0; i < k; ++i) {
+    uint64_t mk = kEmptyKey;
+    uint32_t mr = 0xffffffffu;
+#pragma unroll
+    for (int s = 0; s < kPer; ++s)
+      if (pk_less(hk[s], hr[s], mk, mr)) {
+        mk = hk[s];
+        mr = hr[s];
+      }
+    const PairKey best = block_min_pair(mk, mr, sk, sr);
+    if (threadIdx.x == 0) {
+      const int64_t o = (int64_t)qi * k + i;
+      if (best.r == 0xffffffffu) {
+        out_score[o] = 0.0;
+        out_row[o] = -1;
+      } else {
+        out_score[o] = f64_unorder(~best.k);
+        out_row[o] = (int64_t)best.r;
+      }
+    }
+    if (best.r == 0xffffffffu) continue;
+#pragma unroll
+    for (int s = 0; s < kPer; ++s) {
+      if (hr[s] == best.r && hk[s] == best.k) {
+        const int l = threadIdx.x + kBmThreads * s;
+        head[s] += 1;
+        if (head[s] < k) {
+          hk[s] = cand_key[base + (int64_t)l * k + head[s]];
+          hr[s] = cand_row[base + (int64_t)l * k + head[s]];
+        } else {
+          hk[s] = kEmptyKey;
+          hr[s] = 0xffffffffu;
+        }
+      }
+    }
+  }
+}
+
+// Filtered statistics: number of candidate docs and their total length.
+__global__ void bm25_filtered_stats_kernel(const int32_t *__restrict__ dl, const uint32_t *__restrict__ live,
+                                           const uint32_t *__restrict__ allow, int64_t ndocs,
+                                           unsigned long long *__restrict__ out /* [2] */) {
+  unsigned long long cnt = 0, sum = 0;
+  const int64_t nw = ceil_div(ndocs, 32);
+  for (int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; w < nw; w += (int64_t)gridDim.x * blockDim.x) {
+    uint32_t b = live[w] & allow[w];
+    while (b) {
+      const int bit = __builtin_ctz(b);
+      b &= b - 1;
+      const int64_t d = w * 32 + bit;
+      if (d < ndocs) {
+        cnt += 1;
+        sum += (unsigned long long)dl[d];
+      }
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    cnt += __shfl_xor(cnt, o);
+    sum += __shfl_xor(sum, o);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    if (cnt) atomicAdd(&out[0], cnt);
+    if (sum) atomicAdd(&out[1], sum);
+  }
+}
+
+// Per listed term: number of candidate postings and the first candidate
+// posting's (doc << 32 | first position) key (terms' dict order).
+__global__ void __launch_bounds__(256) bm25_term_df_kernel(const int32_t *__restrict__ terms, int n_terms,
+                                                           const int64_t *__restrict__ term_off,
+                                                           const int32_t *__restrict__ post_doc,
+                                                           const uint32_t *__restrict__ post_pos,
+                                                           const uint32_t *__restrict__ live,
+                                                           const uint32_t *__restrict__ allow,
+                                                           int64_t *__restrict__ out_df, uint64_t *__restrict__ out_first) {
+  const int i = blockIdx.x;
+  if (i >= n_terms) return;
+  const int32_t t = terms ? terms[i] : i;
+  __shared__ unsigned long long red_c[4];
+  __shared__ unsigned long long red_m[4];
+  unsigned long long c = 0, m = ~0ull;
+  const int64_t lo = term_off[t], hi = term_off[t + 1];
+  for (int64_t p = lo + threadIdx.x; p < hi; p += 256) {
+    const int32_t d = post_doc[p];
+    if ((live[d >> 5] & allow[d >> 5]) >> (d & 31) & 1u) {
+      c += 1;
+      const unsigned long long key = ((unsigned long long)(uint32_t)d << 32) | post_pos[p];
+      m = key < m ? key : m;
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    c += __shfl_xor(c, o);
+    const unsigned long long om = __shfl_xor(m, o);
+    m = om < m ? om : m;
+  }
+  if ((threadIdx.x & 63) == 0) {
+    red_c[threadIdx.x >> 6] = c;
+    red_m[threadIdx.x >> 6] = m;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long cc = 0, mm = ~0ull;
+    for (int w = 0; w < 4; ++w) {
+      cc += red_c[w];
+      mm = red_m[w] < mm ? red_m[w] : mm;
+    }
+    out_df[i] = (int64_t)cc;
+    if (out_first) out_first[i] = mm;
+  }
+}
+
+// ---------------- K7: device CSR build (radix sort by (term, doc)) ----------------
+__global__ void bm25_token_keys_kernel(const int32_t *__restrict__ term_ids, const int64_t *__restrict__ doc_off,
+                                       int64_t ndocs, uint64_t *__restrict__ keys, uint32_t *__restrict__ pos,
+                                       int32_t *__restrict__ dl, int32_t *__restrict__ bad) {
+  const int64_t d = (int64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+  if (d >= ndocs) return;
+  const int lane = threadIdx.x & 63;
+  const int64_t b = doc_off[d], e = doc_off[d + 1];
+  if (lane == 0) dl[d] = (int32_t)(e - b);
+  for (int64_t p = b + lane; p < e; p += 64) {
+    const int32_t t = term_ids[p];
+    if (t < 0) atomicOr(bad, 1);
+    keys[p] = ((uint64_t)(uint32_t)t << 32) | (uint64_t)(uint32_t)d;
+    pos[p] = (uint32_t)(p - b);
+  }
+}
+
+__global__ void bm25_postings_from_runs_kernel(const uint64_t *__restrict__ ukeys, const int32_t *__restrict__ counts,
+                                               const int64_t *__restrict__ run_start,
+                                               const uint32_t *__restrict__ sorted_pos, int64_t nruns,
+                                               int32_t *__restrict__ post_doc, uint16_t *__restrict__ post_tf,
+                                               uint32_t *__restrict__ post_pos, int32_t *__restrict__ df,
+                                               int32_t *__restrict__ tf_overflow) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nruns) return;
+  const uint64_t key = ukeys[i];
+  const int32_t t = (int32_t)(key >> 32);
+  post_doc[i] = (int32_t)(uint32_t)key;
+  const int32_t c = counts[i];
+  if (c > 65535) atomicOr(tf_overflow, 1);
+  post_tf[i] = (uint16_t)min(c, 65535);
+  post_pos[i] = sorted_pos[run_start[i]];
+  atomicAdd(&df[t], 1);
+}
+
+__global__ void set_all_bits_kernel(uint32_t *bits, int64_t n) {
+  const int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t nw = ceil_div(n, 32);
+  if (w >= nw) return;
+  const int64_t rem = n - w * 32;
+  bits[w] = rem >= 32 ? 0xffffffffu : ((1u << rem) - 1u);
+}
+
+__global__ void first_key_kernel(const int64_t *__restrict__ term_off, const int32_t *__restrict__ post_doc,
+                                 const uint32_t *__restrict__ post_pos, int32_t vocab,
+                                 uint64_t *__restrict__ first) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= vocab) return;
+  const int64_t p = term_off[t];
+  first[t] = p < term_off[t + 1] ? (((uint64_t)(uint32_t)post_doc[p] << 32) | post_pos[p]) : ~0ull;
+}
+
+}  // namespace cm
+
+using namespace cm;
+
+struct cm_bm25 {
+  int dev = 0;
+  hipStream_t stream = nullptr;
+  int64_t ndocs = 0, npost = 0;
+  int32_t vocab = 0;
+  int64_t n_live = 0, sum_len = 0;
+  double avgdl = 0.0, eps = 0.0;
+  bool empty_vocab = false;  // live docs exist but no tokens (ZeroDivisionError on search)
+  DevBuf term_off, post_doc, post_tf, post_pos, dl, live, idf;
+  std::vector<double> idf_host;
+  DevBuf ws, qbuf, obuf, allow_buf, tmp;
+};
+
+namespace {
+
+// rank_bm25 idf for one term over a candidate set of n docs.
+inline double bm25_idf(int64_t n, int64_t df) {
+  return std::log((double)(n - df) + 0.5) - std::log((double)df + 0.5);
+}
+
+// Unfiltered statistics from df and the terms' first-occurrence order.
+int compute_idf_table(cm_bm25 *h, const std::vector<int32_t> &df, const std::vector<int32_t> &order) {
+  h->idf_host.assign(h->vocab, 0.0);
+  h->empty_vocab = false;
+  h->eps = 0.0;
+  h->avgdl = h->n_live ? (double)h->sum_len / (double)h->n_live : 0.0;
+  if (h->n_live == 0) return CM_OK;
+  if (order.empty()) {
+    h->empty_vocab = true;
+    return CM_OK;
+  }
+  double idf_sum = 0.0;
+  for (int32_t t : order) {
+    const double v = bm25_idf(h->n_live, df[t]);
+    h->idf_host[t] = v;
+    idf_sum = idf_sum + v;
+  }
+  const double avg = idf_sum / (double)order.size();
+  h->eps = 0.25 * avg;
+  for (int32_t t : order)
+    if (h->idf_host[t] < 0) h->idf_host[t] = h->eps;
+  int rc = h->idf.ensure((size_t)std::max(h->vocab, 1) * 8);
+  if (rc) return rc;
+  CM_HIP(hipMemcpyAsync(h->idf.ptr, h->idf_host.data(), (size_t)h->vocab * 8, hipMemcpyHostToDevice, h->stream));
+  return CM_OK;
+}
+
+struct BmWs {
+  double *q_idf;
+  int64_t *bounds;
+  uint64_t *cand_key;
+  uint32_t *cand_row;
+  size_t total;
+};
+
+BmWs bm_ws_layout(const cm_bm25 *h, int nq, int total_terms, int k, void *base) {
+  BmWs w{};
+  char *p = reinterpret_cast<char *>(base);
+  const int64_t nr = std::max<int64_t>(1, ceil_div(h->ndocs, kRange));
+  size_t off = 0;
+  w.q_idf = reinterpret_cast<double *>(p + off);
+  off += round_up((int64_t)std::max(total_terms, 1) * 8, 256);
+  w.bounds = reinterpret_cast<int64_t *>(p + off);
+  off += round_up((int64_t)std::max(total_terms, 1) * (nr + 1) * 8, 256);
+  w.cand_key = reinterpret_cast<uint64_t *>(p + off);
+  off += round_up((int64_t)nq * nr * k * 8, 256);
+  w.cand_row = reinterpret_cast<uint32_t *>(p + off);
+  off += round_up((int64_t)nq * nr * k * 4, 256);
+  w.total = off;
+  return w;
+}
+
+// Launch K2 + merge given q_idf already in the workspace.
+int bm25_launch_core(cm_bm25 *h, const int32_t *q_terms_dev, const int32_t *q_off_dev, int nq, int total_terms, int k,
+                     const uint32_t *allow_dev, double avgdl, const BmWs &w, double *score_dev, int64_t *row_dev,
+                     hipStream_t st) {
+  const int nr = (int)std::max<int64_t>(1, ceil_div(h->ndocs, kRange));
+  if (nr > 16 * kBmThreads) CM_FAIL(CM_EUNSUPPORTED, "BM25 corpus too large for one shard (> 16.7M docs)");
+  const int64_t nb = (int64_t)total_terms * (nr + 1);
+  if (nb > 0) {
+    hipLaunchKernelGGL(bm25_bounds_kernel, dim3((unsigned)ceil_div(nb, 256)), dim3(256), 0, st, q_terms_dev,
+                       total_terms, h->vocab, nr, h->term_off.as<int64_t>(), h->post_doc.as<int32_t>(), w.bounds);
+    CM_HIP(hipGetLastError());
+  }
+  dim3 grid(nr, (unsigned)ceil_div(nq, kQG));
+  hipLaunchKernelGGL(bm25_range_kernel<uint16_t>, grid, dim3(kBmThreads), 0, st, q_off_dev, nq, w.q_idf, w.bounds,
+                     nr, h->post_doc.as<int32_t>(), h->post_tf.as<uint16_t>(), h->dl.as<int32_t>(),
+                     h->live.as<uint32_t>(), allow_dev, h->ndocs, avgdl, k, w.cand_key, w.cand_row);
+  CM_HIP(hipGetLastError());
+  hipLaunchKernelGGL(bm25_merge_kernel, dim3(nq), dim3(kBmThreads), 0, st, w.cand_key, w.cand_row, nr, k,
+                     score_dev, row_dev);
+  CM_HIP(hipGetLastError());
+  return CM_OK;
+}
+
+void bm25_free(cm_bm25 *h) {
+  for (DevBuf *b : {&h->term_off, &h->post_doc, &h->post_tf, &h->post_pos, &h->dl, &h->live, &h->idf, &h->ws,
+                    &h->qbuf, &h->obuf, &h->allow_buf, &h->tmp})
+    b->release();
+}
+
+}  // namespace
+
+extern "C" {
+
+int cm_bm25_create(int device, cm_bm25 **out) {
+  if (!out) CM_FAIL(CM_EINVAL, "out is NULL");
+  *out = nullptr;
+  DeviceGuard dg(device);
+  if (!dg.ok) CM_FAIL(CM_EDEVICE, "cannot select device " + std::to_string(device));
+  cm_bm25 *h = new cm_bm25();
+  h->dev = device;
+  if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete h;
+    CM_FAIL(CM_EDEVICE, "hipStreamCreate failed");
+  }
+  *out = h;
+  return CM_OK;
+}
+
+void cm_bm25_destroy(cm_bm25 *h) {
+  if (!h) return;
+  DeviceGuard dg(h->dev);
+  if (h->stream) (void)hipStreamSynchronize(h->stream);
+  bm25_free(h);
+  if (h->stream) (void)hipStreamDestroy(h->stream);
+  delete h;
+}
+
+int64_t cm_bm25_num_docs(cm_bm25 *h) { return h ? h->ndocs : -1; }
+int64_t cm_bm25_num_postings(cm_bm25 *h) { return h ? h->npost : -1; }
+
+int cm_bm25_stats(cm_bm25 *h, int64_t *n_live, int64_t *sum_len, double *avgdl, double *eps) {
+  if (!h) CM_FAIL(CM_EINVAL, "null handle");
+  if (n_live) *n_live = h->n_live;
+  if (sum_len) *sum_len = h->sum_len;
+  if (avgdl) *avgdl = h->avgdl;
+  if (eps) *eps = h->eps;
+  return CM_OK;
+}
+
+int cm_bm25_build(cm_bm25 *h, const int32_t *term_ids, const int64_t *doc_off, int64_t ndocs, int32_t vocab,
+                  const uint8_t *live) {
+  if (!h) CM_FAIL(CM_EINVAL, "null handle");
+  if (ndocs < 0 || vocab < 0 || (ndocs > 0 && !doc_off)) CM_FAIL(CM_EINVAL, "bad arguments");
+  if (ndocs >= (int64_t)INT32_MAX) CM_FAIL(CM_EINVAL, "too many docs for one shard");
+  DeviceGuard dg(h->dev);
+  const int64_t ntok = ndocs ? doc_off[ndocs] : 0;
+  if (ntok > 0 && !term_ids) CM_FAIL(CM_EINVAL, "term_ids is NULL");
+  for (int64_t d = 0; d < ndocs; ++d)
+    if (doc_off[d + 1] < doc_off[d]) CM_FAIL(CM_EINVAL, "doc_off must be non-decreasing");
+  for (int64_t p = 0; p < ntok; ++p)
+    if (term_ids[p] < 0 || term_ids[p] >= vocab) CM_FAIL(CM_EINVAL, "term id out of range");
+  // pass 1: df over live docs, first-occurrence order, lengths
+  std::vector<int64_t> stamp((size_t)vocab, -1);
+  std::vector<int32_t> df((size_t)vocab, 0), order;
+  std::vector<int32_t> dlh((size_t)ndocs, 0);
+  int64_t n_live = 0, sum_len = 0, npost = 0;
+  for (int64_t d = 0; d < ndocs; ++d) {
+    const int64_t b = doc_off[d], e = doc_off[d + 1];
+    dlh[d] = (int32_t)(e - b);
+    if (live && !live[d]) continue;
+    n_live++;
+    sum_len += e - b;
+    for (int64_t p = b; p < e; ++p) {
+      const int32_t t = term_ids[p];
+      if (stamp[t] != d) {
+        stamp[t] = d;
+        if (df[t]++ == 0) order.push_back(t);
+        npost++;
+      }
+    }
+  }
+  // pass 2: postings (sorted by doc within a term because docs are visited in order)
+  std::vector<int64_t> toff((size_t)vocab + 1, 0);
+  for (int32_t t = 0; t < vocab; ++t) toff[t + 1] = toff[t] + df[t];
+  std::vector<int64_t> fill(toff.begin(), toff.end() - 1);
+  std::vector<int32_t> pdoc((size_t)npost);
+  std::vector<uint16_t> ptf((size_t)npost);
+  std::vector<uint32_t> ppos((size_t)npost);
+  std::vector<int32_t> tfc((size_t)vocab, 0);
+  std::fill(stamp.begin(), stamp.end(), -1);
+  std::vector<int32_t> distinct;
+  std::vector<uint32_t> firstpos((size_t)vocab, 0);
+  for (int64_t d = 0; d < ndocs; ++d) {
+    if (live && !live[d]) continue;
+    distinct.clear();
+    const int64_t b = doc_off[d], e = doc_off[d + 1];
+    for (int64_t p = b; p < e; ++p) {
+      const int32_t t = term_ids[p];
+      if (stamp[t] != d) {
+        stamp[t] = d;
+        tfc[t] = 0;
+        firstpos[t] = (uint32_t)(p - b);
+        distinct.push_back(t);
+      }
+      tfc[t]++;
+    }
+    for (int32_t t : distinct) {
+      if (tfc[t] > 65535) CM_FAIL(CM_EUNSUPPORTED, "term frequency > 65535 in one chunk");
+      const int64_t q = fill[t]++;
+      pdoc[q] = (int32_t)d;
+      ptf[q] = (uint16_t)tfc[t];
+      ppos[q] = firstpos[t];
+    }
+  }
+  // live bitmap
+  const int64_t nw = std::max<int64_t>(1, ceil_div(ndocs, 32));
+  std::vector<uint32_t> lb((size_t)nw, 0);
+  for (int64_t d = 0; d < ndocs; ++d)
+    if (!live || live[d]) lb[d >> 5] |= 1u << (d & 31);
+  int rc;
+  if ((rc = h->term_off.ensure(((size_t)vocab + 1) * 8)) || (rc = h->post_doc.ensure(std::max<int64_t>(npost, 1) * 4)) ||
+      (rc = h->post_tf.ensure(std::max<int64_t>(npost, 1) * 2)) ||
+      (rc = h->post_pos.ensure(std::max<int64_t>(npost, 1) * 4)) ||
+      (rc = h->dl.ensure(std::max<int64_t>(ndocs, 1) * 4)) || (rc = h->live.ensure((size_t)nw * 4)))
+    return rc;
+  CM_HIP(hipMemcpyAsync(h->term_off.ptr, toff.data(), toff.size() * 8, hipMemcpyHostToDevice, h->stream));
+  if (npost) {
+    CM_HIP(hipMemcpyAsync(h->post_doc.ptr, pdoc.data(), (size_t)npost * 4, hipMemcpyHostToDevice, h->stream));
+    CM_HIP(hipMemcpyAsync(h->post_tf.ptr, ptf.data(), (size_t)npost * 2, hipMemcpyHostToDevice, h->stream));
+    CM_HIP(hipMemcpyAsync(h->post_pos.ptr, ppos.data(), (size_t)npost * 4, hipMemcpyHostToDevice, h->stream));
+  }
+  if (ndocs) CM_HIP(hipMemcpyAsync(h->dl.ptr, dlh.data(), (size_t)ndocs * 4, hipMemcpyHostToDevice, h->stream));
+  CM_HIP(hipMemcpyAsync(h->live.ptr, lb.data(), (size_t)nw * 4, hipMemcpyHostToDevice, h->stream));
+  h->ndocs = ndocs;
+  h->npost = npost;
+  h->vocab = vocab;
+  h->n_live = n_live;
+  h->sum_len = sum_len;
+  if ((rc = compute_idf_table(h, df, order))) return rc;
+  CM_HIP(hipStreamSynchronize(h->stream));
+  if (h->empty_vocab) CM_FAIL(CM_EZERODIV, "float division by zero (every live document has an empty token list)");
+  return CM_OK;
+}
+
+int cm_bm25_build_dev(cm_bm25 *h, const int32_t *term_ids_dev, const int64_t *doc_off_dev, int64_t ndocs,
+                      int64_t ntokens, int32_t vocab, void *stream) {
+  if (!h) CM_FAIL(CM_EINVAL, "null handle");
+  if (ndocs <= 0 || ntokens < 0 || vocab <= 0) CM_FAIL(CM_EINVAL, "bad arguments");
+  if (ndocs >= (int64_t)INT32_MAX) CM_FAIL(CM_EINVAL, "too many docs for one shard");
+  DeviceGuard dg(h->dev);
+  hipStream_t st = stream ? (hipStream_t)stream : h->stream;
+  int rc;
+  // scratch: keys in/out (u64), pos in/out (u32), flags
+  DevBuf keys_a, keys_b, pos_a, pos_b, ukeys, counts, runstart, nruns_d, flags, df_d, cub_tmp, firstk;
+  auto cleanup = [&]() {
+    for (DevBuf *b : {&keys_a, &keys_b, &pos_a, &pos_b, &ukeys, &counts, &runstart, &nruns_d, &flags, &df_d, &cub_tmp,
+                      &firstk})
+      b->release();
+  };
+  const size_t nt = (size_t)std::max<int64_t>(ntokens, 1);
+  if ((rc = keys_a.ensure(nt * 8)) || (rc = keys_b.ensure(nt * 8)) || (rc = pos_a.ensure(nt * 4)) ||
+      (rc = pos_b.ensure(nt * 4)) || (rc = flags.ensure(16)) || (rc = h->dl.ensure((size_t)ndocs * 4))) {
+    cleanup();
+    return rc;
+  }
+  CM_HIP(hipMemsetAsync(flags.ptr, 0, 16, st));
+  hipLaunchKernelGGL(bm25_token_keys_kernel, dim3((unsigned)ceil_div(ndocs, 4)), dim3(256), 0, st, term_ids_dev,
+                     doc_off_dev, ndocs, keys_a.as<uint64_t>(), pos_a.as<uint32_t>(), h->dl.as<int32_t>(),
+                     flags.as<int32_t>());
+  CM_HIP(hipGetLastError());
+  int tbits = 1;
+  while ((1ll << tbits) < (int64_t)vocab) ++tbits;
+  hipcub::DoubleBuffer<uint64_t> kbuf(keys_a.as<uint64_t>(), keys_b.as<uint64_t>());
+  hipcub::DoubleBuffer<uint32_t> vbuf(pos_a.as<uint32_t>(), pos_b.as<uint32_t>());
+  size_t tmp_bytes = 0;
+  CM_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, kbuf, vbuf, ntokens, 0, 32 + tbits, st));
+  if ((rc = cub_tmp.ensure(tmp_bytes))) {
+    cleanup();
+    return rc;
+  }
+  CM_HIP(hipcub::DeviceRadixSort::SortPairs(cub_tmp.ptr, tmp_bytes, kbuf, vbuf, ntokens, 0, 32 + tbits, st));
+  uint64_t *sk = kbuf.Current();
+  uint32_t *sp = vbuf.Current();
+  // runs of equal (term, doc): unique keys + counts; reuse the free buffers
+  uint64_t *uk = kbuf.Alternate();
+  int32_t *cnt = reinterpret_cast<int32_t *>(vbuf.Alternate());
+  if ((rc = nruns_d.ensure(8))) {
+    cleanup();
+    return rc;
+  }
+  size_t tmp2 = 0;
+  CM_HIP(hipcub::DeviceRunLengthEncode::Encode(nullptr, tmp2, sk, uk, cnt, nruns_d.as<int64_t>(), ntokens, st));
+  if (tmp2 > cub_tmp.bytes) {
+    cub_tmp.release();
+    if ((rc = cub_tmp.ensure(tmp2))) {
+      cleanup();
+      return rc;
+    }
+  }
+  CM_HIP(hipcub::DeviceRunLengthEncode::Encode(cub_tmp.ptr, tmp2, sk, uk, cnt, nruns_d.as<int64_t>(), ntokens, st));
+  int64_t nruns = 0;
+  int32_t hflags[2] = {0, 0};
+  CM_HIP(hipMemcpyAsync(&nruns, nruns_d.ptr, 8, hipMemcpyDeviceToHost, st));
+  CM_HIP(hipMemcpyAsync(hflags, flags.ptr, 8, hipMemcpyDeviceToHost, st));
+  CM_HIP(hipStreamSynchronize(st));
+  if (hflags[0]) {
+    cleanup();
+    CM_FAIL(CM_EINVAL, "term id out of range");
+  }
+  if ((rc = runstart.ensure((size_t)std::max<int64_t>(nruns, 1) * 8))) {
+    cleanup();
+    return rc;
+  }
+  // run_start = exclusive scan of counts (as int64)
+  {
+    size_t tmp3 = 0;
+    auto in = hipcub::TransformInputIterator<int64_t, hipcub::CastOp<int64_t>, int32_t *>(cnt, hipcub::CastOp<int64_t>());
+    CM_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp3, in, runstart.as<int64_t>(), nruns, st));
+    if (tmp3 > cub_tmp.bytes) {
+      cub_tmp.release();
+      if ((rc = cub_tmp.ensure(tmp3))) {
+        cleanup();
+        return rc;
+      }
+    }
+    CM_HIP(hipcub::DeviceScan::ExclusiveSum(cub_tmp.ptr, tmp3, in, runstart.as<int64_t>(), nruns, st));
+  }
+  if ((rc = h->post_doc.ensure((size_t)std::max<int64_t>(nruns, 1) * 4)) ||
+      (rc = h->post_tf.ensure((size_t)std::max<int64_t>(nruns, 1) * 2)) ||
+      (rc = h->post_pos.ensure((size_t)std::max<int64_t>(nruns, 1) * 4)) ||
+      (rc = df_d.ensure((size_t)vocab * 4)) || (rc = h->term_off.ensure(((size_t)vocab + 1) * 8))) {
+    cleanup();
+    return rc;
+  }
+  CM_HIP(hipMemsetAsync(df_d.ptr, 0, (size_t)vocab * 4, st));
+  hipLaunchKernelGGL(bm25_postings_from_runs_kernel, dim3((unsigned)ceil_div(std::max<int64_t>(nruns, 1), 256)),
+                     dim3(256), 0, st, uk, cnt, runstart.as<int64_t>(), sp, nruns, h->post_doc.as<int32_t>(),
+                     h->post_tf.as<uint16_t>(), h->post_pos.as<uint32_t>(), df_d.as<int32_t>(),
+                     flags.as<int32_t>() + 1);
+  CM_HIP(hipGetLastError());
+  // term_off = exclusive scan of df (int64), last = nruns
+  {
+    size_t tmp3 = 0;
+    auto in = hipcub::TransformInputIterator<int64_t, hipcub::CastOp<int64_t>, int32_t *>(df_d.as<int32_t>(),
+                                                                                          hipcub::CastOp<int64_t>());
+    CM_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp3, in, h->term_off.as<int64_t>(), vocab, st));
+    if (tmp3 > cub_tmp.bytes) {
+      cub_tmp.release();
+      if ((rc = cub_tmp.ensure(tmp3))) {
+        cleanup();
+        return rc;
+      }
+    }
+    CM_HIP(hipcub::DeviceScan::ExclusiveSum(cub_tmp.ptr, tmp3, in, h->term_off.as<int64_t>(), vocab, st));
+    CM_HIP(hipMemcpyAsync(h->term_off.as<int64_t>() + vocab, &nruns, 8, hipMemcpyHostToDevice, st));
+  }
+  const int64_t nw = std::max<int64_t>(1, ceil_div(ndocs, 32));
+  if ((rc = h->live.ensure((size_t)nw * 4)) || (rc = firstk.ensure((size_t)vocab * 8))) {
+    cleanup();
+    return rc;
+  }
+  hipLaunchKernelGGL(set_all_bits_kernel, dim3((unsigned)ceil_div(nw, 256)), dim3(256), 0, st, h->live.as<uint32_t>(),
+                     ndocs);
+  hipLaunchKernelGGL(first_key_kernel, dim3((unsigned)ceil_div(vocab, 256)), dim3(256), 0, st,
+                     h->term_off.as<int64_t>(), h->post_doc.as<int32_t>(), h->post_pos.as<uint32_t>(), vocab,
+                     firstk.as<uint64_t>());
+  CM_HIP(hipGetLastError());
+  std::vector<int32_t> df((size_t)vocab);
+  std::vector<uint64_t> fk((size_t)vocab);
+  CM_HIP(hipMemcpyAsync(df.data(), df_d.ptr, (size_t)vocab * 4, hipMemcpyDeviceToHost, st));
+  CM_HIP(hipMemcpyAsync(fk.data(), firstk.ptr, (size_t)vocab * 8, hipMemcpyDeviceToHost, st));
+  CM_HIP(hipMemcpyAsync(hflags, flags.ptr, 8, hipMemcpyDeviceToHost, st));
+  CM_HIP(hipStreamSynchronize(st));
+  cleanup();
+  if (hflags[1]) CM_FAIL(CM_EUNSUPPORTED, "term frequency > 65535 in one chunk");
+  std::vector<int32_t> order;
+  order.reserve((size_t)vocab);
+  for (int32_t t = 0; t < vocab; ++t)
+    if (df[t] > 0) order.push_back(t);
+  std::sort(order.begin(), order.end(), [&](int32_t a, int32_t b) { return fk[a] < fk[b]; });
+  h->ndocs = ndocs;
+  h->npost = nruns;
+  h->vocab = vocab;
+  h->n_live = ndocs;
+  h->sum_len = ntokens;
+  if ((rc = compute_idf_table(h, df, order))) return rc;
+  CM_HIP(hipStreamSynchronize(h->stream));
+  if (h->empty_vocab) CM_FAIL(CM_EZERODIV, "float division by zero (every live document has an empty token list)");
+  return CM_OK;
+}
+
+int64_t cm_bm25_search_workspace(cm_bm25 *h, int32_t nq, int32_t total_terms, int32_t k) {
+  if (!h || nq < 0 || total_terms < 0 || k <= 0) return -1;
+  return (int64_t)bm_ws_layout(h, nq, total_terms, k, nullptr).total;
+}
+
+int cm_bm25_search_dev(cm_bm25 *h, const int32_t *q_terms_dev, const int32_t *q_off_dev, int32_t nq,
+                       int32_t total_terms, int32_t k, double *score_dev, int64_t *row_dev, void *workspace_dev,
+                       int64_t workspace_bytes, void *stream) {
+  if (!h) CM_FAIL(CM_EINVAL, "null handle");
+  if (nq <= 0) return CM_OK;
+  if (k <= 0 || k > kMaxTopK) CM_FAIL(CM_EINVAL, "k must be in [1, " + std::to_string(kMaxTopK) + "]");
+  if (h->ndocs == 0) CM_FAIL(CM_EINVAL, "empty BM25 index");
+  if (h->empty_vocab) CM_FAIL(CM_EZERODIV, "float division by zero");
+  DeviceGuard dg(h->dev);
+  hipStream_t st = stream ? (hipStream_t)stream : h->stream;
+  BmWs w = bm_ws_layout(h, nq, total_terms, k, workspace_dev);
+  if (!workspace_dev || (int64_t)w.total > workspace_bytes) CM_FAIL(CM_EINVAL, "bm25 workspace too small");
+  if (total_terms > 0) {
+    hipLaunchKernelGGL(bm25_qidf_kernel, dim3((unsigned)ceil_div(total_terms, 256)), dim3(256), 0, st, q_terms_dev,
+                       total_terms, h->idf.as<double>(), h->vocab, w.q_idf);
+    CM_HIP(hipGetLastError());
+  }
+  return bm25_launch_core(h, q_terms_dev, q_off_dev, nq, total_terms, k, nullptr, h->avgdl, w, score_dev, row_dev,
+                          st);
+}
+
+int cm_bm25_search(cm_bm25 *h, const int32_t *q_terms, const int32_t *q_off, int32_t nq, int32_t k,
+                   const uint32_t *allow_bits, double *out_score, int64_t *out_row, int32_t *out_n) {
+  if (!h) CM_FAIL(CM_EINVAL, "null handle");
+  if (nq <= 0) return CM_OK;
+  if (!q_off || !out_score || !out_row) CM_FAIL(CM_EINVAL, "NULL argument");
+  if (k <= 0 || k > kMaxTopK) CM_FAIL(CM_EINVAL, "k must be in [1, " + std::to_string(kMaxTopK) + "]");
+  const int32_t total = q_off[nq];
+  if (total < 0 || (total > 0 && !q_terms)) CM_FAIL(CM_EINVAL, "bad q_off");
+  for (int i = 0; i < nq; ++i)
+    if (q_off[i + 1] < q_off[i]) CM_FAIL(CM_EINVAL, "q_off must be non-decreasing");
+  DeviceGuard dg(h->dev);
+  int rc;
+  // candidate statistics
+  int64_t n_cand = h->n_live, sum_len = h->sum_len;
+  const uint32_t *allow_dev = nullptr;
+  const int64_t nw = std::max<int64_t>(1, ceil_div(h->ndocs, 32));
+  std::vector<double> q_idf((size_t)std::max(total, 1), 0.0);
+  if (allow_bits) {
+    if ((rc = h->allow_buf.ensure((size_t)nw * 4)) || (rc = h->tmp.ensure(16))) return rc;
+    CM_HIP(hipMemcpyAsync(h->allow_buf.ptr, allow_bits, (size_t)nw * 4, hipMemcpyHostToDevice, h->stream));
+    allow_dev = h->allow_buf.as<uint32_t>();
+    CM_HIP(hipMemsetAsync(h->tmp.ptr, 0, 16, h->stream));
+    hipLaunchKernelGGL(bm25_filtered_stats_kernel, dim3((unsigned)std::min<int64_t>(1024, ceil_div(nw, 256))),
+                       dim3(256), 0, h->stream, h->dl.as<int32_t>(), h->live.as<uint32_t>(), allow_dev, h->ndocs,
+                       h->tmp.as<unsigned long long>());
+    CM_HIP(hipGetLastError());
+    unsigned long long st2[2];
+    CM_HIP(hipMemcpyAsync(st2, h->tmp.ptr, 16, hipMemcpyDeviceToHost, h->stream));
+    CM_HIP(hipStreamSynchronize(h->stream));
+    n_cand = (int64_t)st2[0];
+    sum_len = (int64_t)st2[1];
+  }
+  if (n_cand == 0 || h->ndocs == 0) {
+    for (int i = 0; i < nq; ++i) {
+      if (out_n) out_n[i] = 0;
+      for (int j = 0; j < k; ++j) {
+        out_score[(int64_t)i * k + j] = 0.0;
+        out_row[(int64_t)i * k + j] = -1;
+      }
+    }
+    return CM_OK;
+  }
+  if (sum_len == 0) CM_FAIL(CM_EZERODIV, "float division by zero (candidate documents have no tokens)");
+  double avgdl = (double)sum_len / (double)n_cand;
+  if (!allow_bits) {
+    for (int32_t i = 0; i < total; ++i) {
+      const int32_t t = q_terms[i];
+      q_idf[i] = (t >= 0 && t < h->vocab) ? h->idf_host[t] : 0.0;
+    }
+  } else {
+    // filtered df of the distinct query terms
+    std::vector<int32_t> uterms;
+    for (int32_t i = 0; i < total; ++i)
+      if (q_terms[i] >= 0 && q_terms[i] < h->vocab) uterms.push_back(q_terms[i]);
+    std::sort(uterms.begin(), uterms.end());
+    uterms.erase(std::unique(uterms.begin(), uterms.end()), uterms.end());
+    std::vector<int64_t> udf(uterms.size(), 0);
+    bool need_eps = false;
+    if (!uterms.empty()) {
+      const size_t nu = uterms.size();
+      if ((rc = h->qbuf.ensure(nu * 4)) || (rc = h->obuf.ensure(nu * 8))) return rc;
+      CM_HIP(hipMemcpyAsync(h->qbuf.ptr, uterms.data(), nu * 4, hipMemcpyHostToDevice, h->stream));
+      hipLaunchKernelGGL(bm25_term_df_kernel, dim3((unsigned)nu), dim3(256), 0, h->stream, h->qbuf.as<int32_t>(),
+                         (int)nu, h->term_off.as<int64_t>(), h->post_doc.as<int32_t>(), h->post_pos.as<uint32_t>(),
+                         h->live.as<uint32_t>(), allow_dev, h->obuf.as<int64_t>(), (uint64_t *)nullptr);
+      CM_HIP(hipGetLastError());
+      CM_HIP(hipMemcpyAsync(udf.data(), h->obuf.ptr, nu * 8, hipMemcpyDeviceToHost, h->stream));
+      CM_HIP(hipStreamSynchronize(h->stream));
+      for (size_t u = 0; u < nu; ++u)
+        if (udf[u] > 0 && bm25_idf(n_cand, udf[u]) < 0) need_eps = true;
+    }
+    double eps = 0.0;
+    if (need_eps) {
+      // average idf over the whole candidate vocabulary in first-occurrence order
+      const int32_t V = h->vocab;
+      if ((rc = h->obuf.ensure((size_t)V * 16))) return rc;
+      int64_t *dfv = h->obuf.as<int64_t>();
+      uint64_t *fkv = reinterpret_cast<uint64_t *>(h->obuf.as<char>() + (size_t)V * 8);
+      hipLaunchKernelGGL(bm25_term_df_kernel, dim3((unsigned)V), dim3(256), 0, h->stream, (const int32_t *)nullptr,
+                         (int)V, h->term_off.as<int64_t>(), h->post_doc.as<int32_t>(), h->post_pos.as<uint32_t>(),
+                         h->live.as<uint32_t>(), allow_dev, dfv, fkv);
+      CM_HIP(hipGetLastError());
+      std::vector<int64_t> dfh((size_t)V);
+      std::vector<uint64_t> fkh((size_t)V);
+      CM_HIP(hipMemcpyAsync(dfh.data(), dfv, (size_t)V * 8, hipMemcpyDeviceToHost, h->stream));
+      CM_HIP(hipMemcpyAsync(fkh.data(), fkv, (size_t)V * 8, hipMemcpyDeviceToHost, h->stream));
+      CM_HIP(hipStreamSynchronize(h->stream));
+      std::vector<int32_t> order;
+      for (int32_t t = 0; t < V; ++t)
+        if (dfh[t] > 0) order.push_back(t);
+      std::sort(order.begin(), order.end(), [&](int32_t a, int32_t b) { return fkh[a] < fkh[b]; });
+      double s = 0.0;
+      for (int32_t t : order) s = s + bm25_idf(n_cand, dfh[t]);
+      eps = 0.25 * (s / (double)order.size());
+    }
+    for (int32_t i = 0; i < total; ++i) {
+      const int32_t t = q_terms[i];
+      if (t < 0 || t >= h->vocab) continue;
+      const size_t u = std::lower_bound(uterms.begin(), uterms.end(), t) - uterms.begin();
+      const int64_t d = udf[u];
+      if (d <= 0) continue;  // not in the candidate vocabulary: idf.get -> None -> 0
+      const double v = bm25_idf(n_cand, d);
+      q_idf[i] = v < 0 ? eps : v;
+    }
+  }
+  // device search
+  const int64_t wsb = cm_bm25_search_workspace(h, nq, total, k);
+  if ((rc = h->ws.ensure((size_t)wsb))) return rc;
+  BmWs w = bm_ws_layout(h, nq, total, k, h->ws.ptr);
+  const size_t qb = (size_t)std::max(total, 1) * 4 + (size_t)(nq + 1) * 4;
+  if ((rc = h->qbuf.ensure(qb)) || (rc = h->obuf.ensure((size_t)nq * k * 16))) return rc;
+  int32_t *d_terms = h->qbuf.as<int32_t>();
+  int32_t *d_off = d_terms + std::max(total, 1);
+  if (total > 0) CM_HIP(hipMemcpyAsync(d_terms, q_terms, (size_t)total * 4, hipMemcpyHostToDevice, h->stream));
+  CM_HIP(hipMemcpyAsync(d_off, q_off, (size_t)(nq + 1) * 4, hipMemcpyHostToDevice, h->stream));
+  if (total > 0) CM_HIP(hipMemcpyAsync(w.q_idf, q_idf.data(), (size_t)total * 8, hipMemcpyHostToDevice, h->stream));
+  double *d_score = h->obuf.as<double>();
+  int64_t *d_row = reinterpret_cast<int64_t *>(d_score + (size_t)nq * k);
+  rc = bm25_launch_core(h, d_terms, d_off, nq, total, k, allow_dev, avgdl, w, d_score, d_row, h->stream);
+  if (rc) return rc;
+  CM_HIP(hipMemcpyAsync(out_score, d_score, (size_t)nq * k * 8, hipMemcpyDeviceToHost, h->stream));
+  CM_HIP(hipMemcpyAsync(out_row, d_row, (size_t)nq * k * 8, hipMemcpyDeviceToHost, h->stream));
+  CM_HIP(hipStreamSynchronize(h->stream));
+  if (out_n) {
+    const int32_t nv = (int32_t)std::min<int64_t>(k, n_cand);
+    for (int i = 0; i < nq; ++i) out_n[i] = nv;
+  }
+  return CM_OK;
+}
+
+}  // extern "C"

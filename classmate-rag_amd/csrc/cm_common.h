@@ -1,0 +1,98 @@
+// Shared host/device helpers for libclassmate_hip (gfx950 only).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <string>
+
+#include "classmate_hip.h"
+
+namespace cm {
+
+void set_error(const std::string &msg);
+
+// Set the error message and return `code` from the enclosing API function.
+#define CM_FAIL(code, msg)            \
+  do {                                \
+    ::cm::set_error(msg);             \
+    return (code);                    \
+  } while (0)
+
+#define CM_HIP(expr)                                                                         \
+  do {                                                                                       \
+    hipError_t _e = (expr);                                                                  \
+    if (_e != hipSuccess) {                                                                  \
+      ::cm::set_error(std::string("HIP error in ") + #expr + ": " + hipGetErrorString(_e)); \
+      return CM_EDEVICE;                                                                     \
+    }                                                                                        \
+  } while (0)
+
+// RAII: make `dev` current for the duration of an API call, restore after.
+struct DeviceGuard {
+  int prev = -1;
+  bool ok = true;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev) ok = hipSetDevice(dev) == hipSuccess;
+  }
+  ~DeviceGuard() {
+    int cur = -1;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+};
+
+__host__ __device__ inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+__host__ __device__ inline int64_t round_up(int64_t a, int64_t b) { return ceil_div(a, b) * b; }
+
+// Grow-only device buffer.
+struct DevBuf {
+  void *ptr = nullptr;
+  size_t bytes = 0;
+  int ensure(size_t need) {
+    if (need <= bytes) return CM_OK;
+    if (ptr) (void)hipFree(ptr);
+    ptr = nullptr;
+    bytes = 0;
+    if (need == 0) return CM_OK;
+    if (hipMalloc(&ptr, need) != hipSuccess) {
+      set_error("hipMalloc failed for " + std::to_string(need) + " bytes");
+      return CM_ENOMEM;
+    }
+    bytes = need;
+    return CM_OK;
+  }
+  void release() {
+    if (ptr) (void)hipFree(ptr);
+    ptr = nullptr;
+    bytes = 0;
+  }
+  template <typename T>
+  T *as() const {
+    return reinterpret_cast<T *>(ptr);
+  }
+};
+
+// Orderable encodings so that an unsigned integer compare gives the float order.
+__host__ __device__ inline uint32_t f32_order(float f) {
+  uint32_t u = __builtin_bit_cast(uint32_t, f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__host__ __device__ inline float f32_unorder(uint32_t u) {
+  u = (u & 0x80000000u) ? (u & 0x7fffffffu) : ~u;
+  return __builtin_bit_cast(float, u);
+}
+__host__ __device__ inline uint64_t f64_order(double d) {
+  uint64_t u = __builtin_bit_cast(uint64_t, d);
+  return (u & 0x8000000000000000ull) ? ~u : (u | 0x8000000000000000ull);
+}
+__host__ __device__ inline double f64_unorder(uint64_t u) {
+  u = (u & 0x8000000000000000ull) ? (u & 0x7fffffffffffffffull) : ~u;
+  return __builtin_bit_cast(double, u);
+}
+
+constexpr uint64_t kEmptyKey = ~0ull;
+constexpr int kMaxTopK = 256;
+
+}  // namespace cm

@@ -1,0 +1,442 @@
+// Device-side fusion: MMR re-ordering (rag/retrieval/fusion.py:39-61) and
+// Reciprocal Rank Fusion + HybridRetriever's final sort (fusion.py:17-36,
+// 132-167).  Both are tiny per query; they run one workgroup (MMR) or one
+// lane (RRF) per query so a batch of queries costs one launch each and the
+// pipeline never leaves the device between the k-NN and the final list.
+// Compiled with -ffp-contract=off (the fused score must be bit-identical).
+#include "cm_common.h"
+
+#include <algorithm>
+#include <vector>
+
+namespace cm {
+
+constexpr int kMmrThreads = 256;
+constexpr int kMmrMaxPool = 256;
+
+// fp32 dot computed in fp64 and rounded once (closest fp32 to the exact dot).
+__device__ inline float wave_dot(const float *__restrict__ a, const float *__restrict__ b, int dim, int lane) {
+  double s = 0.0;
+  for (int d = lane; d < dim; d += 64) s += (double)a[d] * (double)b[d];
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  return (float)s;
+}
+
+// One workgroup per query.  sims_q = C q ; greedy: argmax(sims_q) first, then
+// maximise f32(lam*sq[i]) - f32((1-lam)*max_{j in sel} sims_cc[i,j]) with
+// strict '>' over remaining i in ascending order (NumPy>=2 float32 scalar
+// arithmetic, the reference's set iteration order).  max-diversity is kept
+// incrementally, so only pool x k pair dots are computed.
+__global__ void __launch_bounds__(kMmrThreads) mmr_kernel(const float *__restrict__ q, const float *__restrict__ cands,
+                                                          const int32_t *__restrict__ n_valid, int pool, int dim,
+                                                          int k, float lam32, float oml32,
+                                                          int32_t *__restrict__ out_order) {
+  __shared__ float sq[kMmrMaxPool];
+  __shared__ float maxdiv[kMmrMaxPool];
+  __shared__ int sel_flag[kMmrMaxPool];
+  __shared__ int cur;
+  const int qi = blockIdx.x;
+  const int n = min(n_valid ? n_valid[qi] : pool, pool);
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const float *qv = q + (int64_t)qi * dim;
+  const float *cv = cands + (int64_t)qi * pool * dim;
+  const int kk = min(k, n);
+  for (int i = threadIdx.x; i < k; i += kMmrThreads) out_order[(int64_t)qi * k + i] = -1;
+  if (n <= 0) return;
+  for (int i = wave; i < n; i += kMmrThreads / 64) {
+    const float s = wave_dot(cv + (int64_t)i * dim, qv, dim, lane);
+    if (lane == 0) sq[i] = s;
+  }
+  for (int i = threadIdx.x; i < n; i += kMmrThreads) {
+    maxdiv[i] = -INFINITY;
+    sel_flag[i] = 0;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int best = 0;
+    for (int i = 1; i < n; ++i)
+      if (sq[i] > sq[best]) best = i;  // np.argmax: first maximum
+    cur = best;
+    sel_flag[best] = 1;
+    out_order[(int64_t)qi * k] = best;
+  }
+  __syncthreads();
+  for (int step = 1; step < kk; ++step) {
+    const int s = cur;
+    // update max-diversity with the newly selected item
+    for (int i = wave; i < n; i += kMmrThreads / 64) {
+      if (sel_flag[i]) continue;
+      const float sim = wave_dot(cv + (int64_t)i * dim, cv + (int64_t)s * dim, dim, lane);
+      if (lane == 0) maxdiv[i] = fmaxf(maxdiv[i], sim);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int best = -1;
+      float bs = -1e9f;
+      for (int i = 0; i < n; ++i) {
+        if (sel_flag[i]) continue;
+        const float a = lam32 * sq[i];
+        const float b = oml32 * maxdiv[i];
+        const float sc = a - b;
+        if (sc > bs) {
+          bs = sc;
+          best = i;
+        }
+      }
+      cur = best;
+      sel_flag[best] = 1;
+      out_order[(int64_t)qi * k + step] = best;
+    }
+    __syncthreads();
+  }
+}
+
+// HybridRetriever.retrieve's merge for one query per lane.
+__global__ void rrf_merge_kernel(const int64_t *__restrict__ vkeys, const float *__restrict__ vdist,
+                                 const int32_t *__restrict__ vn, int kv, const int64_t *__restrict__ bkeys,
+                                 const double *__restrict__ bscore, const int32_t *__restrict__ bn, int kb, int nq,
+                                 double w_vec, double w_bm25, int rrf_k, int top_k, int64_t *__restrict__ out_keys,
+                                 double *__restrict__ out_fused, float *__restrict__ out_vdist,
+                                 double *__restrict__ out_bscore, int32_t *__restrict__ out_flags,
+                                 int32_t *__restrict__ out_n, int64_t *__restrict__ scratch_keys,
+                                 double *__restrict__ scratch_f, double *__restrict__ scratch_v,
+                                 int32_t *__restrict__ scratch_src) {
+  const int qi = blockIdx.x * blockDim.x + threadIdx.x;
+  if (qi >= nq) return;
+  const int nv = vn ? min(vn[qi], kv) : kv;
+  const int nb = bn ? min(bn[qi], kb) : kb;
+  const int cap = kv + kb;
+  int64_t *key = scratch_keys + (int64_t)qi * cap;
+  double *fused = scratch_f + (int64_t)qi * cap;
+  double *vdt = scratch_v + (int64_t)qi * cap;
+  int32_t *src = scratch_src + (int64_t)qi * cap;  // bit0: vec index+1 in low 16, bit16..: bm index+1
+  int m = 0;
+  // by_id in insertion order: vector items (MMR order), then BM25-only items.
+  for (int r = 0; r < nv; ++r) {
+    const int64_t id = vkeys[(int64_t)qi * kv + r];
+    key[m] = id;
+    fused[m] = 0.0 + w_vec * (1.0 / (double)(rrf_k + (r + 1)));
+    vdt[m] = -(double)vdist[(int64_t)qi * kv + r];
+    src[m] = (r + 1);
+    ++m;
+  }
+  for (int r = 0; r < nb; ++r) {
+    const int64_t id = bkeys[(int64_t)qi * kb + r];
+    const double c = w_bm25 * (1.0 / (double)(rrf_k + (r + 1)));
+    int f = -1;
+    for (int j = 0; j < nv; ++j)
+      if (key[j] == id) {
+        f = j;
+        break;
+      }
+    if (f >= 0) {
+      fused[f] = fused[f] + c;
+      src[f] |= (r + 1) << 16;
+    } else {
+      key[m] = id;
+      fused[m] = 0.0 + c;
+      vdt[m] = -0.0;
+      src[m] = (r + 1) << 16;
+      ++m;
+    }
+  }
+  // stable insertion sort by (fused, vd_term) descending
+  for (int i = 1; i < m; ++i) {
+    const int64_t k0 = key[i];
+    const double f0 = fused[i], v0 = vdt[i];
+    const int32_t s0 = src[i];
+    int j = i - 1;
+    while (j >= 0 && (fused[j] < f0 || (fused[j] == f0 && vdt[j] < v0))) {
+      key[j + 1] = key[j];
+      fused[j + 1] = fused[j];
+      vdt[j + 1] = vdt[j];
+      src[j + 1] = src[j];
+      --j;
+    }
+    key[j + 1] = k0;
+    fused[j + 1] = f0;
+    vdt[j + 1] = v0;
+    src[j + 1] = s0;
+  }
+  const int n_out = min(m, top_k);
+  for (int i = 0; i < top_k; ++i) {
+    const int64_t o = (int64_t)qi * top_k + i;
+    if (i < n_out) {
+      const int vi = (src[i] & 0xffff) - 1;
+      const int bi = (src[i] >> 16) - 1;
+      out_keys[o] = key[i];
+      out_fused[o] = fused[i];
+      out_vdist[o] = vi >= 0 ? vdist[(int64_t)qi * kv + vi] : 0.f;
+      out_bscore[o] = bi >= 0 ? bscore[(int64_t)qi * kb + bi] : 0.0;
+      out_flags[o] = (vi >= 0 ? 1 : 0) | (bi >= 0 ? 2 : 0);
+    } else {
+      out_keys[o] = -1;
+      out_fused[o] = 0.0;
+      out_vdist[o] = 0.f;
+      out_bscore[o] = 0.0;
+      out_flags[o] = 0;
+    }
+  }
+  out_n[qi] = n_out;
+}
+
+// rrf_fuse over arbitrary lists (dict semantics) on one lane.
+__global__ void rrf_fuse_kernel(const int64_t *__restrict__ keys, const int32_t *__restrict__ off, int nl,
+                                const double *__restrict__ weights, int rrf_k, int64_t *__restrict__ out_keys,
+                                double *__restrict__ out_score, int32_t *__restrict__ out_n) {
+  if (blockIdx.x != 0 || threadIdx.x != 0) return;
+  int m = 0;
+  for (int li = 0; li < nl; ++li) {
+    const double w = weights ? weights[li] : 1.0;
+    for (int r = 0; r < off[li + 1] - off[li]; ++r) {
+      const int64_t id = keys[off[li] + r];
+      const double c = w * (1.0 / (double)(rrf_k + (r + 1)));
+      int f = -1;
+      for (int j = 0; j < m; ++j)
+        if (out_keys[j] == id) {
+          f = j;
+          break;
+        }
+      if (f < 0) {
+        out_keys[m] = id;
+        out_score[m] = 0.0 + c;
+        ++m;
+      } else {
+        out_score[f] = out_score[f] + c;
+      }
+    }
+  }
+  *out_n = m;
+}
+
+}  // namespace cm
+
+using namespace cm;
+
+namespace {
+
+struct HostStage {
+  hipStream_t st = nullptr;
+  int dev = -1;
+  DevBuf buf;
+  ~HostStage() {
+    buf.release();
+    if (st) (void)hipStreamDestroy(st);
+  }
+};
+
+// per-thread staging for the host-array fusion entry points
+HostStage &stage() {
+  static thread_local HostStage s;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  if (s.dev != dev) {
+    s.buf.release();
+    if (s.st) (void)hipStreamDestroy(s.st);
+    s.st = nullptr;
+    (void)hipStreamCreateWithFlags(&s.st, hipStreamNonBlocking);
+    s.dev = dev;
+  }
+  return s;
+}
+
+struct Carver {
+  char *base;
+  size_t off = 0;
+  template <typename T>
+  T *take(size_t n) {
+    T *p = reinterpret_cast<T *>(base + off);
+    off += round_up((int64_t)std::max<size_t>(n, 1) * sizeof(T), 256);
+    return p;
+  }
+};
+
+}  // namespace
+
+extern "C" {
+
+int cm_mmr_dev(const float *q_dev, const float *cands_dev, const int32_t *n_valid_dev, int32_t nq, int32_t pool,
+               int32_t dim, int32_t k, double lambd, int32_t *order_dev, void *stream) {
+  if (nq <= 0) return CM_OK;
+  if (pool <= 0 || pool > kMmrMaxPool) CM_FAIL(CM_EINVAL, "MMR pool must be in [1, 256]");
+  if (dim <= 0 || k <= 0) CM_FAIL(CM_EINVAL, "bad MMR arguments");
+  const float lam32 = (float)lambd;
+  const float oml32 = (float)(1.0 - lambd);
+  hipLaunchKernelGGL(mmr_kernel, dim3(nq), dim3(kMmrThreads), 0, (hipStream_t)stream, q_dev, cands_dev, n_valid_dev,
+                     pool, dim, k, lam32, oml32, order_dev);
+  CM_HIP(hipGetLastError());
+  return CM_OK;
+}
+
+int cm_mmr(const float *q, const float *cands, const int32_t *n_valid, int32_t nq, int32_t pool, int32_t dim,
+           int32_t k, double lambd, int32_t *out_order) {
+  if (nq <= 0) return CM_OK;
+  if (!q || !cands || !out_order) CM_FAIL(CM_EINVAL, "NULL argument");
+  if (pool <= 0 || pool > kMmrMaxPool || dim <= 0 || k <= 0) CM_FAIL(CM_EINVAL, "bad MMR arguments");
+  HostStage &s = stage();
+  Carver c{nullptr};
+  const size_t nqs = (size_t)nq;
+  c.take<float>(nqs * dim);
+  c.take<float>(nqs * pool * dim);
+  c.take<int32_t>(nqs);
+  c.take<int32_t>(nqs * k);
+  int rc = s.buf.ensure(c.off);
+  if (rc) return rc;
+  Carver d{s.buf.as<char>()};
+  float *dq = d.take<float>(nqs * dim);
+  float *dc = d.take<float>(nqs * pool * dim);
+  int32_t *dn = d.take<int32_t>(nqs);
+  int32_t *dout = d.take<int32_t>(nqs * k);
+  CM_HIP(hipMemcpyAsync(dq, q, nqs * dim * 4, hipMemcpyHostToDevice, s.st));
+  CM_HIP(hipMemcpyAsync(dc, cands, nqs * pool * dim * 4, hipMemcpyHostToDevice, s.st));
+  if (n_valid) CM_HIP(hipMemcpyAsync(dn, n_valid, nqs * 4, hipMemcpyHostToDevice, s.st));
+  rc = cm_mmr_dev(dq, dc, n_valid ? dn : nullptr, nq, pool, dim, k, lambd, dout, s.st);
+  if (rc) return rc;
+  CM_HIP(hipMemcpyAsync(out_order, dout, nqs * k * 4, hipMemcpyDeviceToHost, s.st));
+  CM_HIP(hipStreamSynchronize(s.st));
+  return CM_OK;
+}
+
+int cm_rrf_merge_dev(const int64_t *vkeys, const float *vdist, const int32_t *vn, int32_t kv, const int64_t *bkeys,
+                     const double *bscore, const int32_t *bn, int32_t kb, int32_t nq, double w_vec, double w_bm25,
+                     int32_t rrf_k, int32_t top_k, int64_t *out_keys, double *out_fused, float *out_vdist,
+                     double *out_bscore, int32_t *out_flags, int32_t *out_n, void *stream) {
+  // scratch lives after out_* in a caller workspace-free way: carve from a
+  // per-thread device buffer (graph capture: call once before capture so the
+  // buffer exists; it is reused afterwards).
+  if (nq <= 0) return CM_OK;
+  if (kv < 0 || kb < 0 || top_k <= 0 || kv + kb > 0xffff) CM_FAIL(CM_EINVAL, "bad RRF sizes");
+  static thread_local DevBuf scratch;
+  static thread_local int scratch_dev = -1;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  if (scratch_dev != dev) {
+    scratch.release();
+    scratch_dev = dev;
+  }
+  const int cap = std::max(kv + kb, 1);
+  const size_t need = (size_t)nq * cap * (8 + 8 + 8 + 4) + 1024;
+  if (need > scratch.bytes) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (stream) (void)hipStreamIsCapturing((hipStream_t)stream, &cs);
+    if (cs != hipStreamCaptureStatusNone) CM_FAIL(CM_EINVAL, "rrf scratch must be sized before graph capture");
+    int rc = scratch.ensure(need);
+    if (rc) return rc;
+  }
+  Carver c{scratch.as<char>()};
+  int64_t *sk = c.take<int64_t>((size_t)nq * cap);
+  double *sf = c.take<double>((size_t)nq * cap);
+  double *sv = c.take<double>((size_t)nq * cap);
+  int32_t *ss = c.take<int32_t>((size_t)nq * cap);
+  hipLaunchKernelGGL(rrf_merge_kernel, dim3((unsigned)ceil_div(nq, 64)), dim3(64), 0, (hipStream_t)stream, vkeys,
+                     vdist, vn, kv, bkeys, bscore, bn, kb, nq, w_vec, w_bm25, rrf_k, top_k, out_keys, out_fused,
+                     out_vdist, out_bscore, out_flags, out_n, sk, sf, sv, ss);
+  CM_HIP(hipGetLastError());
+  return CM_OK;
+}
+
+int cm_rrf_merge(const int64_t *vkeys, const float *vdist, const int32_t *vn, int32_t kv, const int64_t *bkeys,
+                 const double *bscore, const int32_t *bn, int32_t kb, int32_t nq, double w_vec, double w_bm25,
+                 int32_t rrf_k, int32_t top_k, int64_t *out_keys, double *out_fused, float *out_vdist,
+                 double *out_bscore, int32_t *out_flags, int32_t *out_n) {
+  if (nq <= 0) return CM_OK;
+  if (top_k <= 0 || kv < 0 || kb < 0) CM_FAIL(CM_EINVAL, "bad RRF sizes");
+  HostStage &s = stage();
+  const size_t n = (size_t)nq;
+  Carver c{nullptr};
+  c.take<int64_t>(n * kv);
+  c.take<float>(n * kv);
+  c.take<int32_t>(n);
+  c.take<int64_t>(n * kb);
+  c.take<double>(n * kb);
+  c.take<int32_t>(n);
+  c.take<int64_t>(n * top_k);
+  c.take<double>(n * top_k);
+  c.take<float>(n * top_k);
+  c.take<double>(n * top_k);
+  c.take<int32_t>(n * top_k);
+  c.take<int32_t>(n);
+  int rc = s.buf.ensure(c.off);
+  if (rc) return rc;
+  Carver d{s.buf.as<char>()};
+  int64_t *dvk = d.take<int64_t>(n * kv);
+  float *dvd = d.take<float>(n * kv);
+  int32_t *dvn = d.take<int32_t>(n);
+  int64_t *dbk = d.take<int64_t>(n * kb);
+  double *dbs = d.take<double>(n * kb);
+  int32_t *dbn = d.take<int32_t>(n);
+  int64_t *ok = d.take<int64_t>(n * top_k);
+  double *of = d.take<double>(n * top_k);
+  float *ov = d.take<float>(n * top_k);
+  double *ob = d.take<double>(n * top_k);
+  int32_t *ofl = d.take<int32_t>(n * top_k);
+  int32_t *on = d.take<int32_t>(n);
+  if (kv) {
+    CM_HIP(hipMemcpyAsync(dvk, vkeys, n * kv * 8, hipMemcpyHostToDevice, s.st));
+    CM_HIP(hipMemcpyAsync(dvd, vdist, n * kv * 4, hipMemcpyHostToDevice, s.st));
+  }
+  if (kb) {
+    CM_HIP(hipMemcpyAsync(dbk, bkeys, n * kb * 8, hipMemcpyHostToDevice, s.st));
+    CM_HIP(hipMemcpyAsync(dbs, bscore, n * kb * 8, hipMemcpyHostToDevice, s.st));
+  }
+  if (vn) CM_HIP(hipMemcpyAsync(dvn, vn, n * 4, hipMemcpyHostToDevice, s.st));
+  if (bn) CM_HIP(hipMemcpyAsync(dbn, bn, n * 4, hipMemcpyHostToDevice, s.st));
+  rc = cm_rrf_merge_dev(dvk, dvd, vn ? dvn : nullptr, kv, dbk, dbs, bn ? dbn : nullptr, kb, nq, w_vec, w_bm25, rrf_k,
+                        top_k, ok, of, ov, ob, ofl, on, s.st);
+  if (rc) return rc;
+  CM_HIP(hipMemcpyAsync(out_keys, ok, n * top_k * 8, hipMemcpyDeviceToHost, s.st));
+  CM_HIP(hipMemcpyAsync(out_fused, of, n * top_k * 8, hipMemcpyDeviceToHost, s.st));
+  CM_HIP(hipMemcpyAsync(out_vdist, ov, n * top_k * 4, hipMemcpyDeviceToHost, s.st));
+  CM_HIP(hipMemcpyAsync(out_bscore, ob, n * top_k * 8, hipMemcpyDeviceToHost, s.st));
+  CM_HIP(hipMemcpyAsync(out_flags, ofl, n * top_k * 4, hipMemcpyDeviceToHost, s.st));
+  CM_HIP(hipMemcpyAsync(out_n, on, n * 4, hipMemcpyDeviceToHost, s.st));
+  CM_HIP(hipStreamSynchronize(s.st));
+  return CM_OK;
+}
+
+int cm_rrf_fuse(const int64_t *keys, const int32_t *off, int32_t nl, const double *weights, int32_t rrf_k,
+                int64_t *out_keys, double *out_score, int32_t *out_n) {
+  if (!out_n || !off) CM_FAIL(CM_EINVAL, "NULL argument");
+  *out_n = 0;
+  if (nl <= 0) return CM_OK;
+  const int32_t total = off[nl];
+  for (int i = 0; i < nl; ++i)
+    if (off[i + 1] < off[i]) CM_FAIL(CM_EINVAL, "off must be non-decreasing");
+  if (total > 0 && (!keys || !out_keys || !out_score)) CM_FAIL(CM_EINVAL, "NULL argument");
+  HostStage &s = stage();
+  Carver c{nullptr};
+  c.take<int64_t>(total);
+  c.take<int32_t>(nl + 1);
+  c.take<double>(nl);
+  c.take<int64_t>(total);
+  c.take<double>(total);
+  c.take<int32_t>(1);
+  int rc = s.buf.ensure(c.off);
+  if (rc) return rc;
+  Carver d{s.buf.as<char>()};
+  int64_t *dk = d.take<int64_t>(total);
+  int32_t *doff = d.take<int32_t>(nl + 1);
+  double *dw = d.take<double>(nl);
+  int64_t *ok = d.take<int64_t>(total);
+  double *os = d.take<double>(total);
+  int32_t *on = d.take<int32_t>(1);
+  if (total) CM_HIP(hipMemcpyAsync(dk, keys, (size_t)total * 8, hipMemcpyHostToDevice, s.st));
+  CM_HIP(hipMemcpyAsync(doff, off, (size_t)(nl + 1) * 4, hipMemcpyHostToDevice, s.st));
+  if (weights) CM_HIP(hipMemcpyAsync(dw, weights, (size_t)nl * 8, hipMemcpyHostToDevice, s.st));
+  hipLaunchKernelGGL(rrf_fuse_kernel, dim3(1), dim3(64), 0, s.st, dk, doff, nl, weights ? dw : nullptr, rrf_k, ok,
+                     os, on);
+  CM_HIP(hipGetLastError());
+  int32_t n = 0;
+  CM_HIP(hipMemcpyAsync(&n, on, 4, hipMemcpyDeviceToHost, s.st));
+  CM_HIP(hipStreamSynchronize(s.st));
+  if (n > 0) {
+    CM_HIP(hipMemcpyAsync(out_keys, ok, (size_t)n * 8, hipMemcpyDeviceToHost, s.st));
+    CM_HIP(hipMemcpyAsync(out_score, os, (size_t)n * 8, hipMemcpyDeviceToHost, s.st));
+    CM_HIP(hipStreamSynchronize(s.st));
+  }
+  *out_n = n;
+  return CM_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,177 @@
+/*
+ * classmate_hip.h — C ABI of libclassmate_hip.so, the MI355X (gfx950) hybrid
+ * retrieval engine behind CLASSMATE-RAG's retrieval API.
+ *
+ * Plain C: pointers + sizes only, no C++/torch types.  Every entry point
+ * names the reference interface it replaces (paths relative to the
+ * taha-kms/CLASSMATE-RAG tree).  Conventions:
+ *   - return 0 (CM_OK) on success, < 0 on error; cm_last_error() gives a
+ *     thread-local message.  CM_EINVAL maps to Python ValueError (the
+ *     reference's convention for length mismatches, e.g. bm25.py:152-153),
+ *     CM_EZERODIV to ZeroDivisionError (rank_bm25 on an empty vocabulary,
+ *     SURVEY.md §8a quirk Q7), everything else to RuntimeError.
+ *   - "host" functions take caller-owned host arrays, run on the handle's
+ *     own HIP stream and return after the results are copied back.
+ *   - "_dev" functions take device pointers plus a hipStream_t (as void*,
+ *     NULL = the handle's stream); they never allocate, never synchronise,
+ *     and are safe to capture into a HIP graph.
+ *   - rows are int64 row indices into the handle's storage; "-1" pads
+ *     results that have fewer than k entries.
+ *   - allow bitmaps: bit (r & 31) of word r >> 5 set => row r may be
+ *     returned (a Chroma `where` / BM25 `_matches_filter` mask).
+ */
+#ifndef CLASSMATE_HIP_H
+#define CLASSMATE_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CM_OK 0
+#define CM_EINVAL (-1)
+#define CM_ENOMEM (-2)
+#define CM_EDEVICE (-3)
+#define CM_EZERODIV (-4)
+#define CM_EUNSUPPORTED (-5)
+
+#define CM_DTYPE_F32 0
+#define CM_DTYPE_BF16 1
+#define CM_DTYPE_F16 2
+#define CM_DTYPE_I32 3
+#define CM_DTYPE_I64 4
+
+/* Library ------------------------------------------------------------- */
+const char *cm_last_error(void);
+int cm_version(void);
+int cm_device_count(int *n);
+/* largest k the fused top-k kernels accept (dense and BM25). */
+int cm_max_topk(void);
+
+/* Dense cosine k-NN ---------------------------------------------------
+ * Replaces ChromaVectorStore (rag/retrieval/vector_chroma.py:81-278) and
+ * the chromadb/hnswlib server it talks to: the corpus lives in HBM as fp32
+ * rows, search is exact brute-force cosine (distance = 1 - cos, the
+ * `hnsw:space=cosine` metric set at vector_chroma.py:156).               */
+typedef struct cm_dense cm_dense;
+
+/* ChromaVectorStore.__init__/_ensure_collection (vector_chroma.py:81-164). */
+int cm_dense_create(int device, int32_t dim, int64_t capacity, cm_dense **out);
+void cm_dense_destroy(cm_dense *h);
+int cm_dense_reserve(cm_dense *h, int64_t capacity);
+/* ChromaVectorStore.upsert (vector_chroma.py:168-200): write n fp32 rows
+ * (host, n x dim row-major) at the given row indices, marking them live.
+ * Rows beyond the current size grow the store. */
+int cm_dense_upsert(cm_dense *h, const float *vecs, const int64_t *rows, int64_t n);
+/* device variant: n contiguous rows starting at row0 from a device buffer. */
+int cm_dense_upsert_dev(cm_dense *h, const float *vecs_dev, int64_t row0, int64_t n, void *stream);
+/* col.delete (vector_chroma.py:181-187): clear the live bit of rows. */
+int cm_dense_delete(cm_dense *h, const int64_t *rows, int64_t n);
+/* ChromaVectorStore.reset_collection (vector_chroma.py:262-269). */
+int cm_dense_reset(cm_dense *h);
+/* ChromaVectorStore.count (vector_chroma.py:255-260). */
+int64_t cm_dense_live_count(cm_dense *h);
+int64_t cm_dense_size(cm_dense *h); /* high-water row count */
+int32_t cm_dense_dim(cm_dense *h);
+/* ChromaVectorStore.query (vector_chroma.py:204-253), batched: for each of
+ * nq queries (host, nq x dim) return the k nearest live+allowed rows in
+ * ascending (distance, row) order.  out_dist/out_row: nq x k.  out_vec
+ * (nullable): nq x k x dim, the stored embeddings (include_embeddings).
+ * allow_bits (nullable, host): ceil(size/32) words.                      */
+int cm_dense_search(cm_dense *h, const float *q, int32_t nq, int32_t k, const uint32_t *allow_bits,
+                    float *out_dist, int64_t *out_row, float *out_vec);
+/* workspace bytes cm_dense_search_dev needs for (nq, k). */
+int64_t cm_dense_search_workspace(cm_dense *h, int32_t nq, int32_t k);
+int cm_dense_search_dev(cm_dense *h, const float *q_dev, int32_t nq, int32_t k, const uint32_t *allow_dev,
+                        float *dist_dev, int64_t *row_dev, void *workspace_dev, int64_t workspace_bytes,
+                        void *stream);
+/* gather stored rows (row < 0 => zeros): out_dev n x dim. */
+int cm_dense_gather_dev(cm_dense *h, const int64_t *rows_dev, int64_t n, float *out_dev, void *stream);
+/* device pointer of the live bitmap (ceil(size/32) words) for callers that
+ * AND their own filters on device. */
+const uint32_t *cm_dense_live_bits_dev(cm_dense *h);
+
+/* BM25 Okapi -------------------------------------------------------------
+ * Replaces BM25Store's scoring (rag/retrieval/bm25.py:140-212) and the
+ * rank_bm25.BM25Okapi it builds per search (k1=1.5, b=0.75, eps=0.25):
+ * CSR postings by term in HBM, term-ordered fp64 accumulation, statistics
+ * (N, avgdl, df, idf with the eps floor) over the filtered candidate set.  */
+typedef struct cm_bm25 cm_bm25;
+
+int cm_bm25_create(int device, cm_bm25 **out);
+void cm_bm25_destroy(cm_bm25 *h);
+/* BM25Store._rebuild / BM25Okapi.__init__ (bm25.py:140-145): build from
+ * doc-major term ids (host): doc d's tokens are term_ids[doc_off[d] ..
+ * doc_off[d+1]) in token order, term ids in [0, vocab).  live (nullable):
+ * one byte per doc, 0 = tombstone (deleted, keeps insertion order of the
+ * others).  Returns CM_EZERODIV when live docs exist but none has a token
+ * (the reference raises ZeroDivisionError there). */
+int cm_bm25_build(cm_bm25 *h, const int32_t *term_ids, const int64_t *doc_off, int64_t ndocs, int32_t vocab,
+                  const uint8_t *live);
+/* same from device arrays (K7: device CSR build by radix sort). */
+int cm_bm25_build_dev(cm_bm25 *h, const int32_t *term_ids_dev, const int64_t *doc_off_dev, int64_t ndocs,
+                      int64_t ntokens, int32_t vocab, void *stream);
+int64_t cm_bm25_num_docs(cm_bm25 *h);
+int64_t cm_bm25_num_postings(cm_bm25 *h);
+/* unfiltered corpus statistics: live docs, total length, avgdl, eps. */
+int cm_bm25_stats(cm_bm25 *h, int64_t *n_live, int64_t *sum_len, double *avgdl, double *eps);
+/* BM25Store.search (bm25.py:175-212) batched: nq queries whose term ids
+ * (host, -1 = unknown term) are q_terms[q_off[i] .. q_off[i+1]) in query
+ * token order (duplicates count twice).  Candidates = live docs with the
+ * allow bit set; statistics are recomputed over them when allow_bits is
+ * given (quirk Q2).  Output per query: k (score, row) in descending score,
+ * ties -> lower row, zero-score docs padding in row order (quirk Q1);
+ * out_n[i] = number of valid entries (min(k, #candidates)).               */
+int cm_bm25_search(cm_bm25 *h, const int32_t *q_terms, const int32_t *q_off, int32_t nq, int32_t k,
+                   const uint32_t *allow_bits, double *out_score, int64_t *out_row, int32_t *out_n);
+/* unfiltered device variant (inputs and outputs device, graph-capturable). */
+int64_t cm_bm25_search_workspace(cm_bm25 *h, int32_t nq, int32_t total_terms, int32_t k);
+int cm_bm25_search_dev(cm_bm25 *h, const int32_t *q_terms_dev, const int32_t *q_off_dev, int32_t nq,
+                       int32_t total_terms, int32_t k, double *score_dev, int64_t *row_dev,
+                       void *workspace_dev, int64_t workspace_bytes, void *stream);
+
+/* Fusion -------------------------------------------------------------- */
+/* _mmr_order (rag/retrieval/fusion.py:39-61) for nq queries at once:
+ * q: nq x dim, cands: nq x pool x dim (fp32), n_valid[i] <= pool rows valid
+ * for query i.  out_order: nq x k indices into the pool (-1 pad).         */
+int cm_mmr(const float *q, const float *cands, const int32_t *n_valid, int32_t nq, int32_t pool, int32_t dim,
+           int32_t k, double lambd, int32_t *out_order);
+int cm_mmr_dev(const float *q_dev, const float *cands_dev, const int32_t *n_valid_dev, int32_t nq, int32_t pool,
+               int32_t dim, int32_t k, double lambd, int32_t *order_dev, void *stream);
+/* rrf_fuse (rag/retrieval/fusion.py:17-36): nl rank lists of int64 keys
+ * (host; list i = keys[off[i] .. off[i+1])).  out_keys/out_score receive
+ * the distinct keys in first-appearance order (Python dict order) and
+ * their fused scores; *out_n = count.  weights nullable (all 1.0).      */
+int cm_rrf_fuse(const int64_t *keys, const int32_t *off, int32_t nl, const double *weights, int32_t rrf_k,
+                int64_t *out_keys, double *out_score, int32_t *out_n);
+/* HybridRetriever.retrieve merge (fusion.py:132-167), batched on device:
+ * per query a vector list (<= kv keys with fp32 distance, MMR order) and a
+ * BM25 list (<= kb keys with fp64 score); outputs the top_k items sorted by
+ * (fused, -distance or -0.0) descending, stable (vector items first).
+ * out_flags bit0 = has vector distance, bit1 = has BM25 score.           */
+int cm_rrf_merge_dev(const int64_t *vkeys, const float *vdist, const int32_t *vn, int32_t kv,
+                     const int64_t *bkeys, const double *bscore, const int32_t *bn, int32_t kb, int32_t nq,
+                     double w_vec, double w_bm25, int32_t rrf_k, int32_t top_k, int64_t *out_keys,
+                     double *out_fused, float *out_vdist, double *out_bscore, int32_t *out_flags,
+                     int32_t *out_n, void *stream);
+int cm_rrf_merge(const int64_t *vkeys, const float *vdist, const int32_t *vn, int32_t kv, const int64_t *bkeys,
+                 const double *bscore, const int32_t *bn, int32_t kb, int32_t nq, double w_vec, double w_bm25,
+                 int32_t rrf_k, int32_t top_k, int64_t *out_keys, double *out_fused, float *out_vdist,
+                 double *out_bscore, int32_t *out_flags, int32_t *out_n);
+
+/* E5 pooling ------------------------------------------------------------
+ * sentence-transformers Pooling(mean) + Normalize as used by
+ * E5MultilingualEmbedder.encode_* (rag/embeddings/__init__.py:85-105):
+ * out[b] = sum_s h[b,s]*m[b,s] / max(sum_s m[b,s], 1e-9), then (if
+ * normalize) out[b] /= max(||out[b]||_2, 1e-12).  hidden: B x S x D of
+ * hidden_dtype (F32/BF16/F16), mask: B x S of mask_dtype (I32/I64),
+ * out: B x D fp32.  All device pointers, torch's stream.                 */
+int cm_meanpool_l2norm(const void *hidden_dev, int32_t hidden_dtype, const void *mask_dev, int32_t mask_dtype,
+                       int32_t B, int32_t S, int32_t D, int32_t normalize, float *out_dev, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CLASSMATE_HIP_H */

@@ -1,0 +1,267 @@
+"""GPU parity of the HIP kernels (through the C ABI) against the CPU oracle.
+
+Bars: BM25 scores bit-identical (fp64) with identical ids/order; dense top-k
+set equality with cosine distance within 1e-4 (north_star tolerance) and the
+exact order wherever neighbouring oracle distances differ by more than 1e-5;
+MMR orders and RRF scores identical to the reference-semantics oracle.
+"""
+import numpy as np
+import pytest
+
+from oracle import ref_semantics as orc
+
+pytestmark = pytest.mark.gpu
+
+DIST_TOL = 1e-4
+
+
+@pytest.fixture(scope="module")
+def eng():
+    from classmate_hip import engine
+    return engine
+
+
+def _bits(mask: np.ndarray) -> np.ndarray:
+    n = mask.shape[0]
+    words = np.zeros((n + 31) // 32, np.uint32)
+    idx = np.nonzero(mask)[0]
+    np.bitwise_or.at(words, idx >> 5, (np.uint32(1) << (idx & 31).astype(np.uint32)))
+    return words
+
+
+def _check_dense(dist, rows, emb, q, k, allow=None):
+    o_rows, o_dist = orc.dense_topk_exact(emb, q, k, allow)
+    for i in range(q.shape[0]):
+        n = len(o_rows[i])
+        got_r = rows[i][rows[i] >= 0]
+        assert len(got_r) == n
+        np.testing.assert_allclose(dist[i][:n], o_dist[i], atol=DIST_TOL)
+        # set equality except for ties within tolerance at the boundary
+        if n == k and n < emb.shape[0]:
+            all_d = 1.0 - (emb.astype(np.float64) @ q[i].astype(np.float64)) / np.linalg.norm(emb, axis=1) / \
+                np.linalg.norm(q[i])
+            kth = o_dist[i][-1]
+            unsure = set(np.nonzero(np.abs(all_d - kth) < 1e-5)[0].tolist())
+            assert set(got_r.tolist()) ^ set(o_rows[i].tolist()) <= unsure
+        else:
+            assert set(got_r.tolist()) == set(o_rows[i].tolist())
+        # order: strict wherever the oracle distances are separated
+        sep = np.diff(o_dist[i]) > 1e-5
+        for j in np.nonzero(sep)[0]:
+            assert got_r[j] == o_rows[i][j] or abs(dist[i][j] - o_dist[i][j]) < 1e-5
+
+
+def test_dense_golden_corpus(eng, corpus, golden):
+    emb, qv = corpus["emb"], corpus["qvecs"]
+    idx = eng.DenseIndex(768)
+    idx.upsert(emb, np.arange(emb.shape[0]))
+    assert idx.live_count() == emb.shape[0]
+    dist, rows = idx.search(qv, 24)
+    _check_dense(dist, rows, emb, qv, 24)
+    # goldens: same ids & fp32 distances as the reference-run exact store
+    ids = corpus["ids"]
+    for i, want in enumerate(golden["dense"]["none"]):
+        assert [ids[r] for r in rows[i]] == [w[0] for w in want]
+        np.testing.assert_allclose(dist[i], [w[1] for w in want], atol=DIST_TOL)
+
+
+def test_dense_filtered_and_deleted(eng, corpus):
+    emb, qv = corpus["emb"], corpus["qvecs"]
+    idx = eng.DenseIndex(768)
+    idx.upsert(emb, np.arange(emb.shape[0]))
+    allow = np.array([m.get("course") == "cs101" for m in corpus["metas"]])
+    dist, rows = idx.search(qv, 24, _bits(allow))
+    _check_dense(dist, rows, emb, qv, 24, allow)
+    dele = np.arange(0, emb.shape[0], 3)
+    idx.delete(dele)
+    live = np.ones(emb.shape[0], bool)
+    live[dele] = False
+    dist, rows = idx.search(qv, 10)
+    _check_dense(dist, rows, emb, qv, 10, live)
+    assert idx.live_count() == int(live.sum())
+    # fewer allowed rows than k -> padded with -1
+    few = np.zeros(emb.shape[0], bool)
+    few[[1, 4, 7]] = True
+    dist, rows = idx.search(qv[:2], 10, _bits(few))
+    assert (rows[:, 3:] == -1).all()
+    assert set(rows[0, :3].tolist()) == {1, 4, 7}
+
+
+@pytest.mark.parametrize("n,nq,k,dim", [(20000, 1, 10, 768), (20000, 48, 24, 768), (9000, 64, 10, 384),
+                                        (5000, 7, 100, 768), (3000, 3, 256, 256), (777, 33, 5, 1000)])
+def test_dense_shapes(eng, n, nq, k, dim):
+    rng = np.random.default_rng(n + nq + k)
+    emb = rng.standard_normal((n, dim)).astype(np.float32)
+    q = rng.standard_normal((nq, dim)).astype(np.float32)
+    q[: nq // 2] = emb[rng.integers(0, n, nq // 2)] + 0.05 * q[: nq // 2]
+    idx = eng.DenseIndex(dim)
+    perm = rng.permutation(n)       # scattered upsert order
+    idx.upsert(emb[perm], perm)
+    dist, rows = idx.search(q, k)
+    _check_dense(dist, rows, emb, q, k)
+
+
+def test_dense_device_path_and_gather(eng):
+    import torch
+    rng = np.random.default_rng(5)
+    emb = rng.standard_normal((4096, 768)).astype(np.float32)
+    q = rng.standard_normal((16, 768)).astype(np.float32)
+    idx = eng.DenseIndex(768)
+    idx.upsert_dev(torch.from_numpy(emb).cuda(), 0)
+    d_t, r_t = idx.search_dev(torch.from_numpy(q).cuda(), 24)
+    torch.cuda.synchronize()
+    d_h, r_h = idx.search(q, 24)
+    assert np.array_equal(r_t.cpu().numpy(), r_h)
+    g = idx.gather_dev(r_t.reshape(-1)).cpu().numpy().reshape(16, 24, 768)
+    assert np.array_equal(g, emb[r_h])
+
+
+def _term_ids(token_lists, vocab=None):
+    vocab = {} if vocab is None else vocab
+    out = []
+    for toks in token_lists:
+        out.append(np.array([vocab.setdefault(t, len(vocab)) for t in toks], np.int32))
+    return out, vocab
+
+
+def _build_bm25(eng, tok_lists):
+    ids, vocab = _term_ids(tok_lists)
+    off = np.zeros(len(ids) + 1, np.int64)
+    off[1:] = np.cumsum([len(x) for x in ids])
+    flat = np.concatenate(ids) if off[-1] else np.zeros(0, np.int32)
+    b = eng.BM25Index()
+    b.build(flat, off, len(vocab))
+    return b, vocab
+
+
+FILTERS = [None, {"course": "cs101", "unit": None, "author": None, "semester": None},
+           {"course": "math201"}, {"language": "en", "doc_type": "pptx"}]
+
+
+@pytest.mark.parametrize("where", FILTERS)
+def test_bm25_bit_exact(eng, corpus, where):
+    toks = [orc.tokenize(t, "en") for t in corpus["texts"]]
+    b, vocab = _build_bm25(eng, toks)
+    ora = orc.BM25Oracle()
+    ora.upsert_many(corpus["ids"], corpus["texts"], corpus["metas"])
+    qs = [[vocab.get(t, -1) for t in orc.tokenize(q, "en")] for q in corpus["qtexts"]]
+    allow = None
+    if where:
+        allow = _bits(np.array([orc.bm25_matches_filter(m, where) for m in corpus["metas"]]))
+    scores, rows, nvalid = b.search(qs, 10, allow)
+    for i, q in enumerate(corpus["qtexts"]):
+        want = ora.search(q, where, top_k=10)
+        got = [[corpus["ids"][r], s] for r, s in zip(rows[i][:nvalid[i]], scores[i][:nvalid[i]])]
+        assert got == [[w["id"], w["score"]] for w in want]
+
+
+def test_bm25_padding_negative_eps_and_dupes(eng):
+    # many docs share 'common' (negative idf), few match the rest; duplicates in the query
+    rng = np.random.default_rng(3)
+    words = [f"w{chr(97 + i)}{chr(97 + j)}" for i in range(20) for j in range(20)]
+    words = ["".join(c for c in w if c.isalpha()) for w in words]
+    texts = []
+    for d in range(3000):
+        n = int(rng.integers(0, 30))
+        ws = [words[int(x)] for x in rng.integers(0, len(words), n)]
+        if rng.random() < 0.8:
+            ws.append("common")
+        texts.append(" ".join(ws))
+    toks = [orc.tokenize(t, "en") for t in texts]
+    b, vocab = _build_bm25(eng, toks)
+    ora = orc.BM25Oracle()
+    ids = [f"d{i}" for i in range(len(texts))]
+    ora.upsert_many(ids, texts, [{"language": "en"}] * len(texts))
+    queries = ["common", "common common wbc", "wbc wbc wbc", "zzzz", "the of", "wab wcd common wab"]
+    qs = [[vocab.get(t, -1) for t in orc.tokenize(q, "en")] for q in queries]
+    for k in (1, 10, 37, 256):
+        scores, rows, nvalid = b.search(qs, k)
+        for i, q in enumerate(queries):
+            want = ora.search(q, None, top_k=k)
+            got = [[ids[r], s] for r, s in zip(rows[i][:nvalid[i]], scores[i][:nvalid[i]])]
+            assert got == [[w["id"], w["score"]] for w in want], (q, k)
+    # filtered subset small enough that 'common' goes negative inside it (filtered eps path)
+    mask = np.zeros(len(texts), bool)
+    mask[:40] = True
+    allow = _bits(mask)
+    scores, rows, nvalid = b.search(qs, 12, allow)
+    sub = orc.BM25Oracle()
+    sub.upsert_many(ids[:40], texts[:40], [{"language": "en"}] * 40)
+    for i, q in enumerate(queries):
+        want = sub.search(q, None, top_k=12)
+        got = [[ids[r], s] for r, s in zip(rows[i][:nvalid[i]], scores[i][:nvalid[i]])]
+        assert got == [[w["id"], w["score"]] for w in want], q
+
+
+def test_bm25_zero_division(eng):
+    b = eng.BM25Index()
+    with pytest.raises(ZeroDivisionError):
+        b.build(np.zeros(0, np.int32), np.zeros(3, np.int64), 5)
+
+
+def test_bm25_device_build_matches_host_build(eng, corpus):
+    import torch
+    toks = [orc.tokenize(t, "en") for t in corpus["texts"]]
+    ids, vocab = _term_ids(toks)
+    off = np.zeros(len(ids) + 1, np.int64)
+    off[1:] = np.cumsum([len(x) for x in ids])
+    flat = np.concatenate(ids)
+    bh = eng.BM25Index()
+    bh.build(flat, off, len(vocab))
+    bd = eng.BM25Index()
+    bd.build_dev(torch.from_numpy(flat).cuda(), torch.from_numpy(off).cuda(), len(vocab))
+    assert bh.stats() == bd.stats()
+    assert bh.num_postings == bd.num_postings
+    qs = [[vocab.get(t, -1) for t in orc.tokenize(q, "en")] for q in corpus["qtexts"]]
+    s1, r1, _ = bh.search(qs, 10)
+    s2, r2, _ = bd.search(qs, 10)
+    assert np.array_equal(r1, r2) and np.array_equal(s1, s2)
+    # unfiltered device path == host path
+    qoff = np.zeros(len(qs) + 1, np.int32)
+    qoff[1:] = np.cumsum([len(q) for q in qs])
+    qflat = np.concatenate([np.asarray(q, np.int32) for q in qs])
+    s3, r3 = bd.search_dev(torch.from_numpy(qflat).cuda(), torch.from_numpy(qoff).cuda(), 10)
+    torch.cuda.synchronize()
+    assert np.array_equal(r3.cpu().numpy(), r1) and np.array_equal(s3.cpu().numpy(), s1)
+
+
+def test_mmr_matches_reference_goldens(eng, corpus, golden):
+    idx = {i: n for n, i in enumerate(corpus["ids"])}
+    cands = np.stack([corpus["emb"][[idx[i] for i in c["pool"]]] for c in golden["mmr"]])
+    order = eng.mmr_order_batch(corpus["qvecs"], cands, 10, 0.5)
+    for i, c in enumerate(golden["mmr"]):
+        assert order[i].tolist() == c["order"]
+    # ragged pools and k > pool
+    nv = np.array([24, 5, 1, 0] * 4, np.int32)
+    order = eng.mmr_order_batch(corpus["qvecs"], cands, 12, 0.3, n_valid=nv)
+    for i in range(16):
+        n = int(nv[i])
+        want = orc.mmr_order(corpus["qvecs"][i], cands[i][:n], list(range(n)), 12, 0.3)
+        assert order[i][: len(want)].tolist() == want
+        assert (order[i][len(want):] == -1).all()
+
+
+def test_rrf(eng, golden):
+    for case in golden["rrf"]:
+        names = {}
+        lists = [[names.setdefault(x, len(names)) for x in l] for l in case["lists"]]
+        keys, scores = eng.rrf_fuse_keys(lists, case["weights"], case["rrf_k"])
+        inv = {v: k for k, v in names.items()}
+        got = {inv[int(k)]: float(s) for k, s in zip(keys, scores)}
+        assert got == case["out"] and list(got) == list(case["out"])
+
+
+def test_meanpool_l2norm(eng):
+    import torch
+    torch.manual_seed(0)
+    for dt in (torch.float32, torch.bfloat16, torch.float16):
+        h = torch.randn(5, 37, 768, device="cuda").to(dt)
+        m = (torch.rand(5, 37, device="cuda") > 0.3).to(torch.int64)
+        m[3] = 0                                    # empty mask -> zero vector
+        out = eng.meanpool_l2norm(h, m)
+        hf, mf = h.float(), m.float().unsqueeze(-1)
+        ref = (hf * mf).sum(1) / mf.sum(1).clamp(min=1e-9)
+        ref = torch.nn.functional.normalize(ref, p=2, dim=1)
+        torch.testing.assert_close(out, ref, atol=2e-6, rtol=1e-5)
+        raw = eng.meanpool_l2norm(h, m.to(torch.int32), normalize=False)
+        torch.testing.assert_close(raw, (hf * mf).sum(1) / mf.sum(1).clamp(min=1e-9), atol=2e-6, rtol=1e-5)
