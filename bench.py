@@ -1,0 +1,432 @@
+#!/usr/bin/env python3
+"""Hybrid-retrieval benchmark on MI355X — BASELINE.json's metric:
+"hybrid queries/sec + recall@10 vs reference, 10M x 768 chunks, 1/2/4/8 GPU".
+
+Workload (BASELINE.json configs[3]; weak scaling for configs[4]): every GPU
+owns a shard of --docs-per-gpu synthetic chunks (default 10M): 768-d unit fp32
+embeddings and BM25 postings (vocabulary 2^20, Zipf 1.07 term draws, chunk
+length ~ Poisson(120)).  One step = one batch of B queries through the whole
+hot path, inputs resident in HBM:
+
+  E5-base query encode (PyTorch-ROCm bf16 forward, random-init weights + HIP
+  mean-pool/L2, K6) -> dense cosine top-24 over the shard (K1, fp32 MFMA)
+  -> MMR to 10 (K4) -> BM25 top-10 (K2/K3, fp64) -> [N>1: RCCL all-gather of
+  per-shard top-k + merge, pool embeddings all-reduce] -> RRF fusion (K5).
+
+value = queries/s of the whole job (each query searches all N x shard chunks).
+The CPU baseline is the oracle (oracle/) run on this host on a bounded sample
+of the same queries over the same shard; recall@10 compares the GPU's final
+top-10 with the oracle's.
+
+  python bench.py [--gpus N --steps K --warmup W] [--mode hybrid|dense|ingest]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+from pathlib import Path
+
+REPO = Path(__file__).resolve().parent
+for _p in (str(REPO), str(REPO / "classmate-rag_amd")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+METRIC = "hybrid queries/sec + recall@10 vs reference, 10M×768 chunks, 1/2/4/8 GPU"
+PEAK_F32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 matrix (dense)
+PEAK_HBM_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E spec
+
+
+def parse_args():
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--mode", choices=["hybrid", "dense", "ingest"], default="hybrid")
+    ap.add_argument("--docs-per-gpu", type=int, default=10_000_000)
+    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--k", type=int, default=10)
+    ap.add_argument("--pool", type=int, default=24)
+    ap.add_argument("--dim", type=int, default=768)
+    ap.add_argument("--vocab", type=int, default=1 << 20)
+    ap.add_argument("--zipf", type=float, default=1.07)
+    ap.add_argument("--avg-len", type=float, default=120.0)
+    ap.add_argument("--q-terms", type=int, default=8)
+    ap.add_argument("--q-tokens", type=int, default=24)
+    ap.add_argument("--e5-layers", type=int, default=12)
+    ap.add_argument("--no-e5", action="store_true", help="use perturbed corpus rows as query embeddings")
+    ap.add_argument("--seq-len", type=int, default=256, help="ingest mode: tokens per chunk")
+    ap.add_argument("--cpu-baseline", type=int, default=1)
+    ap.add_argument("--cpu-queries", type=int, default=64)
+    ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--out", default=None, help="also write the JSON line to this file")
+    return ap.parse_args()
+
+
+def log(*a):
+    if int(os.environ.get("RANK", "0")) == 0:
+        print("[bench]", *a, file=sys.stderr, flush=True)
+
+
+# ---------------------------------------------------------------------------
+# synthetic shard
+# ---------------------------------------------------------------------------
+def gen_dense(dense, n, dim, seed, chunk=1 << 20):
+    import torch
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    for r0 in range(0, n, chunk):
+        m = min(chunk, n - r0)
+        x = torch.randn(m, dim, device="cuda", generator=g)
+        x /= x.norm(dim=1, keepdim=True)
+        dense.upsert_dev(x, r0)
+        del x
+    torch.cuda.synchronize()
+
+
+def gen_tokens(n, vocab, s, avg_len, seed, chunk=1 << 27):
+    import torch
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    lens = torch.poisson(torch.full((n,), float(avg_len), device="cuda"), generator=g).clamp_(min=1).to(torch.int64)
+    doc_off = torch.zeros(n + 1, dtype=torch.int64, device="cuda")
+    torch.cumsum(lens, 0, out=doc_off[1:])
+    ntok = int(doc_off[-1].item())
+    p = 1.0 / torch.arange(1, vocab + 1, dtype=torch.float64, device="cuda").pow(s)
+    cdf = torch.cumsum(p, 0)
+    cdf /= cdf[-1].clone()
+    tokens = torch.empty(ntok, dtype=torch.int32, device="cuda")
+    for t0 in range(0, ntok, chunk):
+        m = min(chunk, ntok - t0)
+        u = torch.rand(m, dtype=torch.float64, device="cuda", generator=g)
+        tokens[t0:t0 + m] = torch.searchsorted(cdf, u).clamp_(max=vocab - 1).to(torch.int32)
+        del u
+    return tokens, doc_off
+
+
+def sample_query_terms(tokens, doc_off, B, q_terms, seed):
+    import torch
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    n = doc_off.numel() - 1
+    tgt = torch.randint(0, n, (B,), device="cuda", generator=g)
+    lo = doc_off[tgt]
+    ln = doc_off[tgt + 1] - lo
+    pos = (torch.rand(B, q_terms, device="cuda", generator=g) * ln.unsqueeze(1)).long()
+    return tokens[lo.unsqueeze(1) + pos].contiguous()           # (B, q_terms) int32
+
+
+# ---------------------------------------------------------------------------
+def main():
+    args = parse_args()
+    import numpy as np
+    import torch
+    from classmate_hip import engine, parallel
+
+    rank, ws = parallel.init_from_env()
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if args.gpus != ws:
+        log(f"note: --gpus {args.gpus} but WORLD_SIZE={ws}; using {ws}")
+    if args.mode == "ingest":
+        return run_ingest(args, rank, ws, dev)
+
+    B, K, P, D = args.batch, args.k, args.pool, args.dim
+    N = args.docs_per_gpu
+    row0 = rank * N
+    t_setup = time.perf_counter()
+    dense = engine.DenseIndex(D, device=local, capacity=N)
+    gen_dense(dense, N, D, seed=args.seed * 1000 + rank)
+    log(f"dense shard {N}x{D} fp32 ready ({time.perf_counter() - t_setup:.1f}s)")
+
+    bm25 = None
+    if args.mode == "hybrid":
+        tokens, doc_off = gen_tokens(N, args.vocab, args.zipf, args.avg_len, seed=args.seed * 1000 + 500 + rank)
+        bm25 = engine.BM25Index(device=local)
+        bm25.build_dev(tokens, doc_off, args.vocab)
+        torch.cuda.synchronize()
+        if ws > 1:   # global statistics (df / N / length sums / first-occurrence order)
+            df, fk = bm25.term_stats()
+            st = bm25.stats()
+            gdf, gfk, gn, gsum = parallel.allreduce_bm25_stats(df, fk, row0, st["n_live"], st["sum_len"])
+            idf, eps = parallel.bm25_idf_table(gdf, gfk, gn)
+            bm25.set_stats(idf, gn, gsum, eps)
+        qt = sample_query_terms(tokens, doc_off, B, args.q_terms, seed=args.seed * 7 + 3)
+        if ws > 1:
+            torch.distributed.broadcast(qt, src=0)
+        q_terms = qt.reshape(-1).contiguous()
+        q_off = (torch.arange(B + 1, device=dev, dtype=torch.int32) * args.q_terms).contiguous()
+        del tokens, doc_off
+        torch.cuda.empty_cache()
+        log(f"bm25 shard: {bm25.num_postings} postings, V={args.vocab} ({time.perf_counter() - t_setup:.1f}s)")
+
+    # queries
+    use_e5 = not args.no_e5 and args.mode == "hybrid"
+    emb = None
+    if use_e5:
+        from classmate_hip.embeddings import E5MultilingualEmbedder
+        emb = E5MultilingualEmbedder.random_init(seed=0, device=str(dev), num_layers=args.e5_layers)
+        g = torch.Generator(device="cuda").manual_seed(args.seed * 13)
+        ids = torch.randint(5, 250002, (B, args.q_tokens), device=dev, generator=g)
+        ids[:, 0] = 0
+        ids[:, -1] = 2
+        mask = torch.ones_like(ids)
+        qbuf = torch.empty((B, D), dtype=torch.float32, device=dev)
+    else:
+        g = torch.Generator(device="cuda").manual_seed(args.seed * 17)
+        qfix = torch.randn(B, D, device=dev, generator=g)
+        qfix /= qfix.norm(dim=1, keepdim=True)
+
+    # buffers (allocated once: the step is allocation-free on our side)
+    dws = torch.empty(dense.workspace_bytes(B, P), dtype=torch.uint8, device=dev)
+    dout = (torch.empty((B, P), dtype=torch.float32, device=dev), torch.empty((B, P), dtype=torch.int64, device=dev))
+    vbuf = torch.empty((B * P, D), dtype=torch.float32, device=dev)
+    obuf = torch.empty((B, K), dtype=torch.int32, device=dev)
+    if bm25 is not None:
+        bws = torch.empty(bm25.workspace_bytes(B, q_terms.numel(), K), dtype=torch.uint8, device=dev)
+        bout = (torch.empty((B, K), dtype=torch.float64, device=dev), torch.empty((B, K), dtype=torch.int64, device=dev))
+    ev = []
+
+    def step(record=False):
+        if use_e5:
+            q = emb.encode_token_ids(ids, mask, out=qbuf)
+        else:
+            q = qfix
+        e = [torch.cuda.Event(enable_timing=True) for _ in range(4)] if record else None
+        if record:
+            e[0].record()
+        d, r = dense.search_dev(q, P, out=dout, workspace=dws)
+        if record:
+            e[1].record()
+        if args.mode == "dense":
+            if record:
+                ev.append(e)
+            return r
+        if ws > 1:
+            rg = torch.where(r >= 0, r + row0, r)
+            d, rg = parallel.merge_dense_topk(d, rg, P)
+            rloc = torch.where((rg >= row0) & (rg < row0 + N), rg - row0, torch.full_like(rg, -1))
+            vecs = dense.gather_dev(rloc.reshape(-1), out=vbuf).view(B, P, D)
+            vecs = parallel.assemble_pool_vectors(rg, vecs, row0, N)
+        else:
+            rg = r
+            vecs = dense.gather_dev(r.reshape(-1), out=vbuf).view(B, P, D)
+        order = engine.mmr_dev(q, vecs, K, 0.5, out=obuf)
+        o = order.long().clamp(min=0)
+        vk = torch.gather(rg, 1, o)
+        vd = torch.gather(d, 1, o)
+        vn = (order >= 0).sum(1, dtype=torch.int32)
+        if record:
+            e[2].record()
+        bs, br = bm25.search_dev(q_terms, q_off, K, out=bout, workspace=bws)
+        if record:
+            e[3].record()
+            ev.append(e)
+        if ws > 1:
+            brg = torch.where(br >= 0, br + row0, br)
+            bs, brg = parallel.merge_bm25_topk(bs, brg, K)
+        else:
+            brg = br
+        bn = (brg >= 0).sum(1, dtype=torch.int32)
+        return engine.rrf_merge_dev(vk.contiguous(), vd.contiguous(), vn, brg.contiguous(), bs.contiguous(), bn,
+                                    w_vec=1.0, w_bm25=1.0, rrf_k=60, top_k=K)
+
+    for _ in range(args.warmup):
+        res = step()
+    torch.cuda.synchronize()
+    if ws > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        res = step(record=True)
+    torch.cuda.synchronize()
+    if ws > 1:
+        torch.distributed.barrier()
+    elapsed = time.perf_counter() - t0
+    elapsed = parallel.max_over_ranks(elapsed, device=dev)
+    dense_ms = sum(e[0].elapsed_time(e[1]) for e in ev) / len(ev)
+    bm25_ms = sum(e[2].elapsed_time(e[3]) for e in ev) / len(ev) if args.mode == "hybrid" else None
+    qps = B * args.steps / elapsed
+    log(f"{args.steps} steps in {elapsed:.3f}s -> {qps:.1f} q/s; dense kernel {dense_ms:.3f} ms/launch"
+        + (f", bm25 {bm25_ms:.3f} ms/launch" if bm25_ms is not None else ""))
+
+    # roofline of the dominant kernel: dense cosine top-k (K1)
+    flops = 2.0 * N * D * B
+    bytes_ = N * D * 4 + N * 4 + B * D * 4
+    mfma_bound = flops / (PEAK_F32_MFMA_TFLOPS * 1e12) >= bytes_ / (PEAK_HBM_GBS * 1e9)
+    traffic = _pmc_traffic(args)
+    if mfma_bound:
+        roof = dict(bound="mfma", achieved=flops / (dense_ms * 1e-3) / 1e12, peak=PEAK_F32_MFMA_TFLOPS,
+                    unit="TFLOP/s")
+    else:
+        roof = dict(bound="hbm", achieved=bytes_ / (dense_ms * 1e-3) / 1e9, peak=PEAK_HBM_GBS, unit="GB/s")
+    roof["frac"] = roof["achieved"] / roof["peak"]
+    roof["traffic"] = traffic
+    roof["kernel"] = "dense_topk_kernel (K1) via cm_dense_search_dev"
+    roof["algorithmic_per_launch"] = dict(flops=flops, bytes=bytes_, rows=N, queries=B, dim=D)
+    roof["avg_launch_ms"] = dense_ms
+
+    out = {
+        "metric": METRIC if args.mode == "hybrid" else f"dense cosine top-{P} queries/sec, {N}x{D} fp32",
+        "value": qps, "unit": "queries/s", "n_gpus": ws, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "f32",
+        "dtypes": {"dense_knn": "f32 (MFMA)", "bm25": "f64", "e5_forward": "bf16" if use_e5 else None,
+                   "fusion": "f64"},
+        "data": "synthetic (seeded): unit-norm Gaussian chunk embeddings, Zipf BM25 postings, random-init "
+                "E5-base weights (no checkpoint offline)",
+        "config": {"workload": ("hybrid retrieve: E5 query encode + cosine top-24 + MMR-10 + BM25 top-10 + RRF "
+                                "top-10" if args.mode == "hybrid" else "dense cosine top-k"),
+                   "chunks_per_gpu": N, "chunks_total": N * ws, "dim": D, "global_batch": B, "k": K, "pool": P,
+                   "bm25_vocab": args.vocab, "zipf_s": args.zipf, "chunk_len_mean": args.avg_len,
+                   "query_terms": args.q_terms, "e5_query_tokens": args.q_tokens if use_e5 else None,
+                   "parallelism": f"corpus-shard x{ws}"},
+        "breakdown_ms": {"dense_search": dense_ms, "bm25_search": bm25_ms},
+        "roofline": roof,
+    }
+    if rank == 0 and ws == 1 and args.cpu_baseline and args.mode == "hybrid":
+        cpu, recall = cpu_baseline_and_recall(args, dense, bm25, res, q_terms, emb, ids if use_e5 else None,
+                                              mask if use_e5 else None, qfix if not use_e5 else None)
+        out["cpu_baseline"] = cpu
+        out["recall_at_10"] = recall
+    else:
+        out["cpu_baseline"] = None
+        out["recall_at_10"] = None
+    out["setup_s"] = time.perf_counter() - t_setup
+    if rank == 0:
+        line = json.dumps(out)
+        print(line, flush=True)
+        if args.out:
+            Path(args.out).write_text(line + "\n")
+    if ws > 1:
+        torch.distributed.destroy_process_group()
+
+
+def _pmc_traffic(args):
+    """HBM bytes per K1 launch from a committed rocprofv3 --pmc summary of this config (or None)."""
+    p = REPO / "profiles" / "pmc_dense_traffic.json"
+    try:
+        d = json.loads(p.read_text())
+        key = f"{args.docs_per_gpu}x{args.dim}_B{args.batch}"
+        return d.get(key)
+    except Exception:
+        return None
+
+
+# ---------------------------------------------------------------------------
+def cpu_baseline_and_recall(args, dense, bm25, res, q_terms, emb, ids, mask, qfix):
+    """Time the CPU oracle on a bounded sample of the same queries over the same shard; recall@10."""
+    import numpy as np
+    import torch
+    from oracle import corc
+    from oracle import ref_semantics as orc
+
+    Qc = min(args.cpu_queries, args.batch)
+    K, P = args.k, args.pool
+    with torch.inference_mode():
+        q = emb.encode_token_ids(ids[:Qc], mask[:Qc]) if emb is not None else qfix[:Qc]
+    qh = q.float().cpu().numpy()
+    qt = q_terms.view(args.batch, -1)[:Qc].cpu().numpy()
+    gpu_keys = res[0][:Qc].cpu().numpy()
+    t = time.perf_counter()
+    C = dense.export()                                  # host copy of the shard (not timed)
+    csr = bm25.export()
+    log(f"cpu baseline: exported shard to host ({time.perf_counter() - t:.1f}s)")
+    term_off = csr["term_off"]
+    df = np.diff(term_off)
+    first = np.full(df.shape[0], np.uint64(0xFFFFFFFFFFFFFFFF))
+    nz = df > 0
+    fp = term_off[:-1][nz]
+    first[nz] = (csr["post_doc"][fp].astype(np.uint64) << np.uint64(32)) | csr["post_pos"][fp].astype(np.uint64)
+    ccsr = dict(term_off=term_off, post_doc=csr["post_doc"], post_tf=csr["post_tf"], dl=csr["dl"],
+                vocab=int(df.shape[0]), ndocs=int(csr["dl"].shape[0]))
+    n_docs = ccsr["ndocs"]
+    avgdl = float(csr["dl"].astype(np.int64).sum()) / n_docs
+    idf, _ = corc.bm25_idf(df, first, n_docs)          # statistics: build-time, not timed
+
+    threads = max(corc.num_threads(), torch.get_num_threads())
+    t0 = time.perf_counter()
+    # dense: fp32 BLAS scan for candidates, exact fp64 re-rank (oracle semantics: 1 - cos, ties -> lower row)
+    sims = C @ qh.T                                    # (N, Qc)
+    cand = np.argpartition(-sims, 4 * P, axis=0)[: 4 * P].T
+    dense_rows, dense_dist = [], []
+    for i in range(Qc):
+        c = np.sort(cand[i])
+        cv = C[c].astype(np.float64)
+        d = 1.0 - (cv @ qh[i].astype(np.float64)) / np.linalg.norm(cv, axis=1) / np.linalg.norm(qh[i])
+        o = np.lexsort((c, d))[:P]
+        dense_rows.append(c[o])
+        dense_dist.append(d[o])
+    t_dense = time.perf_counter() - t0
+    t1 = time.perf_counter()
+    bs, br = corc.bm25_topk(ccsr, idf, avgdl, [list(x) for x in qt], K)
+    t_bm25 = time.perf_counter() - t1
+    t2 = time.perf_counter()
+    cpu_keys = []
+    for i in range(Qc):
+        pool = C[dense_rows[i]]
+        order = orc.mmr_order(qh[i], pool, list(range(P)), K, 0.5)
+        vec_ids = [int(dense_rows[i][j]) for j in order]
+        bm_ids = [int(x) for x in br[i] if x >= 0]
+        fused = orc.rrf_fuse(rank_lists=[vec_ids, bm_ids], weights=[1.0, 1.0], rrf_k=60)
+        vdist = {int(dense_rows[i][j]): float(np.float32(dense_dist[i][j])) for j in order}
+        items = list(dict.fromkeys(vec_ids + bm_ids))
+        items.sort(key=lambda x: (fused[x], -vdist.get(x, 0.0)), reverse=True)
+        cpu_keys.append(items[:K])
+    t_fuse = time.perf_counter() - t2
+    total = time.perf_counter() - t0
+    recall = float(np.mean([len(set(cpu_keys[i]) & set(int(x) for x in gpu_keys[i] if x >= 0)) / K
+                            for i in range(Qc)]))
+    full_n = args.docs_per_gpu
+    cpu = dict(value=Qc / total, unit="queries/s", cores=int(threads), kind="port",
+               sample=f"{Qc} of the {args.batch} queries of one step over the full {full_n}-chunk shard "
+                      f"(dense: numpy fp32 BLAS scan + fp64 re-rank; BM25: oracle/cm_oracle.c OpenMP; "
+                      f"MMR/RRF: oracle/ref_semantics.py; E5 encode excluded)",
+               seconds=total, breakdown_s=dict(dense=t_dense, bm25=t_bm25, mmr_rrf=t_fuse))
+    log(f"cpu baseline {cpu['value']:.2f} q/s on {threads} threads; recall@10 {recall:.4f}")
+    return cpu, recall
+
+
+# ---------------------------------------------------------------------------
+def run_ingest(args, rank, ws, dev):
+    """configs[2]: E5-base batch encode (bf16 forward + HIP mean-pool/L2), chunks/s."""
+    import torch
+    from classmate_hip import parallel
+    from classmate_hip.embeddings import E5MultilingualEmbedder
+    emb = E5MultilingualEmbedder.random_init(seed=0, device=str(dev), num_layers=args.e5_layers)
+    B, S = args.batch, args.seq_len
+    g = torch.Generator(device="cuda").manual_seed(args.seed + rank)
+    ids = torch.randint(5, 250002, (B, S), device=dev, generator=g)
+    ids[:, 0] = 0
+    ids[:, -1] = 2
+    mask = torch.ones_like(ids)
+    out = torch.empty((B, 768), dtype=torch.float32, device=dev)
+    for _ in range(args.warmup):
+        emb.encode_token_ids(ids, mask, out=out)
+    torch.cuda.synchronize()
+    if ws > 1:
+        torch.distributed.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        emb.encode_token_ids(ids, mask, out=out)
+    torch.cuda.synchronize()
+    if ws > 1:
+        torch.distributed.barrier()
+    el = parallel.max_over_ranks(time.perf_counter() - t0, device=dev)
+    flops_seq = args.e5_layers * (24 * S * 768 ** 2 + 4 * S * S * 768)
+    val = B * ws * args.steps / el
+    res = {"metric": "E5-base ingest encode chunks/sec (forward + HIP mean-pool/L2)", "value": val,
+           "unit": "chunks/s", "n_gpus": ws, "steps": args.steps, "warmup": args.warmup,
+           "ms_per_step": el / args.steps * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+           "dtype": "bf16", "data": "synthetic token ids, random-init E5-base weights",
+           "config": {"workload": "E5-base encode", "global_batch": B * ws, "seq_len": S,
+                      "parallelism": f"replicas x{ws}"},
+           "achieved_tflops": val * flops_seq / 1e12}
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()

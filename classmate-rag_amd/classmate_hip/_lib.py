@@ -63,6 +63,7 @@ SIGNATURES = {
     "cm_dense_search": (c_int, c_vp, c_vp, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp),
     "cm_dense_search_workspace": (c_i64, c_vp, c_i32, c_i32),
     "cm_dense_search_dev": (c_int, c_vp, c_vp, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp),
+    "cm_dense_export": (c_int, c_vp, c_i64, c_i64, c_vp, c_vp),
     "cm_dense_gather_dev": (c_int, c_vp, c_vp, c_i64, c_vp, c_vp),
     "cm_dense_live_bits_dev": (c_vp, c_vp),
     "cm_bm25_create": (c_int, c_int, P(c_vp)),
@@ -72,6 +73,9 @@ SIGNATURES = {
     "cm_bm25_num_docs": (c_i64, c_vp),
     "cm_bm25_num_postings": (c_i64, c_vp),
     "cm_bm25_stats": (c_int, c_vp, P(c_i64), P(c_i64), P(c_f64), P(c_f64)),
+    "cm_bm25_export": (c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp),
+    "cm_bm25_term_stats": (c_int, c_vp, c_vp, c_vp),
+    "cm_bm25_set_stats": (c_int, c_vp, c_vp, c_i32, c_i64, c_i64, c_f64),
     "cm_bm25_search": (c_int, c_vp, c_vp, c_vp, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp),
     "cm_bm25_search_workspace": (c_i64, c_vp, c_i32, c_i32, c_i32),
     "cm_bm25_search_dev": (c_int, c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp, c_i64, c_vp),

@@ -1,0 +1,159 @@
+"""E5 embedder on PyTorch-ROCm with the HIP pooling epilogue.
+
+Replaces ``rag.embeddings.E5MultilingualEmbedder`` (rag/embeddings/__init__.py:45-105):
+same constructor arguments, ``query: `` / ``passage: `` prefixes, batch 32,
+mean pooling over the attention mask and L2 normalisation, fp32 numpy output.
+
+* The XLM-R (E5-base: 12 layers, d=768, 12 heads, FFN 3072, vocab 250002)
+  forward runs in PyTorch-ROCm (bf16 by default; SDPA attention).
+* Mean-pool + L2-normalise is the hand-written HIP kernel K6
+  (``cm_meanpool_l2norm``), reading the bf16 hidden states in place.
+
+Weights: ``model_name`` may be a local directory with a Hugging Face
+checkpoint (config + weights + tokenizer) or a hub id already present in the
+local HF cache; nothing is downloaded.  ``E5MultilingualEmbedder.random_init()``
+builds the same architecture with seeded random weights and a deterministic
+hashing tokenizer — what the benchmark uses offline (embedding parity with the
+real E5 weights is therefore unpinned; the pooling kernel is pinned against a
+torch fp32 reference).
+"""
+from __future__ import annotations
+
+import hashlib
+import os
+import re
+from typing import Iterable, List, Optional
+
+import numpy as np
+
+from .. import engine
+
+E5_BASE_CONFIG = dict(vocab_size=250002, hidden_size=768, num_hidden_layers=12, num_attention_heads=12,
+                      intermediate_size=3072, max_position_embeddings=514, type_vocab_size=1,
+                      layer_norm_eps=1e-5, pad_token_id=1, bos_token_id=0, eos_token_id=2)
+MAX_SEQ_LEN = 512  # sentence-transformers max_seq_length of multilingual-e5-base
+
+
+class HashTokenizer:
+    """Deterministic offline stand-in for the XLM-R sentencepiece tokenizer.
+
+    Words -> stable ids in [5, vocab) via blake2b; <s>=0, </s>=2, <pad>=1.
+    Only used with random-init weights (no real vocabulary is available)."""
+
+    def __init__(self, vocab_size: int = 250002):
+        self.vocab_size = vocab_size
+        self._re = re.compile(r"\w+|[^\w\s]", re.UNICODE)
+
+    def encode(self, text: str, max_len: int = MAX_SEQ_LEN) -> List[int]:
+        ids = [0]
+        for w in self._re.findall(text or ""):
+            h = int.from_bytes(hashlib.blake2b(w.encode("utf-8"), digest_size=8).digest(), "little")
+            ids.append(5 + h % (self.vocab_size - 5))
+        ids = ids[: max_len - 1] + [2]
+        return ids
+
+    def __call__(self, texts: List[str], max_len: int = MAX_SEQ_LEN):
+        enc = [self.encode(t, max_len) for t in texts]
+        s = max(len(e) for e in enc)
+        ids = np.ones((len(enc), s), np.int64)
+        mask = np.zeros((len(enc), s), np.int64)
+        for i, e in enumerate(enc):
+            ids[i, : len(e)] = e
+            mask[i, : len(e)] = 1
+        return ids, mask
+
+
+class E5MultilingualEmbedder:
+    def __init__(self, model_name: str = "intfloat/multilingual-e5-base", device: Optional[str] = None,
+                 normalize: bool = True, dtype: str = "bfloat16", _model=None, _tokenizer=None):
+        import torch
+        self.normalize = bool(normalize)
+        self.model_name = model_name
+        self.device = torch.device(device or ("cuda" if torch.cuda.is_available() else "cpu"))
+        if self.device.type != "cuda":
+            raise RuntimeError("E5MultilingualEmbedder needs a ROCm GPU (the pooling epilogue is a HIP kernel)")
+        self.dtype = getattr(torch, dtype)
+        if _model is None:
+            _model, _tokenizer = self._load(model_name)
+        self.model = _model.to(self.device, self.dtype).eval()
+        self.tokenizer = _tokenizer
+        self._graphs = {}
+
+    # ------------------------------------------------------------------
+    @staticmethod
+    def _load(model_name: str):
+        from transformers import AutoModel, AutoTokenizer
+        local = os.path.isdir(model_name)
+        kw = dict(local_files_only=True)
+        try:
+            tok = AutoTokenizer.from_pretrained(model_name, **kw)
+            model = AutoModel.from_pretrained(model_name, attn_implementation="sdpa", **kw)
+        except Exception as e:  # no network: only local checkpoints work
+            raise RuntimeError(f"cannot load {model_name!r} from local files ({'dir' if local else 'HF cache'}): {e}."
+                               " Use E5MultilingualEmbedder.random_init() for offline benchmarking.") from e
+        return model, tok
+
+    @classmethod
+    def random_init(cls, seed: int = 0, device: Optional[str] = None, normalize: bool = True,
+                    dtype: str = "bfloat16", num_layers: int = 12):
+        """E5-base architecture with seeded random weights (no checkpoint available offline)."""
+        import torch
+        from transformers import XLMRobertaConfig, XLMRobertaModel
+        cfg = XLMRobertaConfig(**{**E5_BASE_CONFIG, "num_hidden_layers": num_layers})
+        cfg._attn_implementation = "sdpa"
+        torch.manual_seed(seed)
+        dev = torch.device(device or "cuda")
+        with torch.device(dev):
+            model = XLMRobertaModel(cfg, add_pooling_layer=False).to(getattr(torch, dtype))
+        return cls(model_name="random-init:xlm-roberta-base", device=str(dev), normalize=normalize, dtype=dtype,
+                   _model=model, _tokenizer=HashTokenizer(cfg.vocab_size))
+
+    # ------------------------------------------------------------------
+    @staticmethod
+    def _fmt_queries(queries: Iterable[str]) -> List[str]:
+        return [f"query: {q}" for q in queries]
+
+    @staticmethod
+    def _fmt_passages(texts: Iterable[str]) -> List[str]:
+        return [f"passage: {t}" for t in texts]
+
+    def _tokenize(self, texts: List[str]):
+        import torch
+        if isinstance(self.tokenizer, HashTokenizer):
+            ids, mask = self.tokenizer(texts)
+        else:
+            enc = self.tokenizer(texts, padding=True, truncation=True, max_length=MAX_SEQ_LEN, return_tensors="np")
+            ids, mask = enc["input_ids"], enc["attention_mask"]
+        return (torch.from_numpy(np.ascontiguousarray(ids)).to(self.device),
+                torch.from_numpy(np.ascontiguousarray(mask)).to(self.device))
+
+    def encode_token_ids(self, input_ids, attention_mask, out=None):
+        """Device path: (B,S) int ids + mask on the GPU -> (B,768) fp32 unit rows on the GPU."""
+        import torch
+        with torch.inference_mode():
+            hidden = self.model(input_ids=input_ids, attention_mask=attention_mask).last_hidden_state
+            return engine.meanpool_l2norm(hidden, attention_mask, self.normalize, out=out)
+
+    def _encode(self, texts: List[str], batch_size: int = 32) -> np.ndarray:
+        import torch
+        if not texts:
+            return np.zeros((0, self.model.config.hidden_size), np.float32)
+        # sentence-transformers sorts by length for batching and restores the order
+        order = np.argsort([-len(t) for t in texts], kind="stable")
+        out = np.empty((len(texts), self.model.config.hidden_size), np.float32)
+        for s in range(0, len(texts), batch_size):
+            idx = order[s: s + batch_size]
+            ids, mask = self._tokenize([texts[i] for i in idx])
+            emb = self.encode_token_ids(ids, mask)
+            out[idx] = emb.float().cpu().numpy()
+        torch.cuda.synchronize(self.device)
+        return out
+
+    def encode_queries(self, queries: Iterable[str]) -> np.ndarray:
+        return self._encode(self._fmt_queries(queries)).astype("float32", copy=False)
+
+    def encode_passages(self, texts: Iterable[str]) -> np.ndarray:
+        return self._encode(self._fmt_passages(texts)).astype("float32", copy=False)
+
+
+__all__ = ["E5MultilingualEmbedder", "HashTokenizer", "E5_BASE_CONFIG"]

@@ -122,6 +122,17 @@ class DenseIndex:
                                         L.ptr(vecs)), "cm_dense_search")
         return (dist, rows, vecs) if return_vectors else (dist, rows)
 
+    def export(self, row0: int = 0, n: Optional[int] = None, with_live: bool = False):
+        """Host copy of rows [row0, row0+n) (and their live mask)."""
+        n = self.size - row0 if n is None else int(n)
+        out = np.empty((max(n, 0), self.dim), np.float32)
+        live = np.zeros(max((n + 31) // 32, 1), np.uint32) if with_live else None
+        L.check(L.fn["cm_dense_export"](self._h, int(row0), n, L.ptr(out), L.ptr(live)), "cm_dense_export")
+        if not with_live:
+            return out
+        mask = np.unpackbits(live.view(np.uint8), bitorder="little")[:n].astype(bool)
+        return out, mask
+
     def workspace_bytes(self, nq: int, k: int) -> int:
         n = int(L.fn["cm_dense_search_workspace"](self._h, int(nq), int(k)))
         if n < 0:
@@ -204,6 +215,32 @@ class BM25Index:
         a, e = C.c_double(), C.c_double()
         L.check(L.fn["cm_bm25_stats"](self._h, C.byref(n), C.byref(s), C.byref(a), C.byref(e)), "cm_bm25_stats")
         return dict(n_live=n.value, sum_len=s.value, avgdl=a.value, eps=e.value)
+
+    def export(self):
+        """Host copy of the CSR index: dict(term_off, post_doc, post_tf, post_pos, dl)."""
+        v, p, n = self.vocab, self.num_postings, self.num_docs
+        out = dict(term_off=np.empty(v + 1, np.int64), post_doc=np.empty(max(p, 1), np.int32),
+                   post_tf=np.empty(max(p, 1), np.uint16), post_pos=np.empty(max(p, 1), np.uint32),
+                   dl=np.empty(max(n, 1), np.int32))
+        L.check(L.fn["cm_bm25_export"](self._h, *[L.ptr(out[k]) for k in ("term_off", "post_doc", "post_tf",
+                                                                          "post_pos", "dl")]), "cm_bm25_export")
+        for k in ("post_doc", "post_tf", "post_pos"):
+            out[k] = out[k][:p]
+        out["dl"] = out["dl"][:n]
+        return out
+
+    def term_stats(self):
+        """Local (df[V] int32, first_key[V] uint64 = row << 32 | first position, ~0 if absent)."""
+        df = np.zeros(max(self.vocab, 1), np.int32)
+        fk = np.zeros(max(self.vocab, 1), np.uint64)
+        L.check(L.fn["cm_bm25_term_stats"](self._h, L.ptr(df), L.ptr(fk)), "cm_bm25_term_stats")
+        return df[: self.vocab], fk[: self.vocab]
+
+    def set_stats(self, idf: np.ndarray, n_live: int, sum_len: int, eps: float):
+        """Install corpus-wide statistics (sharded index: every rank scores with the global idf/avgdl)."""
+        v = _c(idf, np.float64)
+        L.check(L.fn["cm_bm25_set_stats"](self._h, L.ptr(v), int(v.shape[0]), int(n_live), int(sum_len), float(eps)),
+                "cm_bm25_set_stats")
 
     def search(self, queries: Sequence[Sequence[int]], k: int, allow_bits: Optional[np.ndarray] = None):
         """queries: per query a list of term ids (-1 unknown). -> scores f64 (nq,k), rows i64, n i32."""

@@ -1,0 +1,192 @@
+"""Multi-GPU sharding of the hybrid retrieval path.
+
+One process per GPU (torch.distributed; backend "nccl" == RCCL over xGMI on
+ROCm, "gloo" for the CPU tests).  The corpus is sharded by chunk: rank r owns
+global rows [row0_r, row0_r + n_r).  Exchanges, and only these:
+
+* build time — BM25 statistics: all-reduce SUM of df[V], N and total length,
+  all-reduce MIN of each term's first (global row, position) key, so every rank
+  computes the same idf table (including rank_bm25's epsilon floor, averaged in
+  the reference's first-occurrence order) and avgdl;
+* per query batch — all-gather of each shard's top-k (dense: distance + global
+  row; BM25: score + global row), then a deterministic merge identical on all
+  ranks; the MMR pool's embeddings are assembled with one all-reduce SUM (each
+  rank contributes the rows it owns, zeros elsewhere).
+
+The merges are torch ops so they run on either backend; the per-shard search is
+the HIP path (classmate_hip.engine).
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional, Tuple
+
+import numpy as np
+
+try:
+    import torch
+    import torch.distributed as dist
+except Exception:  # pragma: no cover
+    torch = None
+    dist = None
+
+EMPTY_U64 = np.uint64(0xFFFFFFFFFFFFFFFF)
+
+
+def world() -> Tuple[int, int]:
+    if dist is not None and dist.is_available() and dist.is_initialized():
+        return dist.get_rank(), dist.get_world_size()
+    return 0, 1
+
+
+# ---------------------------------------------------------------------------
+# BM25 global statistics
+# ---------------------------------------------------------------------------
+def bm25_idf_table(df: np.ndarray, first_key: np.ndarray, n_live: int):
+    """rank_bm25 idf for every term from global df and first-occurrence keys.
+
+    Returns (idf[V] float64, eps).  Terms are visited in ascending first_key
+    order (== the reference's dict insertion order) for the idf average; the
+    logs are CPython's math.log (glibc), like rank_bm25."""
+    present = np.nonzero(df > 0)[0]
+    order = present[np.argsort(first_key[present], kind="stable")]
+    idf = np.zeros(df.shape[0], np.float64)
+    idf_sum = 0.0
+    neg = []
+    log = math.log
+    for t in order.tolist():
+        d = int(df[t])
+        v = log(n_live - d + 0.5) - log(d + 0.5)
+        idf[t] = v
+        idf_sum += v
+        if v < 0:
+            neg.append(t)
+    if len(order) == 0:
+        raise ZeroDivisionError("float division by zero")
+    eps = 0.25 * (idf_sum / len(order))
+    if neg:
+        idf[np.asarray(neg)] = eps
+    return idf, eps
+
+
+def allreduce_bm25_stats(df: np.ndarray, first_key: np.ndarray, row0: int, n_live: int, sum_len: int,
+                         group=None):
+    """Combine per-shard term statistics into the global ones (identity when world == 1)."""
+    fk = first_key.astype(np.uint64).copy()
+    present = fk != EMPTY_U64
+    fk[present] += np.uint64(row0) << np.uint64(32)
+    rank, ws = world()
+    if ws == 1:
+        return df.astype(np.int64), fk, int(n_live), int(sum_len)
+    t_df = torch.from_numpy(df.astype(np.int64))
+    # keys fit in int63 (rows < 2^31): compare as int64, absent = int64 max
+    t_fk = torch.from_numpy(np.where(present, fk, np.uint64(2**63 - 1)).astype(np.int64))
+    t_n = torch.tensor([n_live, sum_len], dtype=torch.int64)
+    dev = _coll_device(group)
+    t_df, t_fk, t_n = t_df.to(dev), t_fk.to(dev), t_n.to(dev)
+    dist.all_reduce(t_df, op=dist.ReduceOp.SUM, group=group)
+    dist.all_reduce(t_fk, op=dist.ReduceOp.MIN, group=group)
+    dist.all_reduce(t_n, op=dist.ReduceOp.SUM, group=group)
+    fk_g = t_fk.cpu().numpy().astype(np.uint64)
+    fk_g[fk_g == np.uint64(2**63 - 1)] = EMPTY_U64
+    n = t_n.cpu().numpy()
+    return t_df.cpu().numpy(), fk_g, int(n[0]), int(n[1])
+
+
+def _coll_device(group=None):
+    backend = dist.get_backend(group)
+    if backend == "nccl":
+        return torch.device("cuda", torch.cuda.current_device())
+    return torch.device("cpu")
+
+
+# ---------------------------------------------------------------------------
+# Per-batch merges
+# ---------------------------------------------------------------------------
+def f32_order_key(dist_t, rows_t):
+    """(dist f32, row i64) -> int64 sort key, ascending == (dist asc, row asc); -1 rows -> max."""
+    b = dist_t.contiguous().view(torch.int32).to(torch.int64) & 0xFFFFFFFF
+    neg = (b & 0x80000000) != 0
+    ordered = torch.where(neg, (~b) & 0xFFFFFFFF, b | 0x80000000)
+    # rows < 2^31; use 31 bits for the row, so the key stays a positive int64 when shifted by 31
+    key = (ordered << 31) | (rows_t & 0x7FFFFFFF)
+    return torch.where(rows_t < 0, torch.full_like(key, torch.iinfo(torch.int64).max), key)
+
+
+def merge_dense_topk(dist_t, rows_t, k: int, group=None):
+    """All-gather per-shard (B,k) (distance, global row) and keep the global top-k."""
+    _, ws = world()
+    if ws == 1:
+        return dist_t[:, :k], rows_t[:, :k]
+    dl = [torch.empty_like(dist_t) for _ in range(ws)]
+    rl = [torch.empty_like(rows_t) for _ in range(ws)]
+    dist.all_gather(dl, dist_t.contiguous(), group=group)
+    dist.all_gather(rl, rows_t.contiguous(), group=group)
+    D = torch.cat(dl, 1)
+    R = torch.cat(rl, 1)
+    key = f32_order_key(D, R)
+    _, idx = torch.sort(key, dim=1)
+    idx = idx[:, :k]
+    return torch.gather(D, 1, idx), torch.gather(R, 1, idx)
+
+
+def merge_bm25_topk(score_t, rows_t, k: int, group=None):
+    """All-gather per-shard (B,k) (score f64, global row) -> global top-k by (score desc, row asc)."""
+    _, ws = world()
+    if ws == 1:
+        return score_t[:, :k], rows_t[:, :k]
+    sl = [torch.empty_like(score_t) for _ in range(ws)]
+    rl = [torch.empty_like(rows_t) for _ in range(ws)]
+    dist.all_gather(sl, score_t.contiguous(), group=group)
+    dist.all_gather(rl, rows_t.contiguous(), group=group)
+    S = torch.cat(sl, 1)
+    R = torch.cat(rl, 1)
+    big = torch.iinfo(torch.int64).max
+    Rk = torch.where(R < 0, torch.full_like(R, big), R)
+    S = S + 0.0                                   # -0.0 == 0.0 like Python
+    Sk = torch.where(R < 0, torch.full_like(S, -math.inf), S)
+    i1 = torch.argsort(Rk, dim=1, stable=True)   # row asc ...
+    S1 = torch.gather(Sk, 1, i1)
+    i2 = torch.argsort(-S1, dim=1, stable=True)  # ... then score desc (stable keeps row order)
+    idx = torch.gather(i1, 1, i2)[:, :k]
+    return torch.gather(score_t.new_tensor(torch.cat(sl, 1)), 1, idx), torch.gather(R, 1, idx)
+
+
+def assemble_pool_vectors(rows_t, local_vecs, row0: int, n_local: int, group=None):
+    """Pool embeddings for global rows: owner rank contributes, others zeros; SUM all-reduce."""
+    _, ws = world()
+    own = (rows_t >= row0) & (rows_t < row0 + n_local)
+    out = torch.where(own.unsqueeze(-1), local_vecs, torch.zeros_like(local_vecs))
+    if ws > 1:
+        dist.all_reduce(out, op=dist.ReduceOp.SUM, group=group)
+    return out
+
+
+def max_over_ranks(x: float, device=None, group=None) -> float:
+    _, ws = world()
+    if ws == 1:
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    return float(t.item())
+
+
+def shard_range(n_total: int, rank: int, ws: int) -> Tuple[int, int]:
+    per = (n_total + ws - 1) // ws
+    lo = min(rank * per, n_total)
+    return lo, min(lo + per, n_total) - lo
+
+
+def init_from_env(backend: Optional[str] = None):
+    """torch.distributed init for torchrun (MASTER_ADDR/PORT, RANK, WORLD_SIZE)."""
+    import os
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    if ws <= 1 or dist.is_initialized():
+        return world()
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    if backend is None:
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+    if backend == "nccl":
+        torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
+    dist.init_process_group(backend=backend)
+    return world()

@@ -508,7 +508,7 @@ int cm_bm25_create(int device, cm_bm25 **out) {
   if (!dg.ok) CM_FAIL(CM_EDEVICE, "cannot select device " + std::to_string(device));
   cm_bm25 *h = new cm_bm25();
   h->dev = device;
-  if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
+  if (hipStreamCreateWithFlags(&h->stream, hipStreamDefault) != hipSuccess) {
     delete h;
     CM_FAIL(CM_EDEVICE, "hipStreamCreate failed");
   }
@@ -638,7 +638,7 @@ int cm_bm25_build_dev(cm_bm25 *h, const int32_t *term_ids_dev, const int64_t *do
   if (ndocs <= 0 || ntokens < 0 || vocab <= 0) CM_FAIL(CM_EINVAL, "bad arguments");
   if (ndocs >= (int64_t)INT32_MAX) CM_FAIL(CM_EINVAL, "too many docs for one shard");
   DeviceGuard dg(h->dev);
-  hipStream_t st = stream ? (hipStream_t)stream : h->stream;
+  hipStream_t st = (hipStream_t)stream;  // NULL = the null stream (torch default)
   int rc;
   // scratch: keys in/out (u64), pos in/out (u32), flags
   DevBuf keys_a, keys_b, pos_a, pos_b, ukeys, counts, runstart, nruns_d, flags, df_d, cub_tmp, firstk;
@@ -779,6 +779,58 @@ int cm_bm25_build_dev(cm_bm25 *h, const int32_t *term_ids_dev, const int64_t *do
   return CM_OK;
 }
 
+int cm_bm25_term_stats(cm_bm25 *h, int32_t *df_out, uint64_t *first_out) {
+  if (!h || !df_out || !first_out) CM_FAIL(CM_EINVAL, "NULL argument");
+  if (h->vocab <= 0) return CM_OK;
+  DeviceGuard dg(h->dev);
+  const int32_t V = h->vocab;
+  int rc;
+  if ((rc = h->obuf.ensure((size_t)V * 16))) return rc;
+  uint64_t *fk = h->obuf.as<uint64_t>();
+  hipLaunchKernelGGL(first_key_kernel, dim3((unsigned)ceil_div(V, 256)), dim3(256), 0, h->stream,
+                     h->term_off.as<int64_t>(), h->post_doc.as<int32_t>(), h->post_pos.as<uint32_t>(), V, fk);
+  CM_HIP(hipGetLastError());
+  std::vector<int64_t> off((size_t)V + 1);
+  CM_HIP(hipMemcpyAsync(off.data(), h->term_off.ptr, ((size_t)V + 1) * 8, hipMemcpyDeviceToHost, h->stream));
+  CM_HIP(hipMemcpyAsync(first_out, fk, (size_t)V * 8, hipMemcpyDeviceToHost, h->stream));
+  CM_HIP(hipStreamSynchronize(h->stream));
+  for (int32_t t = 0; t < V; ++t) df_out[t] = (int32_t)(off[t + 1] - off[t]);
+  return CM_OK;
+}
+
+int cm_bm25_export(cm_bm25 *h, int64_t *term_off, int32_t *post_doc, uint16_t *post_tf, uint32_t *post_pos,
+                   int32_t *dl) {
+  if (!h) CM_FAIL(CM_EINVAL, "null handle");
+  DeviceGuard dg(h->dev);
+  if (term_off) CM_HIP(hipMemcpyAsync(term_off, h->term_off.ptr, ((size_t)h->vocab + 1) * 8, hipMemcpyDeviceToHost, h->stream));
+  if (h->npost) {
+    if (post_doc) CM_HIP(hipMemcpyAsync(post_doc, h->post_doc.ptr, (size_t)h->npost * 4, hipMemcpyDeviceToHost, h->stream));
+    if (post_tf) CM_HIP(hipMemcpyAsync(post_tf, h->post_tf.ptr, (size_t)h->npost * 2, hipMemcpyDeviceToHost, h->stream));
+    if (post_pos) CM_HIP(hipMemcpyAsync(post_pos, h->post_pos.ptr, (size_t)h->npost * 4, hipMemcpyDeviceToHost, h->stream));
+  }
+  if (dl && h->ndocs) CM_HIP(hipMemcpyAsync(dl, h->dl.ptr, (size_t)h->ndocs * 4, hipMemcpyDeviceToHost, h->stream));
+  CM_HIP(hipStreamSynchronize(h->stream));
+  return CM_OK;
+}
+
+int cm_bm25_set_stats(cm_bm25 *h, const double *idf, int32_t vocab, int64_t n_live, int64_t sum_len, double eps) {
+  if (!h || !idf) CM_FAIL(CM_EINVAL, "NULL argument");
+  if (vocab != h->vocab) CM_FAIL(CM_EINVAL, "vocab mismatch");
+  if (n_live <= 0 || sum_len <= 0) CM_FAIL(CM_EINVAL, "n_live and sum_len must be > 0");
+  DeviceGuard dg(h->dev);
+  h->idf_host.assign(idf, idf + vocab);
+  h->n_live = n_live;
+  h->sum_len = sum_len;
+  h->avgdl = (double)sum_len / (double)n_live;
+  h->eps = eps;
+  h->empty_vocab = false;
+  int rc = h->idf.ensure((size_t)std::max(vocab, 1) * 8);
+  if (rc) return rc;
+  CM_HIP(hipMemcpyAsync(h->idf.ptr, idf, (size_t)vocab * 8, hipMemcpyHostToDevice, h->stream));
+  CM_HIP(hipStreamSynchronize(h->stream));
+  return CM_OK;
+}
+
 int64_t cm_bm25_search_workspace(cm_bm25 *h, int32_t nq, int32_t total_terms, int32_t k) {
   if (!h || nq < 0 || total_terms < 0 || k <= 0) return -1;
   return (int64_t)bm_ws_layout(h, nq, total_terms, k, nullptr).total;
@@ -793,7 +845,7 @@ int cm_bm25_search_dev(cm_bm25 *h, const int32_t *q_terms_dev, const int32_t *q_
   if (h->ndocs == 0) CM_FAIL(CM_EINVAL, "empty BM25 index");
   if (h->empty_vocab) CM_FAIL(CM_EZERODIV, "float division by zero");
   DeviceGuard dg(h->dev);
-  hipStream_t st = stream ? (hipStream_t)stream : h->stream;
+  hipStream_t st = (hipStream_t)stream;  // NULL = the null stream (torch default)
   BmWs w = bm_ws_layout(h, nq, total_terms, k, workspace_dev);
   if (!workspace_dev || (int64_t)w.total > workspace_bytes) CM_FAIL(CM_EINVAL, "bm25 workspace too small");
   if (total_terms > 0) {

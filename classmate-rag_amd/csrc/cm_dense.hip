@@ -533,7 +533,7 @@ int cm_dense_create(int device, int32_t dim, int64_t capacity, cm_dense **out) {
   int ld = (int)round_up(dim, 128);
   while (!pick_chunk(ld)) ld += 128;
   h->ld = ld;
-  if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
+  if (hipStreamCreateWithFlags(&h->stream, hipStreamDefault) != hipSuccess) {
     delete h;
     CM_FAIL(CM_EDEVICE, "hipStreamCreate failed");
   }
@@ -602,7 +602,7 @@ int cm_dense_upsert_dev(cm_dense *h, const float *vecs_dev, int64_t row0, int64_
   if (n < 0 || row0 < 0 || row0 + n >= (int64_t)0xffffffffll) CM_FAIL(CM_EINVAL, "bad row range");
   if (n == 0) return CM_OK;
   DeviceGuard dg(h->dev);
-  hipStream_t st = stream ? (hipStream_t)stream : h->stream;
+  hipStream_t st = (hipStream_t)stream;  // NULL = the null stream (torch default)
   if (row0 + n > h->rows_alloc) {
     CM_HIP(hipStreamSynchronize(st));
     int rc = dense_grow(h, row0 + n);
@@ -677,7 +677,7 @@ int cm_dense_search_dev(cm_dense *h, const float *q_dev, int32_t nq, int32_t k, 
   if (nq <= 0) return CM_OK;
   if (k <= 0 || k > kMaxTopK) CM_FAIL(CM_EINVAL, "k must be in [1, " + std::to_string(kMaxTopK) + "]");
   DeviceGuard dg(h->dev);
-  hipStream_t st = stream ? (hipStream_t)stream : h->stream;
+  hipStream_t st = (hipStream_t)stream;  // NULL = the null stream (torch default)
   DenseCfg c = dense_config(h, nq, k);
   if (c.lds > 163840) CM_FAIL(CM_EUNSUPPORTED, "dim/k too large for the LDS-resident query tile");
   DenseWs w = dense_ws_layout(h, c, nq, k, workspace_dev);
@@ -697,10 +697,32 @@ int cm_dense_gather_dev(cm_dense *h, const int64_t *rows_dev, int64_t n, float *
   if (!h) CM_FAIL(CM_EINVAL, "null handle");
   if (n <= 0) return CM_OK;
   DeviceGuard dg(h->dev);
-  hipStream_t st = stream ? (hipStream_t)stream : h->stream;
+  hipStream_t st = (hipStream_t)stream;  // NULL = the null stream (torch default)
   hipLaunchKernelGGL(dense_gather_kernel, dim3((unsigned)n), dim3(256), 0, st, h->C, h->ld, h->dim, rows_dev, n,
                      h->size, out_dev);
   CM_HIP(hipGetLastError());
+  return CM_OK;
+}
+
+int cm_dense_export(cm_dense *h, int64_t row0, int64_t n, float *out, uint32_t *live_out) {
+  if (!h) CM_FAIL(CM_EINVAL, "null handle");
+  if (row0 < 0 || n < 0 || row0 + n > h->size) CM_FAIL(CM_EINVAL, "row range out of bounds");
+  if (n == 0) return CM_OK;
+  DeviceGuard dg(h->dev);
+  if (out) {
+    if (h->ld == h->dim) {
+      CM_HIP(hipMemcpyAsync(out, h->C + row0 * h->ld, (size_t)n * h->dim * 4, hipMemcpyDeviceToHost, h->stream));
+    } else {
+      CM_HIP(hipMemcpy2DAsync(out, (size_t)h->dim * 4, h->C + row0 * h->ld, (size_t)h->ld * 4, (size_t)h->dim * 4,
+                              (size_t)n, hipMemcpyDeviceToHost, h->stream));
+    }
+  }
+  if (live_out) {
+    if (row0 % 32) CM_FAIL(CM_EINVAL, "live export needs row0 % 32 == 0");
+    CM_HIP(hipMemcpyAsync(live_out, h->live + row0 / 32, (size_t)ceil_div(n, 32) * 4, hipMemcpyDeviceToHost,
+                          h->stream));
+  }
+  CM_HIP(hipStreamSynchronize(h->stream));
   return CM_OK;
 }
 

@@ -235,7 +235,7 @@ HostStage &stage() {
     s.buf.release();
     if (s.st) (void)hipStreamDestroy(s.st);
     s.st = nullptr;
-    (void)hipStreamCreateWithFlags(&s.st, hipStreamNonBlocking);
+    (void)hipStreamCreateWithFlags(&s.st, hipStreamDefault);
     s.dev = dev;
   }
   return s;

@@ -12,9 +12,11 @@
  *     SURVEY.md §8a quirk Q7), everything else to RuntimeError.
  *   - "host" functions take caller-owned host arrays, run on the handle's
  *     own HIP stream and return after the results are copied back.
- *   - "_dev" functions take device pointers plus a hipStream_t (as void*,
- *     NULL = the handle's stream); they never allocate, never synchronise,
- *     and are safe to capture into a HIP graph.
+ *   - "_dev" functions take device pointers plus a hipStream_t (as void*;
+ *     NULL = the null/default stream, which is torch's default stream too);
+ *     they never allocate, never synchronise, and are safe to capture into a
+ *     HIP graph.  Handles' private streams (host functions) are blocking, so
+ *     they are ordered after work queued on the null stream.
  *   - rows are int64 row indices into the handle's storage; "-1" pads
  *     results that have fewer than k entries.
  *   - allow bitmaps: bit (r & 31) of word r >> 5 set => row r may be
@@ -87,6 +89,9 @@ int64_t cm_dense_search_workspace(cm_dense *h, int32_t nq, int32_t k);
 int cm_dense_search_dev(cm_dense *h, const float *q_dev, int32_t nq, int32_t k, const uint32_t *allow_dev,
                         float *dist_dev, int64_t *row_dev, void *workspace_dev, int64_t workspace_bytes,
                         void *stream);
+/* copy rows [row0, row0+n) to host (n x dim fp32) and/or their live bits
+ * (row0 % 32 == 0; ceil(n/32) words).  Persistence and verification. */
+int cm_dense_export(cm_dense *h, int64_t row0, int64_t n, float *out, uint32_t *live_out);
 /* gather stored rows (row < 0 => zeros): out_dev n x dim. */
 int cm_dense_gather_dev(cm_dense *h, const int64_t *rows_dev, int64_t n, float *out_dev, void *stream);
 /* device pointer of the live bitmap (ceil(size/32) words) for callers that
@@ -117,6 +122,16 @@ int64_t cm_bm25_num_docs(cm_bm25 *h);
 int64_t cm_bm25_num_postings(cm_bm25 *h);
 /* unfiltered corpus statistics: live docs, total length, avgdl, eps. */
 int cm_bm25_stats(cm_bm25 *h, int64_t *n_live, int64_t *sum_len, double *avgdl, double *eps);
+/* Sharding support: local df per term and the first posting's
+ * (row << 32 | first position) key (0xff..ff when absent), so ranks can
+ * all-reduce df (sum) and first keys (min, after offsetting rows) and agree
+ * on the reference's dict order; then install the global statistics. */
+/* copy the device index to host (any pointer may be NULL): term_off[V+1],
+ * post_doc/post_tf/post_pos[P], dl[N]. */
+int cm_bm25_export(cm_bm25 *h, int64_t *term_off, int32_t *post_doc, uint16_t *post_tf, uint32_t *post_pos,
+                   int32_t *dl);
+int cm_bm25_term_stats(cm_bm25 *h, int32_t *df_out, uint64_t *first_out);
+int cm_bm25_set_stats(cm_bm25 *h, const double *idf, int32_t vocab, int64_t n_live, int64_t sum_len, double eps);
 /* BM25Store.search (bm25.py:175-212) batched: nq queries whose term ids
  * (host, -1 = unknown term) are q_terms[q_off[i] .. q_off[i+1]) in query
  * token order (duplicates count twice).  Candidates = live docs with the
