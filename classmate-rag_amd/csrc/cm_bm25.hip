@@ -34,10 +34,14 @@
 
 namespace cm {
 
-constexpr int kRange = 4096;       // docs per K2 workgroup
-constexpr int kBmThreads = 256;
-constexpr int kSlots = kRange / kBmThreads;  // 16 slots per thread
-constexpr int kQG = 8;             // queries per K2 workgroup
+constexpr int kRange = 1024;                 // docs per range (one wave's LDS score tile)
+constexpr int kBmThreads = 256;              // 4 waves = 4 queries per K2 workgroup
+constexpr int kQPerBlock = kBmThreads / 64;
+constexpr int kSlots = kRange / 64;          // docs per lane in a range (s = u*64 + lane)
+constexpr int kBatch = 16;                   // postings per lane in flight
+constexpr int kBoundsGroup = 64;             // ranges per bounds thread (gallop between them)
+constexpr int kMergeThreads = 1024;
+constexpr int kMergePer = 16;                // lists per merge thread -> <= 16384 ranges (16.7M docs)
 
 struct PairKey {  // (k, r) lexicographic; smaller is better
   uint64_t k;
@@ -47,8 +51,7 @@ __device__ inline bool pk_less(uint64_t ka, uint32_t ra, uint64_t kb, uint32_t r
   return ka < kb || (ka == kb && ra < rb);
 }
 
-// Block-wide argmin of (key,row) over kBmThreads threads. Returns in all threads.
-__device__ inline PairKey block_min_pair(uint64_t key, uint32_t row, uint64_t *sk, uint32_t *sr) {
+__device__ inline void wave_min_pair(uint64_t &key, uint32_t &row) {
   for (int o = 32; o > 0; o >>= 1) {
     const uint64_t ok = __shfl_xor(key, o);
     const uint32_t orr = __shfl_xor(row, o);
@@ -57,6 +60,11 @@ __device__ inline PairKey block_min_pair(uint64_t key, uint32_t row, uint64_t *s
       row = orr;
     }
   }
+}
+
+// Block-wide argmin of (key,row); sk/sr hold one entry per wave. Returns in all threads.
+__device__ inline PairKey block_min_pair(uint64_t key, uint32_t row, uint64_t *sk, uint32_t *sr) {
+  wave_min_pair(key, row);
   const int w = threadIdx.x >> 6;
   if ((threadIdx.x & 63) == 0) {
     sk[w] = key;
@@ -86,33 +94,58 @@ __global__ void bm25_qidf_kernel(const int32_t *__restrict__ q_terms, int n, con
 }
 
 // bounds[i*(nr+1)+r] = first posting of term q_terms[i] with doc >= r*kRange.
-__global__ void bm25_bounds_kernel(const int32_t *__restrict__ q_terms, int n_terms, int32_t vocab, int nr,
-                                   const int64_t *__restrict__ term_off, const int32_t *__restrict__ post_doc,
-                                   int64_t *__restrict__ bounds) {
-  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int64_t per = nr + 1;
-  if (gid >= (int64_t)n_terms * per) return;
-  const int i = (int)(gid / per);
-  const int r = (int)(gid - (int64_t)i * per);
-  const int32_t t = q_terms[i];
-  if (t < 0 || t >= vocab) {
-    bounds[gid] = 0;
-    return;
-  }
-  int64_t lo = term_off[t], hi = term_off[t + 1];
-  if (r == nr) {
-    bounds[gid] = hi;
-    return;
-  }
-  const int32_t target = r * kRange;
+// One thread per (term, group of kBoundsGroup ranges): binary search for the
+// first range of the group, then gallop forward (bounds are monotone in r).
+__device__ inline int64_t lower_bound_doc(const int32_t *__restrict__ post_doc, int64_t lo, int64_t hi, int32_t target) {
   while (lo < hi) {
     const int64_t mid = (lo + hi) >> 1;
     if (post_doc[mid] < target) lo = mid + 1;
     else hi = mid;
   }
-  bounds[gid] = lo;
+  return lo;
 }
 
+__global__ void bm25_bounds_kernel(const int32_t *__restrict__ q_terms, int n_terms, int32_t vocab, int nr,
+                                   const int64_t *__restrict__ term_off, const int32_t *__restrict__ post_doc,
+                                   int64_t *__restrict__ bounds) {
+  const int ngroups = (nr + 1 + kBoundsGroup - 1) / kBoundsGroup;
+  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= (int64_t)n_terms * ngroups) return;
+  const int i = (int)(gid / ngroups);
+  const int g = (int)(gid - (int64_t)i * ngroups);
+  const int32_t t = q_terms[i];
+  int64_t *out = bounds + (int64_t)i * (nr + 1);
+  const int r0 = g * kBoundsGroup;
+  const int r1 = min(r0 + kBoundsGroup, nr + 1);
+  if (t < 0 || t >= vocab) {
+    for (int r = r0; r < r1; ++r) out[r] = 0;
+    return;
+  }
+  const int64_t lo_t = term_off[t], hi_t = term_off[t + 1];
+  int64_t pos = r0 >= nr ? hi_t : lower_bound_doc(post_doc, lo_t, hi_t, r0 * kRange);
+  out[r0] = pos;
+  for (int r = r0 + 1; r < r1; ++r) {
+    if (r == nr) {
+      pos = hi_t;
+    } else {
+      const int32_t target = r * kRange;
+      if (pos < hi_t && post_doc[pos] < target) {
+        int64_t lo = pos, step = 1;
+        while (lo + step < hi_t && post_doc[lo + step] < target) {
+          lo += step;
+          step <<= 1;
+        }
+        pos = lower_bound_doc(post_doc, lo + 1, min(lo + step, hi_t), target);
+      }
+    }
+    out[r] = pos;
+  }
+}
+
+// K2: one workgroup per (range of kRange docs, 4 queries); one wave per query.
+// The wave accumulates its query's terms in order into an LDS fp64 tile (no
+// block barriers: a wave's LDS operations are in order), with kBatch postings
+// per lane in flight, then selects the range's top-k by wave argmin rounds.
 template <typename TF>
 __global__ void __launch_bounds__(kBmThreads)
     bm25_range_kernel(const int32_t *__restrict__ q_off, int nq, const double *__restrict__ q_idf,
@@ -120,14 +153,12 @@ __global__ void __launch_bounds__(kBmThreads)
                       const TF *__restrict__ post_tf, const int32_t *__restrict__ dl, const uint32_t *__restrict__ live,
                       const uint32_t *__restrict__ allow, int64_t ndocs, double avgdl, int k,
                       uint64_t *__restrict__ cand_key, uint32_t *__restrict__ cand_row) {
-  __shared__ double score[kRange];
   __shared__ double kd[kRange];
-  __shared__ uint32_t okbits[kRange / 32];
-  __shared__ uint64_t sk[4];
-  __shared__ uint32_t sr[4];
-  const int r = blockIdx.x;
+  __shared__ double score_all[kQPerBlock][kRange];
+  const int r = blockIdx.y;  // queries fastest: every query group of a range runs together (L2 reuse)
   const int64_t d0 = (int64_t)r * kRange;
   const int tid = threadIdx.x;
+  const int lane = tid & 63;
   for (int s = tid; s < kRange; s += kBmThreads) {
     const int64_t d = d0 + s;
     double v = 0.0;
@@ -139,88 +170,115 @@ __global__ void __launch_bounds__(kBmThreads)
     }
     kd[s] = v;
   }
-  for (int w = tid; w < kRange / 32; w += kBmThreads) {
-    const int64_t gw = d0 / 32 + w;
-    uint32_t b = 0;
-    if (gw * 32 < ndocs) {
-      b = live[gw] & (allow ? allow[gw] : 0xffffffffu);
-      const int64_t rem = ndocs - gw * 32;
-      if (rem < 32) b &= (1u << rem) - 1u;
+  uint32_t okmask = 0;  // bit u: doc d0 + u*64 + lane is a candidate
+#pragma unroll
+  for (int u = 0; u < kSlots; ++u) {
+    const int64_t d = d0 + u * 64 + lane;
+    if (d < ndocs) {
+      const int64_t w = d >> 5;
+      const uint32_t b = (live[w] & (allow ? allow[w] : 0xffffffffu)) >> (d & 31);
+      okmask |= (b & 1u) << u;
     }
-    okbits[w] = b;
   }
-  const int q_begin = blockIdx.y * kQG;
-  const int q_end = min(q_begin + kQG, nq);
-  for (int qi = q_begin; qi < q_end; ++qi) {
-    for (int s = tid; s < kRange; s += kBmThreads) score[s] = 0.0;
-    __syncthreads();
-    const int t0 = q_off[qi], t1 = q_off[qi + 1];
+  __syncthreads();
+  const int wave = tid >> 6;
+  const int qi = blockIdx.x * kQPerBlock + wave;
+  if (qi >= nq) return;  // no block barrier below
+  double *score = score_all[wave];
+  const int t0 = q_off[qi], t1 = q_off[qi + 1];
+  const int64_t bstride = nr + 1;
+  int64_t total = 0;
+  for (int i = t0; i < t1; ++i) total += bounds[(int64_t)i * bstride + r + 1] - bounds[(int64_t)i * bstride + r];
+  if (total > 0) {
+#pragma unroll
+    for (int u = 0; u < kSlots; ++u) score[u * 64 + lane] = 0.0;
     for (int i = t0; i < t1; ++i) {  // query tokens in order (duplicates twice)
       const double idf = q_idf[i];
-      const int64_t lo = bounds[(int64_t)i * (nr + 1) + r];
-      const int64_t hi = bounds[(int64_t)i * (nr + 1) + r + 1];
-      for (int64_t p = lo + tid; p < hi; p += kBmThreads) {
-        const int s = post_doc[p] - (int32_t)d0;
-        const double tf = (double)post_tf[p];
-        const double num = tf * 2.5;
-        const double den = tf + kd[s];
-        const double c = idf * (num / den);
-        score[s] = score[s] + c;
-      }
-      __syncthreads();
-    }
-    // top-k of this range: (score desc, row asc) over candidate rows.
-    uint32_t taken = 0;
-    const uint32_t myw = okbits[(tid * kSlots) >> 5] >> ((tid * kSlots) & 31);
-    auto local_best = [&](uint64_t &bk, uint32_t &br) {
-      bk = kEmptyKey;
-      br = 0xffffffffu;
+      const int64_t lo = bounds[(int64_t)i * bstride + r];
+      const int64_t hi = bounds[(int64_t)i * bstride + r + 1];
+      for (int64_t base = lo; base < hi; base += 64 * kBatch) {
+        int32_t dd[kBatch];
+        TF tt[kBatch];
 #pragma unroll
-      for (int u = 0; u < kSlots; ++u) {
-        if (((myw >> u) & 1u) && !((taken >> u) & 1u)) {
-          const uint64_t key = score_key(score[tid * kSlots + u]);
-          if (key < bk) {  // rows ascending within the thread: first wins ties
-            bk = key;
-            br = (uint32_t)(d0 + tid * kSlots + u);
+        for (int u = 0; u < kBatch; ++u) {
+          const int64_t p = base + u * 64 + lane;
+          dd[u] = p < hi ? post_doc[p] : -1;
+          tt[u] = p < hi ? post_tf[p] : (TF)0;
+        }
+#pragma unroll
+        for (int u = 0; u < kBatch; ++u) {
+          if (dd[u] >= 0) {
+            const int s = dd[u] - (int32_t)d0;
+            const double tf = (double)tt[u];
+            const double num = tf * 2.5;
+            const double den = tf + kd[s];
+            const double c = idf * (num / den);
+            score[s] = score[s] + c;
           }
         }
       }
-    };
-    uint64_t bk;
-    uint32_t br;
-    local_best(bk, br);
-    for (int i = 0; i < k; ++i) {
-      const PairKey best = block_min_pair(bk, br, sk, sr);
-      if (tid == 0) {
-        const int64_t o = ((int64_t)qi * nr + r) * k + i;
-        cand_key[o] = best.k;
-        cand_row[o] = best.r;
-      }
-      if (best.r != 0xffffffffu && br == best.r && bk == best.k) {
-        taken |= 1u << (best.r - (uint32_t)d0 - tid * kSlots);
-        local_best(bk, br);
+    }
+  }
+  // top-k of this (range, query): (score desc, row asc) over candidate docs
+  const uint64_t zero_key = score_key(0.0);
+  uint32_t taken = 0;
+  auto local_best = [&](uint64_t &bk, uint32_t &br) {
+    bk = kEmptyKey;
+    br = 0xffffffffu;
+#pragma unroll
+    for (int u = 0; u < kSlots; ++u) {
+      if (((okmask >> u) & 1u) && !((taken >> u) & 1u)) {
+        const uint64_t key = total > 0 ? score_key(score[u * 64 + lane]) : zero_key;
+        if (key < bk) {  // u ascending == row ascending within the lane
+          bk = key;
+          br = (uint32_t)(d0 + u * 64 + lane);
+        }
       }
     }
-    __syncthreads();
+  };
+  uint64_t bk;
+  uint32_t br;
+  local_best(bk, br);
+  for (int i = 0; i < k; ++i) {
+    uint64_t mk = bk;
+    uint32_t mr = br;
+    wave_min_pair(mk, mr);
+    if (lane == 0) {
+      const int64_t o = ((int64_t)qi * nr + r) * k + i;
+      cand_key[o] = mk;
+      cand_row[o] = mr;
+    }
+    if (mr == 0xffffffffu) {
+      // no candidates left in this range: pad the rest
+      for (int j = i + 1 + lane; j < k; j += 64) {
+        const int64_t o = ((int64_t)qi * nr + r) * k + j;
+        cand_key[o] = kEmptyKey;
+        cand_row[o] = 0xffffffffu;
+      }
+      break;
+    }
+    if (br == mr && bk == mk) {
+      taken |= 1u << ((mr - (uint32_t)d0) >> 6);
+      local_best(bk, br);
+    }
   }
 }
 
 // Tournament merge of nr sorted per-range lists per query.
-__global__ void __launch_bounds__(kBmThreads) bm25_merge_kernel(const uint64_t *__restrict__ cand_key,
-                                                                const uint32_t *__restrict__ cand_row, int nr, int k,
-                                                                double *__restrict__ out_score,
-                                                                int64_t *__restrict__ out_row) {
+__global__ void __launch_bounds__(kMergeThreads) bm25_merge_kernel(const uint64_t *__restrict__ cand_key,
+                                                                   const uint32_t *__restrict__ cand_row, int nr,
+                                                                   int k, double *__restrict__ out_score,
+                                                                   int64_t *__restrict__ out_row) {
   const int qi = blockIdx.x;
-  __shared__ uint64_t sk[4];
-  __shared__ uint32_t sr[4];
-  constexpr int kPer = 16;  // nr <= 4096 lists
-  int head[kPer];
-  uint64_t hk[kPer];
-  uint32_t hr[kPer];
+  __shared__ uint64_t sk[kMergeThreads / 64];
+  __shared__ uint32_t sr[kMergeThreads / 64];
+  int head[kMergePer];
+  uint64_t hk[kMergePer];
+  uint32_t hr[kMergePer];
   const int64_t base = (int64_t)qi * nr * k;
 #pragma unroll
-  for (int s = 0; s < kPer; ++s) {
-    const int l = threadIdx.x + kBmThreads * s;
+  for (int s = 0; s < kMergePer; ++s) {
+    const int l = threadIdx.x + kMergeThreads * s;
     head[s] = 0;
     hk[s] = kEmptyKey;
     hr[s] = 0xffffffffu;
@@ -233,7 +291,7 @@ __global__ void __launch_bounds__(kBmThreads) bm25_merge_kernel(const uint64_t *
     uint64_t mk = kEmptyKey;
     uint32_t mr = 0xffffffffu;
 #pragma unroll
-    for (int s = 0; s < kPer; ++s)
+    for (int s = 0; s < kMergePer; ++s)
       if (pk_less(hk[s], hr[s], mk, mr)) {
         mk = hk[s];
         mr = hr[s];
@@ -251,9 +309,9 @@ __global__ void __launch_bounds__(kBmThreads) bm25_merge_kernel(const uint64_t *
     }
     if (best.r == 0xffffffffu) continue;
 #pragma unroll
-    for (int s = 0; s < kPer; ++s) {
+    for (int s = 0; s < kMergePer; ++s) {
       if (hr[s] == best.r && hk[s] == best.k) {
-        const int l = threadIdx.x + kBmThreads * s;
+        const int l = threadIdx.x + kMergeThreads * s;
         head[s] += 1;
         if (head[s] < k) {
           hk[s] = cand_key[base + (int64_t)l * k + head[s]];
@@ -361,8 +419,8 @@ __global__ void bm25_postings_from_runs_kernel(const uint64_t *__restrict__ ukey
                                                const int64_t *__restrict__ run_start,
                                                const uint32_t *__restrict__ sorted_pos, int64_t nruns,
                                                int32_t *__restrict__ post_doc, uint16_t *__restrict__ post_tf,
-                                               uint32_t *__restrict__ post_pos, int32_t *__restrict__ df,
-                                               int32_t *__restrict__ tf_overflow) {
+                                               uint32_t *__restrict__ post_pos, int64_t *__restrict__ term_off,
+                                               int32_t vocab, int32_t *__restrict__ tf_overflow) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= nruns) return;
   const uint64_t key = ukeys[i];
@@ -372,7 +430,11 @@ __global__ void bm25_postings_from_runs_kernel(const uint64_t *__restrict__ ukey
   if (c > 65535) atomicOr(tf_overflow, 1);
   post_tf[i] = (uint16_t)min(c, 65535);
   post_pos[i] = sorted_pos[run_start[i]];
-  atomicAdd(&df[t], 1);
+  // CSR offsets: the first run of term t starts t's postings; fill skipped terms
+  const int32_t tp = i > 0 ? (int32_t)(ukeys[i - 1] >> 32) : -1;
+  for (int32_t x = tp + 1; x <= t; ++x) term_off[x] = i;
+  if (i == nruns - 1)
+    for (int32_t x = t + 1; x <= vocab; ++x) term_off[x] = nruns;
 }
 
 __global__ void set_all_bits_kernel(uint32_t *bits, int64_t n) {
@@ -473,19 +535,20 @@ int bm25_launch_core(cm_bm25 *h, const int32_t *q_terms_dev, const int32_t *q_of
                      const uint32_t *allow_dev, double avgdl, const BmWs &w, double *score_dev, int64_t *row_dev,
                      hipStream_t st) {
   const int nr = (int)std::max<int64_t>(1, ceil_div(h->ndocs, kRange));
-  if (nr > 16 * kBmThreads) CM_FAIL(CM_EUNSUPPORTED, "BM25 corpus too large for one shard (> 16.7M docs)");
-  const int64_t nb = (int64_t)total_terms * (nr + 1);
+  if (nr > kMergePer * kMergeThreads) CM_FAIL(CM_EUNSUPPORTED, "BM25 shard too large (> 16.7M docs)");
+  const int ngroups = (nr + 1 + kBoundsGroup - 1) / kBoundsGroup;
+  const int64_t nb = (int64_t)total_terms * ngroups;
   if (nb > 0) {
     hipLaunchKernelGGL(bm25_bounds_kernel, dim3((unsigned)ceil_div(nb, 256)), dim3(256), 0, st, q_terms_dev,
                        total_terms, h->vocab, nr, h->term_off.as<int64_t>(), h->post_doc.as<int32_t>(), w.bounds);
     CM_HIP(hipGetLastError());
   }
-  dim3 grid(nr, (unsigned)ceil_div(nq, kQG));
+  dim3 grid((unsigned)ceil_div(nq, kQPerBlock), nr);
   hipLaunchKernelGGL(bm25_range_kernel<uint16_t>, grid, dim3(kBmThreads), 0, st, q_off_dev, nq, w.q_idf, w.bounds,
                      nr, h->post_doc.as<int32_t>(), h->post_tf.as<uint16_t>(), h->dl.as<int32_t>(),
                      h->live.as<uint32_t>(), allow_dev, h->ndocs, avgdl, k, w.cand_key, w.cand_row);
   CM_HIP(hipGetLastError());
-  hipLaunchKernelGGL(bm25_merge_kernel, dim3(nq), dim3(kBmThreads), 0, st, w.cand_key, w.cand_row, nr, k,
+  hipLaunchKernelGGL(bm25_merge_kernel, dim3(nq), dim3(kMergeThreads), 0, st, w.cand_key, w.cand_row, nr, k,
                      score_dev, row_dev);
   CM_HIP(hipGetLastError());
   return CM_OK;
@@ -718,32 +781,16 @@ int cm_bm25_build_dev(cm_bm25 *h, const int32_t *term_ids_dev, const int64_t *do
   if ((rc = h->post_doc.ensure((size_t)std::max<int64_t>(nruns, 1) * 4)) ||
       (rc = h->post_tf.ensure((size_t)std::max<int64_t>(nruns, 1) * 2)) ||
       (rc = h->post_pos.ensure((size_t)std::max<int64_t>(nruns, 1) * 4)) ||
-      (rc = df_d.ensure((size_t)vocab * 4)) || (rc = h->term_off.ensure(((size_t)vocab + 1) * 8))) {
+      (rc = h->term_off.ensure(((size_t)vocab + 1) * 8))) {
     cleanup();
     return rc;
   }
-  CM_HIP(hipMemsetAsync(df_d.ptr, 0, (size_t)vocab * 4, st));
+  if (nruns == 0) CM_HIP(hipMemsetAsync(h->term_off.ptr, 0, ((size_t)vocab + 1) * 8, st));
   hipLaunchKernelGGL(bm25_postings_from_runs_kernel, dim3((unsigned)ceil_div(std::max<int64_t>(nruns, 1), 256)),
                      dim3(256), 0, st, uk, cnt, runstart.as<int64_t>(), sp, nruns, h->post_doc.as<int32_t>(),
-                     h->post_tf.as<uint16_t>(), h->post_pos.as<uint32_t>(), df_d.as<int32_t>(),
+                     h->post_tf.as<uint16_t>(), h->post_pos.as<uint32_t>(), h->term_off.as<int64_t>(), vocab,
                      flags.as<int32_t>() + 1);
   CM_HIP(hipGetLastError());
-  // term_off = exclusive scan of df (int64), last = nruns
-  {
-    size_t tmp3 = 0;
-    auto in = hipcub::TransformInputIterator<int64_t, hipcub::CastOp<int64_t>, int32_t *>(df_d.as<int32_t>(),
-                                                                                          hipcub::CastOp<int64_t>());
-    CM_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp3, in, h->term_off.as<int64_t>(), vocab, st));
-    if (tmp3 > cub_tmp.bytes) {
-      cub_tmp.release();
-      if ((rc = cub_tmp.ensure(tmp3))) {
-        cleanup();
-        return rc;
-      }
-    }
-    CM_HIP(hipcub::DeviceScan::ExclusiveSum(cub_tmp.ptr, tmp3, in, h->term_off.as<int64_t>(), vocab, st));
-    CM_HIP(hipMemcpyAsync(h->term_off.as<int64_t>() + vocab, &nruns, 8, hipMemcpyHostToDevice, st));
-  }
   const int64_t nw = std::max<int64_t>(1, ceil_div(ndocs, 32));
   if ((rc = h->live.ensure((size_t)nw * 4)) || (rc = firstk.ensure((size_t)vocab * 8))) {
     cleanup();
@@ -756,12 +803,14 @@ int cm_bm25_build_dev(cm_bm25 *h, const int32_t *term_ids_dev, const int64_t *do
                      firstk.as<uint64_t>());
   CM_HIP(hipGetLastError());
   std::vector<int32_t> df((size_t)vocab);
+  std::vector<int64_t> toff_h((size_t)vocab + 1);
   std::vector<uint64_t> fk((size_t)vocab);
-  CM_HIP(hipMemcpyAsync(df.data(), df_d.ptr, (size_t)vocab * 4, hipMemcpyDeviceToHost, st));
+  CM_HIP(hipMemcpyAsync(toff_h.data(), h->term_off.ptr, ((size_t)vocab + 1) * 8, hipMemcpyDeviceToHost, st));
   CM_HIP(hipMemcpyAsync(fk.data(), firstk.ptr, (size_t)vocab * 8, hipMemcpyDeviceToHost, st));
   CM_HIP(hipMemcpyAsync(hflags, flags.ptr, 8, hipMemcpyDeviceToHost, st));
   CM_HIP(hipStreamSynchronize(st));
   cleanup();
+  for (int32_t t = 0; t < vocab; ++t) df[t] = (int32_t)(toff_h[t + 1] - toff_h[t]);
   if (hflags[1]) CM_FAIL(CM_EUNSUPPORTED, "term frequency > 65535 in one chunk");
   std::vector<int32_t> order;
   order.reserve((size_t)vocab);

@@ -134,9 +134,12 @@ __global__ void __launch_bounds__(kThreads, 2)
   const int CPT = KS / CH;  // chunks per tile (even, checked on host)
   const int total = iters * CPT;
 
-  f32x4 acc[QT];
+  // two independent accumulation chains per query tile (even / odd k within a
+  // 16-deep step): v_mfma_f32_16x16x4_f32 has a 40-cycle dependent latency vs a
+  // 32-cycle issue interval, so back-to-back MFMAs must not share an accumulator.
+  f32x4 acc[QT][2];
 #pragma unroll
-  for (int t = 0; t < QT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int t = 0; t < QT; ++t) acc[t][0] = acc[t][1] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   auto chunk_ptr = [&](int gc) -> const float * {
     const int it = gc / CPT;
@@ -147,31 +150,46 @@ __global__ void __launch_bounds__(kThreads, 2)
   auto load = [&](f32x4 (&b)[CH], int gc) {
     const float *p = chunk_ptr(gc);
 #pragma unroll
-    for (int u = 0; u < CH; ++u) b[u] = __builtin_nontemporal_load(reinterpret_cast<const f32x4 *>(p + u * 16));
+    for (int u = 0; u < CH; ++u) b[u] = *reinterpret_cast<const f32x4 *>(p + u * 16);
   };
   auto compute = [&](const f32x4 (&b)[CH], int gc) {
     const int c = gc % CPT;
 #pragma unroll
     for (int u = 0; u < CH; ++u) {
       const int ks = c * CH + u;
+      f32x4 bq[QT];
 #pragma unroll
-      for (int t = 0; t < QT; ++t) {
-        const f32x4 bq = qfrag[(t * KS + ks) * 64 + lane];
-        acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(b[u].x, bq.x, acc[t], 0, 0, 0);
-        acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(b[u].y, bq.y, acc[t], 0, 0, 0);
-        acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(b[u].z, bq.z, acc[t], 0, 0, 0);
-        acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(b[u].w, bq.w, acc[t], 0, 0, 0);
-      }
+      for (int t = 0; t < QT; ++t) bq[t] = qfrag[(t * KS + ks) * 64 + lane];
+#pragma unroll
+      for (int t = 0; t < QT; ++t) acc[t][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(b[u].x, bq[t].x, acc[t][0], 0, 0, 0);
+#pragma unroll
+      for (int t = 0; t < QT; ++t) acc[t][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(b[u].y, bq[t].y, acc[t][1], 0, 0, 0);
+#pragma unroll
+      for (int t = 0; t < QT; ++t) acc[t][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(b[u].z, bq[t].z, acc[t][0], 0, 0, 0);
+#pragma unroll
+      for (int t = 0; t < QT; ++t) acc[t][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(b[u].w, bq[t].w, acc[t][1], 0, 0, 0);
     }
   };
-  // Epilogue of one 16-row tile: distances -> threshold filter -> LDS buffer.
-  auto epilogue = [&](int it) {
+  // Epilogue operands of a tile are loaded early (before the next chunk's
+  // prefetch) so waiting for them never drains the prefetch (vmcnt in order).
+  struct EpiOps {
+    f32x4 ic;
+    uint32_t bits;
+  };
+  auto epi_load = [&](int it) -> EpiOps {
     const int64_t row0 = r_begin + (int64_t)it * kStepRows + wave * kRowTile;
     const int64_t w = row0 >> 5;
-    uint32_t bits = 0;
-    if (w < n_words) bits = live[w] & (allow ? allow[w] : 0xffffffffu);
-    bits >>= (row0 & 31) + 4 * g;
-    const f32x4 ic = *reinterpret_cast<const f32x4 *>(invc + row0 + 4 * g);
+    EpiOps e;
+    e.bits = 0;
+    if (w < n_words) e.bits = live[w] & (allow ? allow[w] : 0xffffffffu);
+    e.ic = *reinterpret_cast<const f32x4 *>(invc + row0 + 4 * g);
+    return e;
+  };
+  // Epilogue of one 16-row tile: distances -> threshold filter -> LDS buffer.
+  auto epilogue = [&](int it, const EpiOps &e) {
+    const int64_t row0 = r_begin + (int64_t)it * kStepRows + wave * kRowTile;
+    const uint32_t bits = e.bits >> ((row0 & 31) + 4 * g);
+    const f32x4 ic = e.ic;
 #pragma unroll
     for (int t = 0; t < QT; ++t) {
       const int q = t * 16 + j;
@@ -180,7 +198,7 @@ __global__ void __launch_bounds__(kThreads, 2)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         if ((bits >> r) & 1u) {
-          const float dist = 1.0f - acc[t][r] * iq * ic[r];
+          const float dist = 1.0f - (acc[t][0][r] + acc[t][1][r]) * iq * ic[r];
           const uint64_t key = ((uint64_t)f32_order(dist) << 32) | (uint64_t)(uint32_t)(row0 + 4 * g + r);
           if (key < th) {
             const uint32_t slot = atomicAdd(&cnt[q], 1u);
@@ -188,7 +206,7 @@ __global__ void __launch_bounds__(kThreads, 2)
           }
         }
       }
-      acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+      acc[t][0] = acc[t][1] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
   };
   // One wave per query: rank-merge the buffer into the sorted list.
@@ -233,13 +251,20 @@ __global__ void __launch_bounds__(kThreads, 2)
   if (total > 0) {
     f32x4 bufA[CH], bufB[CH];
     load(bufA, 0);
+    __builtin_amdgcn_sched_barrier(0);
     for (int gc = 0; gc < total; gc += 2) {
       load(bufB, gc + 1);
+      __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of the MFMAs it overlaps
       compute(bufA, gc);
-      if (gc + 2 < total) load(bufA, gc + 2);
+      const bool tile_end = (gc + 2) % CPT == 0;
+      // unconditional (clamped) loads keep one control path, so hipcc can count
+      // the in-order vmcnt exactly for compute(bufB)
+      const EpiOps eo = epi_load((gc + 1) / CPT);
+      load(bufA, min(gc + 2, total - 1));
+      __builtin_amdgcn_sched_barrier(0);
       compute(bufB, gc + 1);
-      if ((gc + 2) % CPT == 0) {
-        epilogue((gc + 1) / CPT);
+      if (tile_end) {
+        epilogue((gc + 1) / CPT, eo);
         __syncthreads();
         merge();
         __syncthreads();
