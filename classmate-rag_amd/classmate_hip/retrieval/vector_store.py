@@ -1,0 +1,233 @@
+"""HBM-resident cosine vector store, drop-in for ``ChromaVectorStore``.
+
+Same constructor, methods and return shapes as rag/retrieval/vector_chroma.py:81-278
+(``upsert`` / ``query`` / ``count`` / ``reset_collection`` / ``from_config``);
+the Chroma client + HNSW server is replaced by ``engine.DenseIndex`` (exact
+brute-force cosine on the GPU, kernel K1).  Extra, build-side: ``query_batch``
+(many query rows at once — the reference returns row 0 only, quirk Q6),
+``save``/``load`` persistence under ``persist_dir/collection_name``.
+
+String ids, documents and metadata stay on the host; rows are assigned in
+insertion order and re-upserting an id overwrites its row in place.
+"""
+from __future__ import annotations
+
+import json
+import os
+import shutil
+from dataclasses import dataclass, field
+from pathlib import Path
+from typing import Any, Dict, List, Mapping, Optional, Sequence
+
+import numpy as np
+
+from .. import engine
+from .filters import MetaIndex, pack_bits
+
+
+@dataclass
+class GpuVectorStore:
+    persist_dir: Optional[Path] = Path("./indexes/chroma")
+    collection_name: str = "classmate_rag"
+    distance: str = "cosine"
+    device: Optional[int] = None
+    autosave: bool = True
+
+    _index: Optional[engine.DenseIndex] = field(default=None, init=False, repr=False)
+    _ids: List[Optional[str]] = field(default_factory=list, init=False, repr=False)
+    _row: Dict[str, int] = field(default_factory=dict, init=False, repr=False)
+    _docs: List[Optional[str]] = field(default_factory=list, init=False, repr=False)
+    _meta: MetaIndex = field(default_factory=MetaIndex, init=False, repr=False)
+    _loaded: bool = field(default=False, init=False, repr=False)
+
+    def __post_init__(self):
+        if self.distance != "cosine":
+            raise ValueError(f"only the 'cosine' space is implemented (got {self.distance!r})")
+        if self.persist_dir is not None:
+            self.persist_dir = Path(self.persist_dir)
+
+    # ---- persistence ----------------------------------------------------
+    @property
+    def _dir(self) -> Optional[Path]:
+        return None if self.persist_dir is None else self.persist_dir / self.collection_name
+
+    def _ensure_loaded(self):
+        if self._loaded:
+            return
+        self._loaded = True
+        d = self._dir
+        if d is not None and (d / "rows.jsonl").exists() and (d / "vectors.npy").exists():
+            self._load_from(d)
+
+    def _load_from(self, d: Path):
+        vecs = np.load(d / "vectors.npy", mmap_mode="r")
+        rows = []
+        with (d / "rows.jsonl").open("r", encoding="utf-8") as f:
+            for line in f:
+                if line.strip():
+                    rows.append(json.loads(line))
+        live = [i for i, r in enumerate(rows) if r.get("id") is not None]
+        self._index = engine.DenseIndex(int(vecs.shape[1]), device=self.device, capacity=len(rows))
+        for i, r in enumerate(rows):
+            self._ids.append(r.get("id"))
+            self._docs.append(r.get("document"))
+            if r.get("id") is not None:
+                self._row[r["id"]] = i
+                self._meta.set(i, r.get("metadata"))
+        if live:
+            idx = np.asarray(live, np.int64)
+            for s in range(0, idx.shape[0], 1 << 16):
+                part = idx[s: s + (1 << 16)]
+                self._index.upsert(np.asarray(vecs[part], np.float32), part)
+
+    def save(self):
+        """Write vectors.npy (row-aligned fp32) + rows.jsonl ({id, document, metadata} or nulls)."""
+        d = self._dir
+        if d is None or self._index is None:
+            return
+        d.mkdir(parents=True, exist_ok=True)
+        vecs = self._index.export()
+        tmp = d / "vectors.tmp.npy"
+        np.save(tmp, vecs)
+        os.replace(tmp, d / "vectors.npy")
+        with (d / "rows.tmp.jsonl").open("w", encoding="utf-8") as f:
+            for i, _id in enumerate(self._ids):
+                rec = {"id": _id, "document": self._docs[i] if _id is not None else None,
+                       "metadata": (self._meta.metas[i] if i < len(self._meta.metas) else None) if _id else None}
+                f.write(json.dumps(rec, ensure_ascii=False) + "\n")
+        os.replace(d / "rows.tmp.jsonl", d / "rows.jsonl")
+
+    # ---- upsert (vector_chroma.py:168-200) ---------------------------------
+    def upsert(self, *, ids: Sequence[str], documents: Sequence[str], metadatas: Sequence[Mapping[str, Any]],
+               embeddings: np.ndarray, batch_size: int = 512) -> None:
+        if len(ids) != len(documents) or len(ids) != len(metadatas) or len(ids) != len(embeddings):
+            raise ValueError("Lengths of ids, documents, metadatas, and embeddings must match.")
+        self._ensure_loaded()
+        if len(ids) == 0:
+            return
+        if len(set(ids)) != len(ids):
+            raise ValueError("Expected IDs to be unique within one upsert call")
+        emb = np.ascontiguousarray(np.asarray(embeddings, dtype=np.float32))
+        if emb.ndim != 2:
+            raise ValueError("embeddings must be a 2-D array (n, dim)")
+        if self._index is None:
+            self._index = engine.DenseIndex(emb.shape[1], device=self.device, capacity=len(ids))
+        elif emb.shape[1] != self._index.dim:
+            raise ValueError(f"Embedding dimension {emb.shape[1]} does not match collection dimensionality "
+                             f"{self._index.dim}")
+        rows = np.empty(len(ids), np.int64)
+        for i, _id in enumerate(ids):
+            r = self._row.get(_id)
+            if r is None:
+                r = len(self._ids)
+                self._ids.append(_id)
+                self._docs.append(None)
+                self._row[_id] = r
+            rows[i] = r
+            self._docs[r] = documents[i]
+            self._meta.set(r, metadatas[i])
+        self._index.upsert(emb, rows)
+        if self.autosave:
+            self.save()
+
+    def delete(self, ids: Sequence[str]) -> None:
+        """col.delete(ids=...) (vector_chroma.py:181-187); unknown ids are ignored."""
+        self._ensure_loaded()
+        rows = [self._row.pop(i) for i in ids if i in self._row]
+        if not rows:
+            return
+        for r in rows:
+            self._ids[r] = None
+            self._docs[r] = None
+            self._meta.remove(r)
+        self._index.delete(np.asarray(rows, np.int64))
+        if self.autosave:
+            self.save()
+
+    # ---- query (vector_chroma.py:204-253) ------------------------------------
+    def _search(self, q: np.ndarray, where, top_k: int, include_embeddings: bool):
+        if top_k is None or int(top_k) <= 0:
+            raise ValueError(f"Expected n_results to be a positive integer, got {top_k}")
+        self._ensure_loaded()
+        if self._index is None:
+            return None
+        if where:
+            mask = self._meta.chroma_mask(where)
+            allow, n_ok = pack_bits(mask), int(mask.sum())
+        else:
+            allow, n_ok = None, self._index.live_count()
+        k = min(int(top_k), n_ok)
+        if k <= 0:
+            return None
+        if k > engine.L.max_topk():
+            raise ValueError(f"top_k={top_k} exceeds the GPU top-k limit {engine.L.max_topk()}")
+        return self._index.search(q, k, allow, return_vectors=include_embeddings)
+
+    def _items(self, dist, rows, vecs, i, include_documents, include_embeddings) -> List[Dict[str, Any]]:
+        out = []
+        for j in range(rows.shape[1]):
+            r = int(rows[i, j])
+            if r < 0:
+                break
+            item = {"id": self._ids[r], "document": self._docs[r] if include_documents else None,
+                    "metadata": self._meta.metas[r],
+                    "distance": float(dist[i, j])}
+            if include_embeddings:
+                item["embedding"] = np.array(vecs[i, j], dtype="float32")
+            out.append(item)
+        return out
+
+    def query(self, *, query_embeddings: np.ndarray, where: Optional[Dict[str, Any]] = None, top_k: int = 8,
+              include_documents: bool = True, include_embeddings: bool = False) -> List[Dict[str, Any]]:
+        q = np.asarray(query_embeddings).astype("float32")
+        if q.ndim == 1:
+            q = q[None, :]
+        res = self._search(q[:1], where, top_k, include_embeddings)   # row 0 only, like the reference
+        if res is None:
+            return []
+        dist, rows = res[0], res[1]
+        vecs = res[2] if include_embeddings else None
+        return self._items(dist, rows, vecs, 0, include_documents, include_embeddings)
+
+    def query_batch(self, *, query_embeddings: np.ndarray, where: Optional[Dict[str, Any]] = None, top_k: int = 8,
+                    include_documents: bool = True, include_embeddings: bool = False) -> List[List[Dict[str, Any]]]:
+        q = np.atleast_2d(np.asarray(query_embeddings).astype("float32"))
+        res = self._search(q, where, top_k, include_embeddings)
+        if res is None:
+            return [[] for _ in range(q.shape[0])]
+        dist, rows = res[0], res[1]
+        vecs = res[2] if include_embeddings else None
+        return [self._items(dist, rows, vecs, i, include_documents, include_embeddings) for i in range(q.shape[0])]
+
+    # ---- admin ------------------------------------------------------------------
+    def count(self) -> int:
+        self._ensure_loaded()
+        try:
+            return 0 if self._index is None else self._index.live_count()
+        except Exception:
+            return 0
+
+    def reset_collection(self) -> None:
+        self._ensure_loaded()
+        if self._index is not None:
+            self._index.close()
+        self._index = None
+        self._ids, self._row, self._docs = [], {}, []
+        self._meta = MetaIndex()
+        d = self._dir
+        if d is not None and d.exists():
+            shutil.rmtree(d, ignore_errors=True)
+
+    @classmethod
+    def from_config(cls) -> "GpuVectorStore":
+        """Same settings as the reference (rag/config.py:75-76,179-180), read from the environment."""
+        return cls(persist_dir=Path(os.getenv("CHROMA_PERSIST_DIRECTORY", "./indexes/chroma") or "./indexes/chroma"),
+                   collection_name=os.getenv("CHROMA_COLLECTION_NAME", "classmate_rag") or "classmate_rag",
+                   distance="cosine")
+
+    # rows <-> ids for the batched device pipeline
+    def id_of(self, row: int) -> Optional[str]:
+        return self._ids[row]
+
+
+ChromaVectorStore = GpuVectorStore

@@ -1,0 +1,151 @@
+"""Drop-in API parity on the GPU: the classmate_hip.retrieval classes, used the
+way rag/pipeline/rag.py and rag/admin/inspect.py use the reference classes,
+must reproduce the reference-generated goldens (tests/golden/hybrid_1k.json).
+
+Bars: BM25 ids + fp64 scores identical; RRF fused scores identical; vector
+ids identical with distances within 1e-4 (exact brute force vs the reference's
+HNSW-free exact stand-in); MMR orders identical.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-4
+FILTERS = {
+    "none": None,
+    "course_cs101": {"course": "cs101", "unit": None, "author": None, "semester": None,
+                     "source_path": None, "created_at": None},
+    "course_only": {"course": "math201"},
+    "tags_exam": {"course": "cs101", "tags": ["exam"]},
+    "lang_en_doctype": {"language": "en", "doc_type": "pptx"},
+}
+
+
+class PresetEmbedder:
+    def __init__(self, qtexts, qvecs):
+        self.t = dict(zip(qtexts, qvecs))
+
+    def encode_queries(self, qs):
+        return np.stack([self.t[q] for q in qs]).astype(np.float32)
+
+
+@pytest.fixture(scope="module")
+def stores(corpus, tmp_path_factory):
+    from classmate_hip.retrieval import BM25Store, GpuVectorStore
+    d = tmp_path_factory.mktemp("idx")
+    vs = GpuVectorStore(persist_dir=d / "chroma")
+    vs.upsert(ids=corpus["ids"], documents=corpus["texts"], metadatas=corpus["metas"], embeddings=corpus["emb"])
+    bm = BM25Store(index_dir=d / "bm25")
+    bm.upsert_many(ids=corpus["ids"], texts=corpus["texts"], metadatas=corpus["metas"])
+    return vs, bm, d
+
+
+@pytest.mark.parametrize("fname", list(FILTERS))
+def test_bm25store_search(stores, corpus, golden, fname):
+    _, bm, _ = stores
+    for q, want in zip(corpus["qtexts"], golden["bm25"][fname]):
+        got = [[r["id"], r["score"]] for r in bm.search(query=q, where=FILTERS[fname], top_k=10)]
+        assert got == want
+
+
+def test_bm25store_misc(stores, corpus, golden):
+    from classmate_hip.retrieval import BM25Store
+    _, bm, _ = stores
+    m = golden["misc"]
+    assert bm.search(query="   ", top_k=5) == m["empty_query"]
+    assert [[r["id"], r["score"]] for r in bm.search(query="the and of", top_k=5)] == m["stopword_only_query"]
+    got = [[r["id"], r["score"]] for r in bm.search(query=corpus["qtexts"][0], where={"course": "cs101", "unit": "u1",
+                                                                                   "doc_type": "pptx"}, top_k=500)]
+    assert got == m["topk_gt_n_filtered"]
+    s2 = BM25Store(index_dir=None)
+    s2.upsert_many(ids=["a", "b", "c"], texts=["alpha beta", "beta gamma", "gamma delta"],
+                   metadatas=[{"language": "en", "tags": ["x", "y"]}, {"language": "en", "tags": ["x"]},
+                              {"language": "en"}])
+    s2.upsert_many(ids=["a"], texts=["alpha alpha zeta"], metadatas=[{"language": "en", "tags": ["y"]}])
+    s2.delete_many(["b"])
+    s2.upsert_many(ids=["b"], texts=["beta beta beta"], metadatas=[{"language": "en"}])
+    assert [[r["id"], r["score"]] for r in s2.search(query="beta alpha gamma", top_k=5)] == m["reorder_after_delete"]
+    assert [[r["id"], r["score"]] for r in s2.search(query="alpha", where={"tags": {"$contains": "y"}}, top_k=5)] \
+        == m["tags_contains"]
+
+
+@pytest.mark.parametrize("fname", list(FILTERS))
+def test_vector_store_query(stores, corpus, golden, fname):
+    from classmate_hip.retrieval import build_where_filter
+    vs, _, _ = stores
+    f = FILTERS[fname]
+    cw = build_where_filter(f) if f else None
+    for qv, want in zip(corpus["qvecs"], golden["dense"][fname]):
+        got = vs.query(query_embeddings=qv, where=cw, top_k=24)
+        assert [r["id"] for r in got] == [w[0] for w in want]
+        np.testing.assert_allclose([r["distance"] for r in got], [w[1] for w in want], atol=TOL)
+        assert set(got[0]) == {"id", "document", "metadata", "distance"}
+
+
+def test_vector_store_persistence_and_delete(stores, corpus):
+    from classmate_hip.retrieval import GpuVectorStore
+    vs, _, d = stores
+    again = GpuVectorStore(persist_dir=d / "chroma")          # a new process-style reload
+    assert again.count() == len(corpus["ids"])
+    q = corpus["qvecs"][0]
+    a = vs.query(query_embeddings=q, top_k=5, include_embeddings=True)
+    b = again.query(query_embeddings=q, top_k=5, include_embeddings=True)
+    assert [r["id"] for r in a] == [r["id"] for r in b]
+    assert all(np.array_equal(x["embedding"], y["embedding"]) for x, y in zip(a, b))
+    again.delete([a[0]["id"]])
+    assert again.count() == len(corpus["ids"]) - 1
+    assert again.query(query_embeddings=q, top_k=1)[0]["id"] == a[1]["id"]
+    again.reset_collection()
+    assert again.count() == 0
+
+
+def _rows(res):
+    return [[r["id"], r["scores"]["fused"], r["scores"]["vector_distance"], r["scores"]["bm25_score"]] for r in res]
+
+
+def _check(got, want):
+    assert [g[0] for g in got] == [w[0] for w in want]
+    for g, w in zip(got, want):
+        assert g[1] == w[1]                                   # fused: bit-identical
+        assert g[3] == w[3]                                   # bm25 score: bit-identical (or both None)
+        if w[2] is None:
+            assert g[2] is None
+        else:
+            assert abs(g[2] - w[2]) <= TOL
+
+
+@pytest.mark.parametrize("fname", list(FILTERS) + ["none_vector_only"])
+def test_hybrid_retrieve(stores, corpus, golden, fname):
+    from classmate_hip.retrieval import HybridRetriever
+    vs, bm, _ = stores
+    retr = HybridRetriever(vector_store=vs, bm25_store=bm, embedder=PresetEmbedder(corpus["qtexts"], corpus["qvecs"]),
+                           k_vector=10, k_bm25=10)
+    for q, want in zip(corpus["qtexts"], golden["retrieve"][fname]):
+        if fname == "none_vector_only":
+            got = retr.retrieve(question=q, filters=None, top_k=12, hybrid=False)
+        else:
+            got = retr.retrieve(question=q, filters=FILTERS[fname], top_k=10)
+        _check(_rows(got), want)
+
+
+@pytest.mark.parametrize("fname", ["none", "course_cs101", "tags_exam"])
+def test_retrieve_batch_equals_retrieve(stores, corpus, golden, fname):
+    from classmate_hip.retrieval import HybridRetriever
+    vs, bm, _ = stores
+    retr = HybridRetriever(vector_store=vs, bm25_store=bm, embedder=PresetEmbedder(corpus["qtexts"], corpus["qvecs"]),
+                           k_vector=10, k_bm25=10)
+    batch = retr.retrieve_batch(questions=corpus["qtexts"], filters=FILTERS[fname], top_k=10)
+    for got, want in zip(batch, golden["retrieve"][fname]):
+        _check(_rows(got), want)
+
+
+def test_mmr_and_rrf_public_functions(corpus, golden):
+    from classmate_hip.retrieval import _mmr_order, rrf_fuse
+    idx = {i: n for n, i in enumerate(corpus["ids"])}
+    for qv, case in zip(corpus["qvecs"], golden["mmr"]):
+        cand = corpus["emb"][[idx[i] for i in case["pool"]]]
+        assert _mmr_order(qv, cand, case["pool"], 10) == case["order"]
+    for case in golden["rrf"]:
+        got = rrf_fuse(rank_lists=case["lists"], weights=case["weights"], rrf_k=case["rrf_k"])
+        assert got == case["out"] and list(got) == list(case["out"])

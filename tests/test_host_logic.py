@@ -1,0 +1,127 @@
+"""Host-side logic of the drop-in layer (no GPU): tokenizer, where-filters ->
+row bitmaps, JSONL persistence format, error conventions.  Checked against
+the reference-generated goldens and the pinned oracle."""
+import json
+
+import numpy as np
+import pytest
+
+from oracle import ref_semantics as orc
+from classmate_hip.retrieval import filters as F
+from classmate_hip.retrieval.tokenize import _tokenize
+
+FILTERS = {
+    "none": None,
+    "course_cs101": {"course": "cs101", "unit": None, "author": None, "semester": None,
+                     "source_path": None, "created_at": None},
+    "course_only": {"course": "math201"},
+    "tags_exam": {"course": "cs101", "tags": ["exam"]},
+    "lang_en_doctype": {"language": "en", "doc_type": "pptx"},
+}
+
+
+def test_tokenizer_matches_reference_goldens(golden):
+    for case in golden["tokenize"]:
+        assert _tokenize(case["text"], "en") == case["en"]
+        assert _tokenize(case["text"], "it") == case["it"]
+
+
+def test_tokenizer_matches_oracle_on_corpus(corpus):
+    for t in corpus["texts"][:200] + corpus["qtexts"]:
+        assert _tokenize(t, "en") == orc.tokenize(t, "en")
+        assert _tokenize(t, "it") == orc.tokenize(t, "it")
+
+
+def test_build_where_filter_goldens(golden):
+    for name, f in FILTERS.items():
+        assert (F.build_where_filter(f) if f else None) == golden["where"][name]
+    assert F.build_where_filter({"doc_type": "other", "tags": "a b, C-d"}) == \
+        {"$and": [{"tag_a_b": True}, {"tag_c_d": True}]}
+    assert F.build_where_filter({"course": "  "}) is None
+
+
+def _index(metas):
+    m = F.MetaIndex()
+    for i, x in enumerate(metas):
+        m.set(i, x)
+    return m
+
+
+@pytest.mark.parametrize("where", list(FILTERS.values()) + [
+    {"$and": [{"course": "cs101"}, {"unit": "u2"}]}, {"tags": {"$contains": "x"}}, {"page": 3},
+    {"course": None, "unit": "u1"}])
+def test_bm25_mask_matches_matches_filter(corpus, where):
+    metas = [dict(m, tags=["x"] if i % 6 == 0 else ["y"]) for i, m in enumerate(corpus["metas"])]
+    got = _index(metas).bm25_mask(where)
+    want = np.array([orc.bm25_matches_filter(m, where) for m in metas])
+    assert np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("fname", list(FILTERS))
+def test_chroma_mask_matches_oracle(corpus, fname):
+    f = FILTERS[fname]
+    cw = F.build_where_filter(f) if f else None
+    got = _index(corpus["metas"]).chroma_mask(cw)
+    want = np.array([orc.chroma_matches(m, cw) for m in corpus["metas"]])
+    assert np.array_equal(got, want)
+
+
+def test_chroma_typed_equality_and_operators():
+    m = _index([{"a": 1}, {"a": True}, {"a": 1.0}, {"b": 2}, {"a": "1"}])
+    assert m.chroma_mask({"a": 1}).tolist() == [True, False, False, False, False]
+    assert m.chroma_mask({"a": True}).tolist() == [False, True, False, False, False]
+    assert m.chroma_mask({"a": {"$ne": 1}}).tolist() == [False, True, True, False, True]
+    assert m.chroma_mask({"$or": [{"a": 1}, {"b": 2}]}).tolist() == [True, False, False, True, False]
+    assert m.chroma_mask({"a": {"$in": [1, "1"]}}).tolist() == [True, False, False, False, True]
+    # BM25 semantics use Python equality: 1 == 1.0 == True
+    assert m.bm25_mask({"course": None}).tolist() == [True] * 5
+    m.remove(0)
+    assert m.chroma_mask(None).tolist() == [False, True, True, True, True]
+
+
+def test_pack_bits_layout():
+    rng = np.random.default_rng(0)
+    for n in (1, 31, 32, 33, 1000):
+        mask = rng.random(n) < 0.4
+        w = F.pack_bits(mask)
+        assert w.dtype == np.uint32 and w.shape[0] == max((n + 31) // 32, 1)
+        back = np.array([(w[i >> 5] >> (i & 31)) & 1 for i in range(n)], bool)
+        assert np.array_equal(back, mask)
+
+
+def test_bm25store_host_semantics(tmp_path):
+    from classmate_hip.retrieval import BM25Store
+    s = BM25Store(index_dir=tmp_path)
+    with pytest.raises(ValueError):
+        s.upsert_many(ids=["a"], texts=["x", "y"], metadatas=[{}])
+    with pytest.raises(ZeroDivisionError):                       # quirk Q7, raised at upsert like _rebuild
+        s.upsert_many(ids=["x1", "x2"], texts=["the and", "12 34"], metadatas=[{"language": "en"}] * 2)
+    s2 = BM25Store(index_dir=tmp_path)
+    s2.upsert_many(ids=["a", "b"], texts=["alpha beta", "gamma"], metadatas=[{"language": "en"}, {"language": "it"}])
+    s2.upsert_many(ids=["a"], texts=["alpha alpha"], metadatas=[{"language": "auto"}])   # detected (fallback en)
+    assert list(s2._entries) == ["a", "b"]                                               # in-place replace
+    s2.save()
+    lines = [json.loads(x) for x in (tmp_path / "bm25_index.jsonl").read_text().splitlines()]
+    assert lines[0] == {"id": "a", "text": "alpha alpha", "tokens": ["alpha", "alpha"],
+                        "metadata": {"language": "en"}}
+    s3 = BM25Store.load_or_create(tmp_path)
+    assert [e.tokens for e in s3._entries.values()] == [["alpha", "alpha"], ["gamma"]]
+    assert s3.search(query="   ", top_k=3) == []
+    assert BM25Store(index_dir=tmp_path / "none").search(query="alpha") == []
+
+
+def test_rrf_weights_error_before_device():
+    from classmate_hip.retrieval import rrf_fuse
+    with pytest.raises(ValueError):
+        rrf_fuse(rank_lists=[["a"], ["b"]], weights=[1.0])
+    assert rrf_fuse(rank_lists=[]) == {}
+
+
+def test_vector_store_argument_errors(tmp_path):
+    from classmate_hip.retrieval import GpuVectorStore
+    vs = GpuVectorStore(persist_dir=tmp_path)
+    with pytest.raises(ValueError):
+        vs.upsert(ids=["a", "b"], documents=["x"], metadatas=[{}], embeddings=np.zeros((1, 4), np.float32))
+    assert vs.count() == 0 and vs.query(query_embeddings=np.zeros(4, np.float32)) == []
+    with pytest.raises(ValueError):
+        GpuVectorStore(persist_dir=None, distance="l2")
