@@ -229,6 +229,14 @@ class BM25Index:
         out["dl"] = out["dl"][:n]
         return out
 
+    def set_head_policy(self, min_df_frac: float = 1.0 / 64, max_bytes: int = 8 << 30):
+        """Dense tf tiles for high-df terms (same results; max_bytes=0 disables)."""
+        L.check(L.fn["cm_bm25_set_head_policy"](self._h, float(min_df_frac), int(max_bytes)), "cm_bm25_set_head_policy")
+
+    @property
+    def num_head_terms(self) -> int:
+        return int(L.fn["cm_bm25_num_head_terms"](self._h))
+
     def term_stats(self):
         """Local (df[V] int32, first_key[V] uint64 = row << 32 | first position, ~0 if absent)."""
         df = np.zeros(max(self.vocab, 1), np.int32)

@@ -149,7 +149,7 @@ def merge_bm25_topk(score_t, rows_t, k: int, group=None):
     S1 = torch.gather(Sk, 1, i1)
     i2 = torch.argsort(-S1, dim=1, stable=True)  # ... then score desc (stable keeps row order)
     idx = torch.gather(i1, 1, i2)[:, :k]
-    return torch.gather(score_t.new_tensor(torch.cat(sl, 1)), 1, idx), torch.gather(R, 1, idx)
+    return torch.gather(S, 1, idx), torch.gather(R, 1, idx)
 
 
 def assemble_pool_vectors(rows_t, local_vecs, row0: int, n_local: int, group=None):

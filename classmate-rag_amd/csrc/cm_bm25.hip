@@ -29,6 +29,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <numeric>
 #include <vector>
 
@@ -37,8 +38,6 @@ namespace cm {
 constexpr int kRange = 1024;                 // docs per range (one wave's LDS score tile)
 constexpr int kBmThreads = 256;              // 4 waves = 4 queries per K2 workgroup
 constexpr int kQPerBlock = kBmThreads / 64;
-constexpr int kSlots = kRange / 64;          // docs per lane in a range (s = u*64 + lane)
-constexpr int kBatch = 16;                   // postings per lane in flight
 constexpr int kBoundsGroup = 64;             // ranges per bounds thread (gallop between them)
 constexpr int kMergeThreads = 1024;
 constexpr int kMergePer = 16;                // lists per merge thread -> <= 16384 ranges (16.7M docs)
@@ -107,7 +106,7 @@ __device__ inline int64_t lower_bound_doc(const int32_t *__restrict__ post_doc, 
 
 __global__ void bm25_bounds_kernel(const int32_t *__restrict__ q_terms, int n_terms, int32_t vocab, int nr,
                                    const int64_t *__restrict__ term_off, const int32_t *__restrict__ post_doc,
-                                   int64_t *__restrict__ bounds) {
+                                   const int32_t *__restrict__ head_id, int64_t *__restrict__ bounds) {
   const int ngroups = (nr + 1 + kBoundsGroup - 1) / kBoundsGroup;
   const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (gid >= (int64_t)n_terms * ngroups) return;
@@ -117,7 +116,7 @@ __global__ void bm25_bounds_kernel(const int32_t *__restrict__ q_terms, int n_te
   int64_t *out = bounds + (int64_t)i * (nr + 1);
   const int r0 = g * kBoundsGroup;
   const int r1 = min(r0 + kBoundsGroup, nr + 1);
-  if (t < 0 || t >= vocab) {
+  if (t < 0 || t >= vocab || (head_id && head_id[t] >= 0)) {  // unknown or dense-tile term: no postings walk
     for (int r = r0; r < r1; ++r) out[r] = 0;
     return;
   }
@@ -142,126 +141,369 @@ __global__ void bm25_bounds_kernel(const int32_t *__restrict__ q_terms, int n_te
   }
 }
 
-// K2: one workgroup per (range of kRange docs, 4 queries); one wave per query.
-// The wave accumulates its query's terms in order into an LDS fp64 tile (no
-// block barriers: a wave's LDS operations are in order), with kBatch postings
-// per lane in flight, then selects the range's top-k by wave argmin rounds.
+// K2: one wave per (query, group of consecutive ranges of kRange docs); the
+// 4 waves of a workgroup are 4 consecutive queries over the same ranges, and
+// workgroups are remapped so each XCD owns a contiguous run of range groups
+// (every query's head tiles for those ranges then share that XCD's L2).
+// Waves never synchronise with each other.
+//
+// Lane l owns docs d0 + 16l .. d0 + 16l + 15 of the current range and keeps
+// their K_d and fp64 scores in registers.  Lane j (< 64) holds the descriptor
+// of query term j (term, head id, idf, tail postings [lo, hi) of the range).
+// Per range:
+//   * the range's tail postings of all the query's tail terms are gathered into
+//     the wave's LDS slice with one coalesced pass (term-major, doc-sorted);
+//   * terms are applied in query order (duplicates twice), so every document
+//     sums its contributions in rank_bm25's order:
+//       - head term: 16 tf bytes per lane from the dense tile (a 2-deep
+//         prefetch ring runs over the (range, head term) sequence), 16
+//         predicated independent register updates;
+//       - tail term: each lane binary-searches its 16-doc window in the
+//         term's LDS postings and applies the (usually 0-1) hits;
+//   * top-k of the range, pruned by the query's global threshold T (atomicMin
+//     of every range's k-th best key: any range's k-th best bounds the global
+//     k-th best), so most ranges stop after one argmin.
+// dl / live / allow words and the tail bounds of range r+1 are loaded while
+// range r is scored.
+constexpr int kTailCapW = 320;  // tail postings gathered per (wave, range); overflow terms read from global
+constexpr int kMaxRangesPerWave = 16;
+#ifndef K2_SLOT_GROUP
+#define K2_SLOT_GROUP 4
+#endif
+#ifndef K2_WAVES_PER_EU
+#define K2_WAVES_PER_EU 2
+#endif
+
+__device__ inline double bm25_contrib(double idf, uint32_t tfi, double kdv) {
+  const double tf = (double)tfi;
+  const double num = tf * 2.5;
+  const double den = tf + kdv;
+  return idf * (num / den);
+}
+__device__ inline double readlane_f64(double v, int j) {
+  const uint64_t b = __double_as_longlong(v);
+  const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)b, j);
+  const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(b >> 32), j);
+  return __longlong_as_double(((uint64_t)hi << 32) | lo);
+}
+__device__ inline int64_t readlane_i64(int64_t v, int j) {
+  const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)(uint64_t)v, j);
+  const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)((uint64_t)v >> 32), j);
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+__device__ inline void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+// first index in [lo, hi) of a doc-sorted posting list (LDS or global) with doc >= target
+template <typename P>
+__device__ inline int first_ge(const P *__restrict__ a, int lo, int hi, int32_t target) {
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (a[mid] < target) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+__device__ inline double kd_of(int32_t dlen, double avgdl) {
+  double t = 0.75 * (double)dlen;
+  t = t / avgdl;
+  t = 0.25 + t;
+  return 1.5 * t;
+}
+
 template <typename TF>
-__global__ void __launch_bounds__(kBmThreads)
-    bm25_range_kernel(const int32_t *__restrict__ q_off, int nq, const double *__restrict__ q_idf,
-                      const int64_t *__restrict__ bounds, int nr, const int32_t *__restrict__ post_doc,
-                      const TF *__restrict__ post_tf, const int32_t *__restrict__ dl, const uint32_t *__restrict__ live,
-                      const uint32_t *__restrict__ allow, int64_t ndocs, double avgdl, int k,
-                      uint64_t *__restrict__ cand_key, uint32_t *__restrict__ cand_row) {
-  __shared__ double kd[kRange];
-  __shared__ double score_all[kQPerBlock][kRange];
-  const int r = blockIdx.y;  // queries fastest: every query group of a range runs together (L2 reuse)
-  const int64_t d0 = (int64_t)r * kRange;
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  for (int s = tid; s < kRange; s += kBmThreads) {
-    const int64_t d = d0 + s;
-    double v = 0.0;
-    if (d < ndocs) {
-      double t = 0.75 * (double)dl[d];
-      t = t / avgdl;
-      t = 0.25 + t;
-      v = 1.5 * t;
-    }
-    kd[s] = v;
-  }
-  uint32_t okmask = 0;  // bit u: doc d0 + u*64 + lane is a candidate
-#pragma unroll
-  for (int u = 0; u < kSlots; ++u) {
-    const int64_t d = d0 + u * 64 + lane;
-    if (d < ndocs) {
-      const int64_t w = d >> 5;
-      const uint32_t b = (live[w] & (allow ? allow[w] : 0xffffffffu)) >> (d & 31);
-      okmask |= (b & 1u) << u;
-    }
-  }
-  __syncthreads();
-  const int wave = tid >> 6;
-  const int qi = blockIdx.x * kQPerBlock + wave;
-  if (qi >= nq) return;  // no block barrier below
-  double *score = score_all[wave];
-  const int t0 = q_off[qi], t1 = q_off[qi + 1];
+__global__ void __launch_bounds__(kBmThreads) __attribute__((amdgpu_waves_per_eu(K2_WAVES_PER_EU)))
+    bm25_range_kernel(const int32_t *__restrict__ q_terms, const int32_t *__restrict__ q_off, int nq,
+                      const double *__restrict__ q_idf, const int64_t *__restrict__ bounds, int nr, int rpw,
+                      const int64_t *__restrict__ term_off, const int32_t *__restrict__ post_doc,
+                      const TF *__restrict__ post_tf, const int32_t *__restrict__ head_id,
+                      const uint8_t *__restrict__ headtf, int64_t npad, const int32_t *__restrict__ dl,
+                      const uint32_t *__restrict__ live, const uint32_t *__restrict__ allow, int64_t ndocs,
+                      double avgdl, int k, uint64_t *__restrict__ cand_key, uint32_t *__restrict__ cand_row,
+                      unsigned long long *__restrict__ thr_key, int dbg) {
+  __shared__ int32_t s_pdoc[kQPerBlock][kTailCapW];
+  __shared__ uint16_t s_ptf[kQPerBlock][kTailCapW];
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  // XCD-aware remap: hardware places workgroup b on XCD b % 8
+  const int nb = gridDim.x;
+  const int b = blockIdx.x;
+  const int per = nb >> 3, rem = nb & 7, x = b & 7, y = b >> 3;
+  const int lb = (x < rem ? x * (per + 1) : rem * (per + 1) + (x - rem) * per) + y;
+  const int nqg = (nq + kQPerBlock - 1) / kQPerBlock;
+  const int qi = (lb % nqg) * kQPerBlock + wave;
+  const int rg = lb / nqg;
+  if (qi >= nq) return;
+  const int r0 = rg * rpw, r1 = min(r0 + rpw, nr);
+  if (r0 >= r1) return;
+  int32_t *pdoc = s_pdoc[wave];
+  uint16_t *ptf = s_ptf[wave];
+  const int tb = q_off[qi];
+  const int L = q_off[qi + 1] - tb;
   const int64_t bstride = nr + 1;
-  int64_t total = 0;
-  for (int i = t0; i < t1; ++i) total += bounds[(int64_t)i * bstride + r + 1] - bounds[(int64_t)i * bstride + r];
-  if (total > 0) {
+  // ---- per-wave term descriptors (lane j <-> query term j < 64)
+  int32_t my_t = -1, my_h = -1;
+  double my_idf = 0.0;
+  int64_t my_lo = 0, my_hi = 0;
+  if (lane < L) {
+    my_t = q_terms[tb + lane];
+    my_idf = q_idf[tb + lane];
+    my_h = (my_t >= 0 && head_id) ? head_id[my_t] : -1;
+    my_lo = bounds[(int64_t)(tb + lane) * bstride + r0];
+    my_hi = bounds[(int64_t)(tb + lane) * bstride + r0 + 1];
+  }
+  const uint64_t headmask = __ballot(lane < L && my_t >= 0 && my_h >= 0);
+  unsigned long long *tq = thr_key + qi;
+  // ---- head-tile prefetch ring over the (range, head term) sequence
+  int c_r = r0;
+  uint64_t c_m = headmask;
+  auto tile_at = [&](int r, uint64_t m) -> uint4 {
+    if (m == 0 || r >= r1) return uint4{0, 0, 0, 0};
+    const int j = __builtin_ctzll(m);
+    const int32_t h = __builtin_amdgcn_readlane(my_h, j);
+    return *reinterpret_cast<const uint4 *>(headtf + (int64_t)h * npad + (int64_t)r * kRange + 16 * lane);
+  };
+  auto advance = [&](int &r, uint64_t &m) {
+    m &= m - 1;
+    if (m == 0) {
+      ++r;
+      m = headmask;
+    }
+  };
+  uint4 n1 = tile_at(c_r, c_m);
+  if (headmask) advance(c_r, c_m);
+  uint4 n2 = tile_at(c_r, c_m);
+  if (headmask) advance(c_r, c_m);
+  // ---- range r: dl / bitmap words (loaded one range ahead)
+  int4 dlq[4];
+  uint32_t lw = 0, aw = 0xffffffffu;
+  auto load_range_words = [&](int r) {
+    const int64_t db = (int64_t)r * kRange + 16 * lane;
+    if (db + 16 <= ndocs) {
+      const int4 *p4 = reinterpret_cast<const int4 *>(dl + db);
 #pragma unroll
-    for (int u = 0; u < kSlots; ++u) score[u * 64 + lane] = 0.0;
-    for (int i = t0; i < t1; ++i) {  // query tokens in order (duplicates twice)
-      const double idf = q_idf[i];
-      const int64_t lo = bounds[(int64_t)i * bstride + r];
-      const int64_t hi = bounds[(int64_t)i * bstride + r + 1];
-      for (int64_t base = lo; base < hi; base += 64 * kBatch) {
-        int32_t dd[kBatch];
-        TF tt[kBatch];
+      for (int v = 0; v < 4; ++v) dlq[v] = p4[v];
+    } else {
+      int32_t t[16];
 #pragma unroll
-        for (int u = 0; u < kBatch; ++u) {
-          const int64_t p = base + u * 64 + lane;
-          dd[u] = p < hi ? post_doc[p] : -1;
-          tt[u] = p < hi ? post_tf[p] : (TF)0;
+      for (int u = 0; u < 16; ++u) t[u] = db + u < ndocs ? dl[db + u] : 0;
+#pragma unroll
+      for (int v = 0; v < 4; ++v) dlq[v] = int4{t[4 * v], t[4 * v + 1], t[4 * v + 2], t[4 * v + 3]};
+    }
+    const int64_t w = db < ndocs ? db >> 5 : 0;
+    lw = live[w];
+    aw = allow ? allow[w] : 0xffffffffu;
+  };
+  load_range_words(r0);
+  for (int r = r0; r < r1; ++r) {
+    const int64_t d0 = (int64_t)r * kRange;
+    const int64_t db = d0 + 16 * lane;
+    double kdr[16];
+    {
+      const int32_t dlv[16] = {dlq[0].x, dlq[0].y, dlq[0].z, dlq[0].w, dlq[1].x, dlq[1].y, dlq[1].z, dlq[1].w,
+                               dlq[2].x, dlq[2].y, dlq[2].z, dlq[2].w, dlq[3].x, dlq[3].y, dlq[3].z, dlq[3].w};
+#pragma unroll
+      for (int u = 0; u < 16; ++u) kdr[u] = kd_of(dlv[u], avgdl);
+    }
+    uint32_t okmask = 0;
+    if (db < ndocs) {
+      okmask = ((lw & aw) >> (db & 31)) & 0xffffu;
+      const int64_t rm = ndocs - db;
+      if (rm < 16) okmask &= (1u << rm) - 1u;
+    }
+    // this range's tail postings -> LDS (term-major); next range's words/bounds in flight
+    const int cnt = (int)(my_hi - my_lo);
+    int incl = cnt;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int v = __shfl_up(incl, o);
+      if (lane >= o) incl += v;
+    }
+    const int excl = incl - cnt;
+    const int my_off = (cnt > 0 && incl <= kTailCapW) ? excl : -1;
+    const uint64_t inmask = __ballot(cnt > 0 && incl <= kTailCapW);
+    const int n_in = inmask ? __builtin_amdgcn_readlane(incl, 63 - __builtin_clzll(inmask)) : 0;
+    for (int e0 = 0; e0 < n_in; e0 += 64) {  // wave-uniform trip count: every lane takes part in the shuffles
+      const int e = e0 + lane;
+      int lo = 0, hi = 63;  // last lane whose exclusive offset <= e (offsets are non-decreasing)
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (__shfl(excl, mid) <= e) lo = mid;
+        else hi = mid - 1;
+      }
+      // several lanes can share an offset (empty terms): the last one is the one with postings
+      const int64_t src = __shfl(my_lo, lo) + (e - __shfl(excl, lo));
+      if (e < n_in) {
+        const int32_t doc = post_doc[src];
+        pdoc[e] = doc;
+        ptf[e] = (uint16_t)post_tf[src];
+      }
+    }
+    int64_t nx_lo = my_hi, nx_hi = my_hi;
+    if (r + 1 < r1) {
+      load_range_words(r + 1);
+      if (lane < L) nx_hi = bounds[(int64_t)(tb + lane) * bstride + r + 2];
+    }
+    wave_lds_sync();
+    double sc[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) sc[u] = 0.0;
+    const int32_t wlo = (int32_t)(db - d0), whi = wlo + 16;  // this lane's window, range-relative
+    if (!(dbg & 1)) {
+      for (int j = 0; j < L; ++j) {
+        int32_t t, hh;
+        double idf;
+        int c, off;
+        int64_t plo;
+        if (j < 64) {
+          t = __builtin_amdgcn_readlane(my_t, j);
+          hh = __builtin_amdgcn_readlane(my_h, j);
+          idf = readlane_f64(my_idf, j);
+          c = __builtin_amdgcn_readlane(cnt, j);
+          off = __builtin_amdgcn_readlane(my_off, j);
+          plo = readlane_i64(my_lo, j);
+        } else {  // long query: descriptor from global, postings from global
+          const int i = tb + j;
+          t = q_terms[i];
+          hh = (t >= 0 && head_id) ? head_id[t] : -1;
+          idf = q_idf[i];
+          plo = bounds[(int64_t)i * bstride + r];
+          c = (int)(bounds[(int64_t)i * bstride + r + 1] - plo);
+          off = -1;
         }
+        if (t < 0) continue;
+        if (hh >= 0) {
+          uint4 v;
+          if (j < 64) {
+            v = n1;
+            n1 = n2;
+            n2 = tile_at(c_r, c_m);
+            advance(c_r, c_m);
+          } else {
+            v = *reinterpret_cast<const uint4 *>(headtf + (int64_t)hh * npad + db);
+          }
+          const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
+          uint32_t satm = 0;
 #pragma unroll
-        for (int u = 0; u < kBatch; ++u) {
-          if (dd[u] >= 0) {
-            const int s = dd[u] - (int32_t)d0;
-            const double tf = (double)tt[u];
-            const double num = tf * 2.5;
-            const double den = tf + kd[s];
-            const double c = idf * (num / den);
-            score[s] = score[s] + c;
+          for (int u = 0; u < 16; ++u) {
+            const uint32_t tfi = (wv[u >> 2] >> (8 * (u & 3))) & 0xffu;
+            if (tfi == 255u) satm |= 1u << u;
+            else if (tfi != 0u) sc[u] = sc[u] + bm25_contrib(idf, tfi, kdr[u]);
+            if ((u & (K2_SLOT_GROUP - 1)) == K2_SLOT_GROUP - 1) __builtin_amdgcn_sched_barrier(0);  // bound live temps
+          }
+          if (satm) {  // saturated byte (tf >= 255): exact tf from the postings
+#pragma unroll
+            for (int u = 0; u < 16; ++u) {
+              if ((satm >> u) & 1u) {
+                const int64_t p = lower_bound_doc(post_doc, term_off[t], term_off[t + 1], (int32_t)(db + u));
+                sc[u] = sc[u] + bm25_contrib(idf, (uint32_t)post_tf[p], kdr[u]);
+              }
+            }
+          }
+        } else if (c > 0) {
+          // lane's window [wlo, whi) of the term's doc-sorted postings: walk it slot by slot
+          // (compile-time register indices; a wave skips the block when no lane has a hit)
+          if (off >= 0) {
+            int e = first_ge(pdoc + off, 0, c, (int32_t)d0 + wlo);
+            int32_t nd = e < c ? pdoc[off + e] - (int32_t)d0 : INT32_MAX;
+            if (nd < whi) {
+#pragma unroll
+              for (int u = 0; u < 16; ++u) {
+                if (nd == wlo + u) {
+                  sc[u] = sc[u] + bm25_contrib(idf, ptf[off + e], kdr[u]);
+                  ++e;
+                  nd = e < c ? pdoc[off + e] - (int32_t)d0 : INT32_MAX;
+                }
+              }
+            }
+          } else {
+            int64_t e = lower_bound_doc(post_doc, plo, plo + c, (int32_t)db);
+            int32_t nd = e < plo + c ? post_doc[e] - (int32_t)d0 : INT32_MAX;
+            if (nd < whi) {
+#pragma unroll
+              for (int u = 0; u < 16; ++u) {
+                if (nd == wlo + u) {
+                  sc[u] = sc[u] + bm25_contrib(idf, (uint32_t)post_tf[e], kdr[u]);
+                  ++e;
+                  nd = e < plo + c ? post_doc[e] - (int32_t)d0 : INT32_MAX;
+                }
+              }
+            }
           }
         }
       }
+    } else if (headmask) {  // ablation: keep the ring in step
+      for (int j = 0; j < min(L, 64); ++j)
+        if ((headmask >> j) & 1) {
+          n1 = n2;
+          n2 = tile_at(c_r, c_m);
+          advance(c_r, c_m);
+        }
     }
-  }
-  // top-k of this (range, query): (score desc, row asc) over candidate docs
-  const uint64_t zero_key = score_key(0.0);
-  uint32_t taken = 0;
-  auto local_best = [&](uint64_t &bk, uint32_t &br) {
-    bk = kEmptyKey;
-    br = 0xffffffffu;
+    // ---- top-k of this (range, query), pruned by the query's global threshold
+    uint32_t taken = 0;
+    auto local_best = [&](uint64_t &bk, uint32_t &br) {
+      bk = kEmptyKey;
+      br = 0xffffffffu;
 #pragma unroll
-    for (int u = 0; u < kSlots; ++u) {
-      if (((okmask >> u) & 1u) && !((taken >> u) & 1u)) {
-        const uint64_t key = total > 0 ? score_key(score[u * 64 + lane]) : zero_key;
-        if (key < bk) {  // u ascending == row ascending within the lane
-          bk = key;
-          br = (uint32_t)(d0 + u * 64 + lane);
+      for (int u = 0; u < 16; ++u) {
+        if (((okmask >> u) & 1u) && !((taken >> u) & 1u)) {
+          const uint64_t key = score_key(sc[u]);
+          if (key < bk) {  // u ascending == row ascending within the lane
+            bk = key;
+            br = (uint32_t)(db + u);
+          }
         }
       }
-    }
-  };
-  uint64_t bk;
-  uint32_t br;
-  local_best(bk, br);
-  for (int i = 0; i < k; ++i) {
-    uint64_t mk = bk;
-    uint32_t mr = br;
-    wave_min_pair(mk, mr);
-    if (lane == 0) {
-      const int64_t o = ((int64_t)qi * nr + r) * k + i;
-      cand_key[o] = mk;
-      cand_row[o] = mr;
-    }
-    if (mr == 0xffffffffu) {
-      // no candidates left in this range: pad the rest
-      for (int j = i + 1 + lane; j < k; j += 64) {
-        const int64_t o = ((int64_t)qi * nr + r) * k + j;
-        cand_key[o] = kEmptyKey;
-        cand_row[o] = 0xffffffffu;
+    };
+    uint64_t bk;
+    uint32_t br;
+    local_best(bk, br);
+    const uint64_t T = (dbg & 2) ? 0ull : __hip_atomic_load(tq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int i = 0;
+    uint64_t last = kEmptyKey;
+    for (; i < k; ++i) {
+      uint64_t mk = bk;
+      uint32_t mr = br;
+      wave_min_pair(mk, mr);
+      if (mr == 0xffffffffu || mk > T) break;  // nothing left that can enter the global top-k
+      if (lane == 0) {
+        const int64_t o = ((int64_t)qi * nr + r) * k + i;
+        cand_key[o] = mk;
+        cand_row[o] = mr;
       }
-      break;
+      last = mk;
+      if (br == mr && bk == mk) {
+        taken |= 1u << (mr - (uint32_t)db);
+        local_best(bk, br);
+      }
     }
-    if (br == mr && bk == mk) {
-      taken |= 1u << ((mr - (uint32_t)d0) >> 6);
-      local_best(bk, br);
+    for (int j = i + lane; j < k; j += 64) {
+      const int64_t o = ((int64_t)qi * nr + r) * k + j;
+      cand_key[o] = kEmptyKey;
+      cand_row[o] = 0xffffffffu;
     }
+    if (i == k && lane == 0 && last < T) atomicMin(tq, (unsigned long long)last);
+    my_lo = nx_lo;
+    my_hi = nx_hi;
+    wave_lds_sync();  // LDS slice reused by the next range
   }
+}
+
+// Dense head-term tiles: tf[h][doc] (uint8, 255 = saturated) from the CSR.
+__global__ void bm25_head_fill_kernel(const int32_t *__restrict__ head_terms, int nhead,
+                                      const int64_t *__restrict__ term_off, const int32_t *__restrict__ post_doc,
+                                      const uint16_t *__restrict__ post_tf, uint8_t *__restrict__ headtf,
+                                      int64_t npad) {
+  const int h = blockIdx.y;
+  if (h >= nhead) return;
+  const int32_t t = head_terms[h];
+  const int64_t lo = term_off[t], hi = term_off[t + 1];
+  uint8_t *row = headtf + (int64_t)h * npad;
+  for (int64_t p = lo + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < hi; p += (int64_t)gridDim.x * blockDim.x)
+    row[post_doc[p]] = (uint8_t)min((int)post_tf[p], 255);
 }
 
 // Tournament merge of nr sorted per-range lists per query.
@@ -467,6 +709,11 @@ struct cm_bm25 {
   double avgdl = 0.0, eps = 0.0;
   bool empty_vocab = false;  // live docs exist but no tokens (ZeroDivisionError on search)
   DevBuf term_off, post_doc, post_tf, post_pos, dl, live, idf;
+  DevBuf headtf, head_id;  // dense tf tiles for high-df terms (K2 fast path)
+  int32_t nhead = 0;
+  int64_t npad = 0;
+  double head_min_frac = 1.0 / 64.0;      // df > ndocs * frac qualifies
+  int64_t head_max_bytes = 8ll << 30;    // tile memory budget
   std::vector<double> idf_host;
   DevBuf ws, qbuf, obuf, allow_buf, tmp;
 };
@@ -505,7 +752,50 @@ int compute_idf_table(cm_bm25 *h, const std::vector<int32_t> &df, const std::vec
   return CM_OK;
 }
 
+// Select head terms (df > ndocs * head_min_frac, highest df first, within the
+// byte budget) and build their dense uint8 tf tiles on the handle's stream.
+int build_head_tiles(cm_bm25 *h, const std::vector<int32_t> &df) {
+  h->nhead = 0;
+  h->npad = round_up(std::max<int64_t>(h->ndocs, 1), kRange);
+  const double thr = (double)h->ndocs * h->head_min_frac;
+  std::vector<int32_t> cand;
+  for (int32_t t = 0; t < h->vocab; ++t)
+    if ((double)df[t] > thr && df[t] > 0) cand.push_back(t);
+  std::sort(cand.begin(), cand.end(), [&](int32_t a, int32_t b) { return df[a] > df[b] || (df[a] == df[b] && a < b); });
+  const int64_t max_h = h->head_max_bytes / h->npad;
+  if ((int64_t)cand.size() > max_h) cand.resize((size_t)std::max<int64_t>(max_h, 0));
+  std::vector<int32_t> hid((size_t)std::max(h->vocab, 1), -1);
+  for (size_t i = 0; i < cand.size(); ++i) hid[cand[i]] = (int32_t)i;
+  int rc;
+  if ((rc = h->head_id.ensure((size_t)std::max(h->vocab, 1) * 4))) return rc;
+  CM_HIP(hipMemcpyAsync(h->head_id.ptr, hid.data(), (size_t)std::max(h->vocab, 1) * 4, hipMemcpyHostToDevice,
+                        h->stream));
+  if (!cand.empty()) {
+    const size_t bytes = cand.size() * (size_t)h->npad;
+    if ((rc = h->headtf.ensure(bytes)) || (rc = h->tmp.ensure(cand.size() * 4))) return rc;
+    CM_HIP(hipMemsetAsync(h->headtf.ptr, 0, bytes, h->stream));
+    CM_HIP(hipMemcpyAsync(h->tmp.ptr, cand.data(), cand.size() * 4, hipMemcpyHostToDevice, h->stream));
+    hipLaunchKernelGGL(bm25_head_fill_kernel, dim3(64, (unsigned)cand.size()), dim3(256), 0, h->stream,
+                       h->tmp.as<int32_t>(), (int)cand.size(), h->term_off.as<int64_t>(), h->post_doc.as<int32_t>(),
+                       h->post_tf.as<uint16_t>(), h->headtf.as<uint8_t>(), h->npad);
+    CM_HIP(hipGetLastError());
+    CM_HIP(hipStreamSynchronize(h->stream));  // tmp is reused by later calls
+  }
+  h->nhead = (int32_t)cand.size();
+  return CM_OK;
+}
+
+// CM_BM25_DEBUG (ablation only): bit0 skip scoring, bit1 skip the per-range top-k.
+int bm25_debug_flags() {
+  static int f = [] {
+    const char *e = getenv("CM_BM25_DEBUG");
+    return e ? atoi(e) : 0;
+  }();
+  return f;
+}
+
 struct BmWs {
+  unsigned long long *thr;
   double *q_idf;
   int64_t *bounds;
   uint64_t *cand_key;
@@ -518,6 +808,8 @@ BmWs bm_ws_layout(const cm_bm25 *h, int nq, int total_terms, int k, void *base) 
   char *p = reinterpret_cast<char *>(base);
   const int64_t nr = std::max<int64_t>(1, ceil_div(h->ndocs, kRange));
   size_t off = 0;
+  w.thr = reinterpret_cast<unsigned long long *>(p + off);
+  off += round_up((int64_t)std::max(nq, 1) * 8, 256);
   w.q_idf = reinterpret_cast<double *>(p + off);
   off += round_up((int64_t)std::max(total_terms, 1) * 8, 256);
   w.bounds = reinterpret_cast<int64_t *>(p + off);
@@ -540,13 +832,21 @@ int bm25_launch_core(cm_bm25 *h, const int32_t *q_terms_dev, const int32_t *q_of
   const int64_t nb = (int64_t)total_terms * ngroups;
   if (nb > 0) {
     hipLaunchKernelGGL(bm25_bounds_kernel, dim3((unsigned)ceil_div(nb, 256)), dim3(256), 0, st, q_terms_dev,
-                       total_terms, h->vocab, nr, h->term_off.as<int64_t>(), h->post_doc.as<int32_t>(), w.bounds);
+                       total_terms, h->vocab, nr, h->term_off.as<int64_t>(), h->post_doc.as<int32_t>(),
+                       h->nhead ? h->head_id.as<int32_t>() : (const int32_t *)nullptr, w.bounds);
     CM_HIP(hipGetLastError());
   }
-  dim3 grid((unsigned)ceil_div(nq, kQPerBlock), nr);
-  hipLaunchKernelGGL(bm25_range_kernel<uint16_t>, grid, dim3(kBmThreads), 0, st, q_off_dev, nq, w.q_idf, w.bounds,
-                     nr, h->post_doc.as<int32_t>(), h->post_tf.as<uint16_t>(), h->dl.as<int32_t>(),
-                     h->live.as<uint32_t>(), allow_dev, h->ndocs, avgdl, k, w.cand_key, w.cand_row);
+  CM_HIP(hipMemsetAsync(w.thr, 0xff, (size_t)nq * 8, st));  // no threshold yet
+  // ranges per wave: enough waves to fill 256 CUs several times over, long runs otherwise
+  const int64_t work = (int64_t)nq * nr;
+  const int rpw = (int)std::min<int64_t>(kMaxRangesPerWave, std::max<int64_t>(1, work / (256 * 4 * 48)));
+  const int64_t nblk = (int64_t)ceil_div(nq, kQPerBlock) * ceil_div(nr, rpw);
+  if (nblk > INT32_MAX) CM_FAIL(CM_EUNSUPPORTED, "BM25 batch too large");
+  hipLaunchKernelGGL(bm25_range_kernel<uint16_t>, dim3((unsigned)nblk), dim3(kBmThreads), 0, st, q_terms_dev,
+                     q_off_dev, nq, w.q_idf, w.bounds, nr, rpw, h->term_off.as<int64_t>(), h->post_doc.as<int32_t>(), h->post_tf.as<uint16_t>(),
+                     h->nhead ? h->head_id.as<int32_t>() : (const int32_t *)nullptr, h->headtf.as<uint8_t>(),
+                     h->npad, h->dl.as<int32_t>(), h->live.as<uint32_t>(), allow_dev, h->ndocs, avgdl, k,
+                     w.cand_key, w.cand_row, w.thr, bm25_debug_flags());
   CM_HIP(hipGetLastError());
   hipLaunchKernelGGL(bm25_merge_kernel, dim3(nq), dim3(kMergeThreads), 0, st, w.cand_key, w.cand_row, nr, k,
                      score_dev, row_dev);
@@ -556,7 +856,7 @@ int bm25_launch_core(cm_bm25 *h, const int32_t *q_terms_dev, const int32_t *q_of
 
 void bm25_free(cm_bm25 *h) {
   for (DevBuf *b : {&h->term_off, &h->post_doc, &h->post_tf, &h->post_pos, &h->dl, &h->live, &h->idf, &h->ws,
-                    &h->qbuf, &h->obuf, &h->allow_buf, &h->tmp})
+                    &h->qbuf, &h->obuf, &h->allow_buf, &h->tmp, &h->headtf, &h->head_id})
     b->release();
 }
 
@@ -690,6 +990,7 @@ int cm_bm25_build(cm_bm25 *h, const int32_t *term_ids, const int64_t *doc_off, i
   h->n_live = n_live;
   h->sum_len = sum_len;
   if ((rc = compute_idf_table(h, df, order))) return rc;
+  if ((rc = build_head_tiles(h, df))) return rc;
   CM_HIP(hipStreamSynchronize(h->stream));
   if (h->empty_vocab) CM_FAIL(CM_EZERODIV, "float division by zero (every live document has an empty token list)");
   return CM_OK;
@@ -823,6 +1124,7 @@ int cm_bm25_build_dev(cm_bm25 *h, const int32_t *term_ids_dev, const int64_t *do
   h->n_live = ndocs;
   h->sum_len = ntokens;
   if ((rc = compute_idf_table(h, df, order))) return rc;
+  if ((rc = build_head_tiles(h, df))) return rc;
   CM_HIP(hipStreamSynchronize(h->stream));
   if (h->empty_vocab) CM_FAIL(CM_EZERODIV, "float division by zero (every live document has an empty token list)");
   return CM_OK;
@@ -861,6 +1163,23 @@ int cm_bm25_export(cm_bm25 *h, int64_t *term_off, int32_t *post_doc, uint16_t *p
   CM_HIP(hipStreamSynchronize(h->stream));
   return CM_OK;
 }
+
+int cm_bm25_set_head_policy(cm_bm25 *h, double min_df_frac, int64_t max_bytes) {
+  if (!h) CM_FAIL(CM_EINVAL, "null handle");
+  if (!(min_df_frac >= 0.0) || max_bytes < 0) CM_FAIL(CM_EINVAL, "bad head policy");
+  DeviceGuard dg(h->dev);
+  h->head_min_frac = min_df_frac;
+  h->head_max_bytes = max_bytes;
+  if (h->vocab <= 0) return CM_OK;
+  std::vector<int64_t> off((size_t)h->vocab + 1);
+  CM_HIP(hipMemcpyAsync(off.data(), h->term_off.ptr, off.size() * 8, hipMemcpyDeviceToHost, h->stream));
+  CM_HIP(hipStreamSynchronize(h->stream));
+  std::vector<int32_t> df((size_t)h->vocab);
+  for (int32_t t = 0; t < h->vocab; ++t) df[t] = (int32_t)(off[t + 1] - off[t]);
+  return build_head_tiles(h, df);
+}
+
+int32_t cm_bm25_num_head_terms(cm_bm25 *h) { return h ? h->nhead : -1; }
 
 int cm_bm25_set_stats(cm_bm25 *h, const double *idf, int32_t vocab, int64_t n_live, int64_t sum_len, double eps) {
   if (!h || !idf) CM_FAIL(CM_EINVAL, "NULL argument");

@@ -122,6 +122,12 @@ int64_t cm_bm25_num_docs(cm_bm25 *h);
 int64_t cm_bm25_num_postings(cm_bm25 *h);
 /* unfiltered corpus statistics: live docs, total length, avgdl, eps. */
 int cm_bm25_stats(cm_bm25 *h, int64_t *n_live, int64_t *sum_len, double *avgdl, double *eps);
+/* Dense head-term tiles (K2 fast path): terms with df > ndocs * min_df_frac
+ * (highest df first, at most max_bytes of uint8 tf tiles) are scored from a
+ * [term][doc] tf tile instead of their postings.  Default 1/64 and 8 GiB;
+ * max_bytes = 0 disables.  Results are identical either way. */
+int cm_bm25_set_head_policy(cm_bm25 *h, double min_df_frac, int64_t max_bytes);
+int32_t cm_bm25_num_head_terms(cm_bm25 *h);
 /* Sharding support: local df per term and the first posting's
  * (row << 32 | first position) key (0xff..ff when absent), so ranks can
  * all-reduce df (sum) and first keys (min, after offsetting rows) and agree

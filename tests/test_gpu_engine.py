@@ -265,3 +265,95 @@ def test_meanpool_l2norm(eng):
         torch.testing.assert_close(out, ref, atol=2e-6, rtol=1e-5)
         raw = eng.meanpool_l2norm(h, m.to(torch.int32), normalize=False)
         torch.testing.assert_close(raw, (hf * mf).sum(1) / mf.sum(1).clamp(min=1e-9), atol=2e-6, rtol=1e-5)
+
+
+@pytest.mark.parametrize("policy", [(1.0 / 64, 8 << 30), (0.0, 8 << 30), (1.0, 0), (0.0, 0)])
+def test_bm25_head_tile_policies_bit_exact(eng, corpus, policy):
+    """Dense head-term tiles (any split of head/tail terms) give the same bits as the oracle."""
+    toks = [orc.tokenize(t, "en") for t in corpus["texts"]]
+    b, vocab = _build_bm25(eng, toks)
+    b.set_head_policy(*policy)
+    if policy[1] == 0:
+        assert b.num_head_terms == 0
+    elif policy[0] == 0.0:
+        assert b.num_head_terms == len(vocab)
+    ora = orc.BM25Oracle()
+    ora.upsert_many(corpus["ids"], corpus["texts"], corpus["metas"])
+    qs = [[vocab.get(t, -1) for t in orc.tokenize(q, "en")] for q in corpus["qtexts"]]
+    for where in (None, {"course": "math201"}):
+        allow = None if where is None else _bits(np.array([orc.bm25_matches_filter(m, where)
+                                                           for m in corpus["metas"]]))
+        scores, rows, nvalid = b.search(qs, 10, allow)
+        for i, q in enumerate(corpus["qtexts"]):
+            want = ora.search(q, where, top_k=10)
+            got = [[corpus["ids"][r], s] for r, s in zip(rows[i][:nvalid[i]], scores[i][:nvalid[i]])]
+            assert got == [[w["id"], w["score"]] for w in want]
+
+
+def test_bm25_saturated_tf_slow_path(eng):
+    texts = ["spam " * 300 + "eggs", "spam eggs eggs", "eggs", "spam " * 256, "ham"] * 3
+    ids = [f"d{i}" for i in range(len(texts))]
+    toks = [orc.tokenize(t, "en") for t in texts]
+    b, vocab = _build_bm25(eng, toks)
+    b.set_head_policy(0.0, 1 << 30)               # every term in a tile -> tf 300 saturates the byte
+    ora = orc.BM25Oracle()
+    ora.upsert_many(ids, texts, [{"language": "en"}] * len(texts))
+    for q in ["spam", "eggs spam", "ham spam spam"]:
+        scores, rows, nvalid = b.search([[vocab.get(t, -1) for t in orc.tokenize(q, "en")]], 8)
+        want = ora.search(q, None, top_k=8)
+        assert [[ids[r], s] for r, s in zip(rows[0][:nvalid[0]], scores[0][:nvalid[0]])] == \
+            [[w["id"], w["score"]] for w in want]
+
+
+@pytest.mark.parametrize("policy", [(1.0 / 64, 8 << 30), (1.0, 0)])
+def test_bm25_long_queries_and_tail_overflow(eng, corpus, policy):
+    """> 96 query terms per workgroup and > 768 tail postings per range exercise
+    K2's global-memory fallbacks; results stay bit-identical."""
+    texts = corpus["texts"] * 3                      # 3000 docs -> ranges of 1024 docs
+    ids = [f"r{i}" for i in range(len(texts))]
+    toks = [orc.tokenize(t, "en") for t in texts]
+    b, vocab = _build_bm25(eng, toks)
+    b.set_head_policy(*policy)
+    rng = np.random.default_rng(11)
+    words = list(vocab)
+    queries = [" ".join(words[int(x)] for x in rng.integers(0, 40, 45)) for _ in range(6)]   # frequent terms
+    queries += [" ".join(words[int(x)] for x in rng.integers(0, len(words), 30)) for _ in range(3)]
+    ora = orc.BM25Oracle()
+    ora.upsert_many(ids, texts, [{"language": "en"}] * len(texts))
+    qs = [[vocab.get(t, -1) for t in orc.tokenize(q, "en")] for q in queries]
+    scores, rows, nvalid = b.search(qs, 10)
+    for i, q in enumerate(queries):
+        want = ora.search(q, None, top_k=10)
+        assert [[ids[r], s] for r, s in zip(rows[i][:nvalid[i]], scores[i][:nvalid[i]])] == \
+            [[w["id"], w["score"]] for w in want]
+
+
+@pytest.mark.parametrize("policy", [(1.0 / 64, 8 << 30), (1.0, 0)])
+def test_bm25_many_ranges_vs_c_oracle(eng, policy):
+    """~150 ranges of 1024 docs: K2's per-query global threshold pruning and the K3
+    merge must keep the exact oracle top-k (ties by row, zero-score padding for a
+    rare term, k up to the 256 maximum)."""
+    from oracle import corc
+    rng = np.random.default_rng(5)
+    nd, vocab = 150_000, 4000
+    lens = np.maximum(rng.poisson(30, nd), 1)
+    off = np.zeros(nd + 1, np.int64)
+    off[1:] = np.cumsum(lens)
+    p = 1.0 / np.arange(1, vocab + 1) ** 1.1
+    toks = rng.choice(vocab, size=int(off[-1]), p=p / p.sum()).astype(np.int32)
+    b = eng.BM25Index()
+    b.build(toks, off, vocab)
+    b.set_head_policy(*policy)
+    csr = corc.build_csr(toks, off, vocab)
+    idf, _ = corc.bm25_idf(csr["df"], csr["first_key"], nd)
+    avgdl = float(lens.sum()) / nd
+    rare = int(np.nonzero(csr["df"] == csr["df"][csr["df"] > 0].min())[0][0])
+    queries = [rng.integers(0, vocab, 6).tolist() for _ in range(20)]
+    queries += [[0, 1, 2], [3, 3, 7], [rare], [rare, vocab - 1], [int(x) for x in rng.integers(0, 50, 40)]]
+    for k in (1, 10, 256):
+        scores, rows, nvalid = b.search(queries, k)
+        o_sc, o_rw = corc.bm25_topk(csr, idf, avgdl, queries, k)
+        for i in range(len(queries)):
+            assert nvalid[i] == k
+            assert rows[i][:k].tolist() == o_rw[i].tolist(), (k, i)
+            assert scores[i][:k].tolist() == o_sc[i].tolist(), (k, i)

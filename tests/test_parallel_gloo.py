@@ -1,0 +1,147 @@
+"""World-size-2 (gloo, CPU) tests of the multi-GPU exchange steps in
+classmate_hip.parallel: sharded BM25 statistics must give the
+single-shard idf table / avgdl bit-for-bit, and the all-gather top-k merges must
+give the unsharded oracle top-k (ties by global row, zero-score padding).
+
+Per-shard top-k here comes from the C oracle (no GPU); on the GPU the same merge
+consumes the HIP shards' outputs (bench.py).
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from oracle import corc
+
+WS = 2
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _corpus(seed=3, nd=6000, vocab=700):
+    rng = np.random.default_rng(seed)
+    lens = np.maximum(rng.poisson(12, nd), 1)
+    off = np.zeros(nd + 1, np.int64)
+    off[1:] = np.cumsum(lens)
+    p = 1.0 / np.arange(1, vocab + 1) ** 1.2
+    toks = rng.choice(vocab, size=int(off[-1]), p=p / p.sum()).astype(np.int32)
+    toks[toks == vocab - 1] = 0                      # term vocab-1 absent everywhere
+    rare = int(vocab - 2)
+    toks[np.isin(toks, [rare])] = 1
+    toks[off[nd - 3]] = rare                         # rare term: a single doc, in the last shard
+    queries = [rng.integers(0, 60, 5).tolist() for _ in range(12)] + [[rare], [rare, vocab - 1], [0, 0, 3]]
+    return toks, off, vocab, queries
+
+
+def _worker(rank, port, out_q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(WS))
+    dist.init_process_group("gloo", rank=rank, world_size=WS)
+    try:
+        from classmate_hip import parallel as P
+        toks, off, vocab, queries = _corpus()
+        nd = off.shape[0] - 1
+        row0, n = P.shard_range(nd, rank, WS)
+        loc_off = off[row0:row0 + n + 1] - off[row0]
+        loc_toks = toks[off[row0]:off[row0 + n]]
+        csr = corc.build_csr(loc_toks, loc_off, vocab)
+        df, fk, n_all, sum_len = P.allreduce_bm25_stats(csr["df"], csr["first_key"], row0, n,
+                                                        int(loc_off[-1]))
+        idf, eps = P.bm25_idf_table(df, fk, n_all)
+        avgdl = sum_len / n_all
+        res = {"rank": rank, "idf": idf, "eps": eps, "avgdl": avgdl, "n": n_all}
+        # BM25: shard top-k with global statistics, then the all-gather merge
+        for k in (1, 10, 64):
+            sc, rw = corc.bm25_topk(csr, idf, avgdl, queries, k)
+            S, R = P.merge_bm25_topk(torch.from_numpy(sc), torch.from_numpy(rw + row0), k)
+            res[f"bm25_{k}"] = (S.numpy(), R.numpy())
+        # dense: shard top-k (f32 distances) then merge
+        rng = np.random.default_rng(8)
+        emb = rng.standard_normal((nd, 32)).astype(np.float32)
+        emb[5] = emb[4]                               # exact duplicate rows across the shard boundary region
+        emb[nd // 2 + 1] = emb[4]
+        q = rng.standard_normal((6, 32)).astype(np.float32)
+        q[0] = emb[4]
+        d, r = corc.dense_topk_f64(emb[row0:row0 + n], q, 16)
+        D, R = P.merge_dense_topk(torch.from_numpy(d.astype(np.float32)), torch.from_numpy(r + row0), 16)
+        res["dense"] = (D.numpy(), R.numpy())
+        # pool assembly: owner contributes its rows
+        rows = torch.tensor([[0, nd - 1, nd // 2, 7]])
+        own = (rows >= row0) & (rows < row0 + n)
+        local = torch.from_numpy(emb)[rows.clamp(0, nd - 1)] * own.unsqueeze(-1)
+        res["pool"] = P.assemble_pool_vectors(rows, local, row0, n).numpy()
+        res["max"] = P.max_over_ranks(float(rank) + 0.5)
+        out_q.put(res)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.fixture(scope="module")
+def results():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, port, q)) for r in range(WS)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=240) for _ in range(WS)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return sorted(out, key=lambda r: r["rank"])
+
+
+def test_sharded_stats_equal_single_shard(results):
+    toks, off, vocab, _ = _corpus()
+    csr = corc.build_csr(toks, off, vocab)
+    idf, eps = corc.bm25_idf(csr["df"], csr["first_key"], off.shape[0] - 1)
+    for r in results:
+        assert r["n"] == off.shape[0] - 1
+        assert r["eps"] == eps
+        assert np.array_equal(r["idf"][csr["df"] > 0], idf[csr["df"] > 0])
+        assert r["avgdl"] == float(off[-1]) / (off.shape[0] - 1)
+
+
+@pytest.mark.parametrize("k", [1, 10, 64])
+def test_bm25_merge_equals_unsharded_oracle(results, k):
+    toks, off, vocab, queries = _corpus()
+    csr = corc.build_csr(toks, off, vocab)
+    idf, _ = corc.bm25_idf(csr["df"], csr["first_key"], off.shape[0] - 1)
+    sc, rw = corc.bm25_topk(csr, idf, float(off[-1]) / (off.shape[0] - 1), queries, k)
+    for r in results:                                  # identical on every rank
+        S, R = r[f"bm25_{k}"]
+        assert np.array_equal(R, rw)
+        assert np.array_equal(S, sc)
+
+
+def test_dense_merge_equals_unsharded(results):
+    rng = np.random.default_rng(8)
+    toks, off, _, _ = _corpus()
+    nd = off.shape[0] - 1
+    emb = rng.standard_normal((nd, 32)).astype(np.float32)
+    emb[5] = emb[4]
+    emb[nd // 2 + 1] = emb[4]
+    q = rng.standard_normal((6, 32)).astype(np.float32)
+    q[0] = emb[4]
+    d, r = corc.dense_topk_f64(emb, q, 16)
+    for res in results:
+        D, R = res["dense"]
+        assert np.array_equal(R, r)                    # ties (duplicate rows) by ascending global row
+        np.testing.assert_array_equal(D, d.astype(np.float32))
+
+
+def test_pool_assembly_and_max(results):
+    toks, off, _, _ = _corpus()
+    nd = off.shape[0] - 1
+    emb = np.random.default_rng(8).standard_normal((nd, 32)).astype(np.float32)
+    want = emb[[0, nd - 1, nd // 2, 7]]
+    for r in results:
+        np.testing.assert_array_equal(r["pool"][0], want)
+        assert r["max"] == 1.5

@@ -1,0 +1,43 @@
+"""Ablation/profiling probe for the BM25 kernels at the bench's 10M shape (not a test).
+
+python tools/bm25_probe.py [--docs N] [--batch B] [--reps R]
+Env CM_BM25_DEBUG=1 (skip scoring) / 2 (skip range top-k) for ablations.
+"""
+import argparse
+import os
+import sys
+import time
+from pathlib import Path
+
+REPO = Path(__file__).resolve().parents[1]
+sys.path[:0] = [str(REPO), str(REPO / "classmate-rag_amd")]
+import torch  # noqa: E402
+from bench import gen_tokens, sample_query_terms  # noqa: E402
+from classmate_hip import engine  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--docs", type=int, default=10_000_000)
+ap.add_argument("--batch", type=int, default=256)
+ap.add_argument("--reps", type=int, default=5)
+ap.add_argument("--head-frac", type=float, default=1.0 / 64)
+ap.add_argument("--head-bytes", type=int, default=8 << 30)
+a = ap.parse_args()
+tok, off = gen_tokens(a.docs, 1 << 20, 1.07, 120.0, seed=1500)
+b = engine.BM25Index()
+b.build_dev(tok, off, 1 << 20)
+b.set_head_policy(a.head_frac, a.head_bytes)
+qt = sample_query_terms(tok, off, a.batch, 8, seed=10)
+q_terms = qt.reshape(-1).contiguous()
+q_off = (torch.arange(a.batch + 1, device="cuda", dtype=torch.int32) * 8).contiguous()
+out = b.search_dev(q_terms, q_off, 10)
+torch.cuda.synchronize()
+ts = []
+for _ in range(a.reps):
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    b.search_dev(q_terms, q_off, 10, out=out)
+    e1.record()
+    torch.cuda.synchronize()
+    ts.append(e0.elapsed_time(e1))
+print(f"docs={a.docs} B={a.batch} head_terms={b.num_head_terms} dbg={os.environ.get('CM_BM25_DEBUG', '0')} "
+      f"search_ms={sorted(ts)[len(ts) // 2]:.3f} all={['%.2f' % t for t in ts]}", flush=True)
