@@ -37,7 +37,6 @@ namespace cm {
 
 constexpr int kRange = 1024;                 // docs per range (one wave's LDS score tile)
 constexpr int kBmThreads = 256;              // 4 waves = 4 queries per K2 workgroup
-constexpr int kQPerBlock = kBmThreads / 64;
 constexpr int kBoundsGroup = 64;             // ranges per bounds thread (gallop between them)
 constexpr int kMergeThreads = 1024;
 constexpr int kMergePer = 16;                // lists per merge thread -> <= 16384 ranges (16.7M docs)
@@ -141,35 +140,41 @@ __global__ void bm25_bounds_kernel(const int32_t *__restrict__ q_terms, int n_te
   }
 }
 
-// K2: one wave per (query, group of consecutive ranges of kRange docs); the
-// 4 waves of a workgroup are 4 consecutive queries over the same ranges, and
-// workgroups are remapped so each XCD owns a contiguous run of range groups
-// (every query's head tiles for those ranges then share that XCD's L2).
+// K2: one wave per (group of 4 queries, group of consecutive ranges of kRange
+// docs); the 4 waves of a workgroup take 4 consecutive query groups over the
+// same ranges, and workgroups are remapped so each XCD owns a contiguous run of
+// range groups (all queries' head tiles for those ranges share that XCD's L2).
 // Waves never synchronise with each other.
 //
 // Lane l owns docs d0 + 16l .. d0 + 16l + 15 of the current range and keeps
-// their K_d and fp64 scores in registers.  Lane j (< 64) holds the descriptor
-// of query term j (term, head id, idf, tail postings [lo, hi) of the range).
-// Per range:
-//   * the range's tail postings of all the query's tail terms are gathered into
-//     the wave's LDS slice with one coalesced pass (term-major, doc-sorted);
-//   * terms are applied in query order (duplicates twice), so every document
-//     sums its contributions in rank_bm25's order:
+// their K_d (computed once per range, shared by the 4 queries) and the current
+// query's fp64 scores in registers.  Lane 16q + j holds the descriptor of term
+// j (< 16) of the wave's query q (term, head id, idf, tail postings [lo, hi) of
+// the range).  Per range:
+//   * the range's tail postings of all 4 queries' tail terms are gathered into
+//     the wave's LDS slice with one coalesced pass (query/term-major, doc-sorted);
+//   * per query, terms are applied in query order (duplicates twice), so every
+//     document sums its contributions in rank_bm25's order:
 //       - head term: 16 tf bytes per lane from the dense tile (a 2-deep
-//         prefetch ring runs over the (range, head term) sequence), 16
+//         prefetch ring runs over the (range, query, head term) sequence), 16
 //         predicated independent register updates;
 //       - tail term: each lane binary-searches its 16-doc window in the
-//         term's LDS postings and applies the (usually 0-1) hits;
-//   * top-k of the range, pruned by the query's global threshold T (atomicMin
-//     of every range's k-th best key: any range's k-th best bounds the global
-//     k-th best), so most ranges stop after one argmin.
+//         term's LDS postings and walks the (usually 0-1) hits slot by slot;
+//   * top-k of the (range, query), pruned by the query's global threshold T
+//     (atomicMin of every range's k-th best key: any range's k-th best bounds
+//     the global k-th best), so most ranges stop after one argmin.
 // dl / live / allow words and the tail bounds of range r+1 are loaded while
 // range r is scored.
-constexpr int kTailCapW = 320;  // tail postings gathered per (wave, range); overflow terms read from global
+constexpr int kTailCapW = 512;  // tail postings gathered per (wave, range); overflow terms read from global
 constexpr int kMaxRangesPerWave = 16;
-#ifndef K2_SLOT_GROUP
-#define K2_SLOT_GROUP 4
-#endif
+// Ratio table: tf*2.5 / (tf + K_d) depends on (tf, dl) only, so per search the
+// quotients for dl in [lut_dmin, lut_dmin + kLutW) and tf < kLutTF are computed
+// once (IEEE division, bit-identical to the per-posting quotient) and K2 reads
+// them from LDS; other (dl, tf) pairs divide in place.
+constexpr int kLutW = 128;
+constexpr int kLutTF = 16;
+constexpr int kQPerWave = 4;    // queries per wave; lanes 16q..16q+15 hold query q's first 16 term descriptors
+constexpr int kTermLanes = 64 / kQPerWave;
 #ifndef K2_WAVES_PER_EU
 #define K2_WAVES_PER_EU 2
 #endif
@@ -180,23 +185,59 @@ __device__ inline double bm25_contrib(double idf, uint32_t tfi, double kdv) {
   const double den = tf + kdv;
   return idf * (num / den);
 }
+// Same bits as bm25_contrib for every operand K2 can see (tf in [0, 65535], kd in
+// [0.375, 2^40)): the quotient is the compiler's IEEE division sequence (rcp, two
+// Newton steps, residual correction) without v_div_scale / v_div_fixup, which are
+// identities when neither operand is near the exponent range limits.
+__device__ inline double bm25_contrib_fast(double idf, uint32_t tfi, double kdv) {
+  const double tf = (double)tfi;
+  const double num = tf * 2.5;
+  const double den = tf + kdv;
+  double r = __builtin_amdgcn_rcp(den);
+  double e = __builtin_fma(-den, r, 1.0);
+  r = __builtin_fma(r, e, r);
+  e = __builtin_fma(-den, r, 1.0);
+  r = __builtin_fma(r, e, r);
+  const double q0 = num * r;
+  const double rem = __builtin_fma(-den, q0, num);
+  return idf * __builtin_fma(rem, r, q0);
+}
+__device__ inline double kd_of(int32_t dlen, double avgdl) {
+  double t = 0.75 * (double)dlen;
+  t = t / avgdl;
+  t = 0.25 + t;
+  return 1.5 * t;
+}
+__global__ void bm25_lut_kernel(double avgdl, int dmin, double *__restrict__ lut) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= kLutW * kLutTF) return;
+  const int tf = i % kLutTF, dl = dmin + i / kLutTF;
+  if (tf == 0) {
+    lut[i] = 0.0;
+    return;
+  }
+  const double t = (double)tf;
+  const double num = t * 2.5;
+  const double den = t + kd_of(dl, avgdl);
+  lut[i] = num / den;
+}
 __device__ inline double readlane_f64(double v, int j) {
   const uint64_t b = __double_as_longlong(v);
   const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)b, j);
   const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(b >> 32), j);
   return __longlong_as_double(((uint64_t)hi << 32) | lo);
 }
-__device__ inline int64_t readlane_i64(int64_t v, int j) {
-  const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)(uint64_t)v, j);
-  const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)((uint64_t)v >> 32), j);
-  return (int64_t)(((uint64_t)hi << 32) | lo);
+__device__ inline uint64_t readlane_u64(uint64_t v, int j) {
+  const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)v, j);
+  const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(v >> 32), j);
+  return ((uint64_t)hi << 32) | lo;
 }
 __device__ inline void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
-// first index in [lo, hi) of a doc-sorted posting list (LDS or global) with doc >= target
+// first index in [lo, hi) of a doc-sorted posting list with doc >= target
 template <typename P>
 __device__ inline int first_ge(const P *__restrict__ a, int lo, int hi, int32_t target) {
   while (lo < hi) {
@@ -205,12 +246,6 @@ __device__ inline int first_ge(const P *__restrict__ a, int lo, int hi, int32_t 
     else hi = mid;
   }
   return lo;
-}
-__device__ inline double kd_of(int32_t dlen, double avgdl) {
-  double t = 0.75 * (double)dlen;
-  t = t / avgdl;
-  t = 0.25 + t;
-  return 1.5 * t;
 }
 
 template <typename TF>
@@ -221,10 +256,15 @@ __global__ void __launch_bounds__(kBmThreads) __attribute__((amdgpu_waves_per_eu
                       const TF *__restrict__ post_tf, const int32_t *__restrict__ head_id,
                       const uint8_t *__restrict__ headtf, int64_t npad, const int32_t *__restrict__ dl,
                       const uint32_t *__restrict__ live, const uint32_t *__restrict__ allow, int64_t ndocs,
-                      double avgdl, int k, uint64_t *__restrict__ cand_key, uint32_t *__restrict__ cand_row,
+                      double avgdl, const double *__restrict__ lut, int lut_dmin, int k,
+                      uint64_t *__restrict__ cand_key, uint32_t *__restrict__ cand_row,
                       unsigned long long *__restrict__ thr_key, int dbg) {
-  __shared__ int32_t s_pdoc[kQPerBlock][kTailCapW];
-  __shared__ uint16_t s_ptf[kQPerBlock][kTailCapW];
+  __shared__ double s_lut[kLutW * kLutTF];
+  __shared__ int32_t s_pdoc[kBmThreads / 64][kTailCapW];
+  __shared__ uint16_t s_ptf[kBmThreads / 64][kTailCapW];
+  __shared__ uint64_t s_keys[kBmThreads / 64][16 * 64];
+  for (int i = threadIdx.x; i < kLutW * kLutTF; i += kBmThreads) s_lut[i] = lut[i];
+  __syncthreads();  // the only block-wide barrier
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   // XCD-aware remap: hardware places workgroup b on XCD b % 8
@@ -232,31 +272,38 @@ __global__ void __launch_bounds__(kBmThreads) __attribute__((amdgpu_waves_per_eu
   const int b = blockIdx.x;
   const int per = nb >> 3, rem = nb & 7, x = b & 7, y = b >> 3;
   const int lb = (x < rem ? x * (per + 1) : rem * (per + 1) + (x - rem) * per) + y;
-  const int nqg = (nq + kQPerBlock - 1) / kQPerBlock;
-  const int qi = (lb % nqg) * kQPerBlock + wave;
-  const int rg = lb / nqg;
-  if (qi >= nq) return;
+  const int nqg = (nq + kQPerWave - 1) / kQPerWave;
+  const int wid = lb * (kBmThreads / 64) + wave;
+  const int q0 = (wid % nqg) * kQPerWave;
+  const int rg = wid / nqg;
   const int r0 = rg * rpw, r1 = min(r0 + rpw, nr);
-  if (r0 >= r1) return;
+  if (r0 >= r1) return;  // whole wave
+  const int nqw = min(kQPerWave, nq - q0);
   int32_t *pdoc = s_pdoc[wave];
   uint16_t *ptf = s_ptf[wave];
-  const int tb = q_off[qi];
-  const int L = q_off[qi + 1] - tb;
+  uint64_t *keys = s_keys[wave];
   const int64_t bstride = nr + 1;
-  // ---- per-wave term descriptors (lane j <-> query term j < 64)
+  // ---- per-wave term descriptors (lane 16q + j <-> term j of query q0 + q)
+  const int my_q = lane / kTermLanes, my_j = lane % kTermLanes;
+  int my_tb = 0, my_L = 0;
+  if (my_q < nqw) {
+    my_tb = q_off[q0 + my_q];
+    my_L = q_off[q0 + my_q + 1] - my_tb;
+  }
+  const bool has_term = my_q < nqw && my_j < my_L;
+  const int my_i = my_tb + my_j;
   int32_t my_t = -1, my_h = -1;
   double my_idf = 0.0;
   int64_t my_lo = 0, my_hi = 0;
-  if (lane < L) {
-    my_t = q_terms[tb + lane];
-    my_idf = q_idf[tb + lane];
+  if (has_term) {
+    my_t = q_terms[my_i];
+    my_idf = q_idf[my_i];
     my_h = (my_t >= 0 && head_id) ? head_id[my_t] : -1;
-    my_lo = bounds[(int64_t)(tb + lane) * bstride + r0];
-    my_hi = bounds[(int64_t)(tb + lane) * bstride + r0 + 1];
+    my_lo = bounds[(int64_t)my_i * bstride + r0];
+    my_hi = bounds[(int64_t)my_i * bstride + r0 + 1];
   }
-  const uint64_t headmask = __ballot(lane < L && my_t >= 0 && my_h >= 0);
-  unsigned long long *tq = thr_key + qi;
-  // ---- head-tile prefetch ring over the (range, head term) sequence
+  const uint64_t headmask = __ballot(has_term && my_t >= 0 && my_h >= 0);
+  // ---- head-tile prefetch ring over the (range, query, head term) sequence
   int c_r = r0;
   uint64_t c_m = headmask;
   auto tile_at = [&](int r, uint64_t m) -> uint4 {
@@ -276,7 +323,7 @@ __global__ void __launch_bounds__(kBmThreads) __attribute__((amdgpu_waves_per_eu
   if (headmask) advance(c_r, c_m);
   uint4 n2 = tile_at(c_r, c_m);
   if (headmask) advance(c_r, c_m);
-  // ---- range r: dl / bitmap words (loaded one range ahead)
+  // ---- range words (loaded one range ahead)
   int4 dlq[4];
   uint32_t lw = 0, aw = 0xffffffffu;
   auto load_range_words = [&](int r) {
@@ -300,20 +347,35 @@ __global__ void __launch_bounds__(kBmThreads) __attribute__((amdgpu_waves_per_eu
   for (int r = r0; r < r1; ++r) {
     const int64_t d0 = (int64_t)r * kRange;
     const int64_t db = d0 + 16 * lane;
-    double kdr[16];
+    // thresholds of the wave's queries (lanes 0..nqw-1); latency hidden behind K_d
+    uint64_t Tv = kEmptyKey;
+    if (lane < nqw && !(dbg & 2)) Tv = __hip_atomic_load(thr_key + q0 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (dbg & 2) Tv = 0;
+    // LUT row base (dl - lut_dmin) * kLutTF per slot, 0xffff = outside the table (packed 2 x 16 bit)
+    uint32_t lbp[8];
     {
       const int32_t dlv[16] = {dlq[0].x, dlq[0].y, dlq[0].z, dlq[0].w, dlq[1].x, dlq[1].y, dlq[1].z, dlq[1].w,
                                dlq[2].x, dlq[2].y, dlq[2].z, dlq[2].w, dlq[3].x, dlq[3].y, dlq[3].z, dlq[3].w};
 #pragma unroll
-      for (int u = 0; u < 16; ++u) kdr[u] = kd_of(dlv[u], avgdl);
+      for (int v = 0; v < 8; ++v) {
+        const uint32_t r0 = (uint32_t)(dlv[2 * v] - lut_dmin), r1 = (uint32_t)(dlv[2 * v + 1] - lut_dmin);
+        const uint32_t b0 = r0 < (uint32_t)kLutW ? r0 * kLutTF : 0xffffu;
+        const uint32_t b1 = r1 < (uint32_t)kLutW ? r1 * kLutTF : 0xffffu;
+        lbp[v] = b0 | (b1 << 16);
+      }
     }
+    // contribution of (slot u, tf) from the table, or by division off the table
+    auto lut_base = [&](int u) -> uint32_t { return (lbp[u >> 1] >> (16 * (u & 1))) & 0xffffu; };
+    auto slow_contrib = [&](int u, double idf, uint32_t tfi) -> double {
+      return bm25_contrib_fast(idf, tfi, kd_of(dl[db + u], avgdl));
+    };
     uint32_t okmask = 0;
     if (db < ndocs) {
       okmask = ((lw & aw) >> (db & 31)) & 0xffffu;
       const int64_t rm = ndocs - db;
       if (rm < 16) okmask &= (1u << rm) - 1u;
     }
-    // this range's tail postings -> LDS (term-major); next range's words/bounds in flight
+    // this range's tail postings -> LDS; next range's words/bounds in flight
     const int cnt = (int)(my_hi - my_lo);
     int incl = cnt;
 #pragma unroll
@@ -336,163 +398,165 @@ __global__ void __launch_bounds__(kBmThreads) __attribute__((amdgpu_waves_per_eu
       // several lanes can share an offset (empty terms): the last one is the one with postings
       const int64_t src = __shfl(my_lo, lo) + (e - __shfl(excl, lo));
       if (e < n_in) {
-        const int32_t doc = post_doc[src];
-        pdoc[e] = doc;
+        pdoc[e] = post_doc[src];
         ptf[e] = (uint16_t)post_tf[src];
       }
     }
     int64_t nx_lo = my_hi, nx_hi = my_hi;
     if (r + 1 < r1) {
       load_range_words(r + 1);
-      if (lane < L) nx_hi = bounds[(int64_t)(tb + lane) * bstride + r + 2];
+      if (has_term) nx_hi = bounds[(int64_t)my_i * bstride + r + 2];
     }
     wave_lds_sync();
-    double sc[16];
-#pragma unroll
-    for (int u = 0; u < 16; ++u) sc[u] = 0.0;
     const int32_t wlo = (int32_t)(db - d0), whi = wlo + 16;  // this lane's window, range-relative
-    if (!(dbg & 1)) {
-      for (int j = 0; j < L; ++j) {
-        int32_t t, hh;
-        double idf;
-        int c, off;
-        int64_t plo;
-        if (j < 64) {
-          t = __builtin_amdgcn_readlane(my_t, j);
-          hh = __builtin_amdgcn_readlane(my_h, j);
-          idf = readlane_f64(my_idf, j);
-          c = __builtin_amdgcn_readlane(cnt, j);
-          off = __builtin_amdgcn_readlane(my_off, j);
-          plo = readlane_i64(my_lo, j);
-        } else {  // long query: descriptor from global, postings from global
-          const int i = tb + j;
-          t = q_terms[i];
-          hh = (t >= 0 && head_id) ? head_id[t] : -1;
-          idf = q_idf[i];
-          plo = bounds[(int64_t)i * bstride + r];
-          c = (int)(bounds[(int64_t)i * bstride + r + 1] - plo);
-          off = -1;
-        }
-        if (t < 0) continue;
-        if (hh >= 0) {
-          uint4 v;
-          if (j < 64) {
-            v = n1;
-            n1 = n2;
-            n2 = tile_at(c_r, c_m);
-            advance(c_r, c_m);
-          } else {
-            v = *reinterpret_cast<const uint4 *>(headtf + (int64_t)hh * npad + db);
-          }
-          const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
-          uint32_t satm = 0;
+    for (int qq = 0; qq < nqw; ++qq) {
+      const int qi = q0 + qq;
+      const int base = qq * kTermLanes;
+      const int L = __builtin_amdgcn_readlane(my_L, base);
+      double sc[16];
 #pragma unroll
-          for (int u = 0; u < 16; ++u) {
-            const uint32_t tfi = (wv[u >> 2] >> (8 * (u & 3))) & 0xffu;
-            if (tfi == 255u) satm |= 1u << u;
-            else if (tfi != 0u) sc[u] = sc[u] + bm25_contrib(idf, tfi, kdr[u]);
-            if ((u & (K2_SLOT_GROUP - 1)) == K2_SLOT_GROUP - 1) __builtin_amdgcn_sched_barrier(0);  // bound live temps
+      for (int u = 0; u < 16; ++u) sc[u] = 0.0;
+      if (!(dbg & 1)) {
+        for (int j = 0; j < L; ++j) {
+          int32_t t, hh;
+          double idf;
+          int c, off;
+          int64_t plo;
+          if (j < kTermLanes) {
+            const int ln = base + j;
+            t = __builtin_amdgcn_readlane(my_t, ln);
+            hh = __builtin_amdgcn_readlane(my_h, ln);
+            idf = readlane_f64(my_idf, ln);
+            c = __builtin_amdgcn_readlane(cnt, ln);
+            off = __builtin_amdgcn_readlane(my_off, ln);
+            plo = (int64_t)readlane_u64((uint64_t)my_lo, ln);
+          } else {  // long query: descriptor, bounds and postings from global
+            const int i = __builtin_amdgcn_readlane(my_tb, base) + j;
+            t = q_terms[i];
+            hh = (t >= 0 && head_id) ? head_id[t] : -1;
+            idf = q_idf[i];
+            plo = bounds[(int64_t)i * bstride + r];
+            c = (int)(bounds[(int64_t)i * bstride + r + 1] - plo);
+            off = -1;
           }
-          if (satm) {  // saturated byte (tf >= 255): exact tf from the postings
+          if (t < 0) continue;
+          if (hh >= 0) {
+            uint4 v;
+            if (j < kTermLanes) {
+              v = n1;
+              n1 = n2;
+              n2 = tile_at(c_r, c_m);
+              advance(c_r, c_m);
+            } else {
+              v = *reinterpret_cast<const uint4 *>(headtf + (int64_t)hh * npad + db);
+            }
+            const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
+            if (__ballot((wv[0] | wv[1] | wv[2] | wv[3]) != 0u) == 0) continue;  // no doc of the range has the term
+            // branch-free: tf == 0 (and off-table slots) read the table's 0.0 entry, adding
+            // idf * +-0.0, which leaves a (never -0.0) score unchanged
+            uint32_t slowm = 0;
 #pragma unroll
             for (int u = 0; u < 16; ++u) {
-              if ((satm >> u) & 1u) {
-                const int64_t p = lower_bound_doc(post_doc, term_off[t], term_off[t + 1], (int32_t)(db + u));
-                sc[u] = sc[u] + bm25_contrib(idf, (uint32_t)post_tf[p], kdr[u]);
-              }
+              const uint32_t tfi = (wv[u >> 2] >> (8 * (u & 3))) & 0xffu;
+              const uint32_t b = lut_base(u);
+              const bool ok = b != 0xffffu && tfi < (uint32_t)kLutTF;
+              sc[u] = sc[u] + idf * s_lut[ok ? b + tfi : 0u];
+              if (!ok && tfi != 0u) slowm |= 1u << u;
             }
-          }
-        } else if (c > 0) {
-          // lane's window [wlo, whi) of the term's doc-sorted postings: walk it slot by slot
-          // (compile-time register indices; a wave skips the block when no lane has a hit)
-          if (off >= 0) {
-            int e = first_ge(pdoc + off, 0, c, (int32_t)d0 + wlo);
-            int32_t nd = e < c ? pdoc[off + e] - (int32_t)d0 : INT32_MAX;
+            if (slowm) {
+#pragma unroll
+              for (int u = 0; u < 16; ++u)
+                if ((slowm >> u) & 1u)
+                  sc[u] = sc[u] + slow_contrib(u, idf, (wv[u >> 2] >> (8 * (u & 3))) & 0xffu);
+            }
+          } else if (c > 0) {
+            // lane's window [wlo, whi) of the term's doc-sorted postings (LDS, or global on
+            // overflow: one flat-pointer path), walked slot by slot (compile-time register
+            // indices; the wave skips the block when no lane has a hit)
+            const int32_t *pd = off >= 0 ? pdoc + off : post_doc + plo;
+            const TF *pt = off >= 0 ? reinterpret_cast<const TF *>(ptf + off) : post_tf + plo;
+            int e = first_ge(pd, 0, c, (int32_t)d0 + wlo);
+            int32_t nd = e < c ? pd[e] - (int32_t)d0 : INT32_MAX;
             if (nd < whi) {
 #pragma unroll
               for (int u = 0; u < 16; ++u) {
                 if (nd == wlo + u) {
-                  sc[u] = sc[u] + bm25_contrib(idf, ptf[off + e], kdr[u]);
+                  const uint32_t tfi = (uint32_t)pt[e];
+                  const uint32_t b = lut_base(u);
+                  sc[u] = sc[u] + ((b != 0xffffu && tfi < (uint32_t)kLutTF) ? idf * s_lut[b + tfi]
+                                                                             : slow_contrib(u, idf, tfi));
                   ++e;
-                  nd = e < c ? pdoc[off + e] - (int32_t)d0 : INT32_MAX;
-                }
-              }
-            }
-          } else {
-            int64_t e = lower_bound_doc(post_doc, plo, plo + c, (int32_t)db);
-            int32_t nd = e < plo + c ? post_doc[e] - (int32_t)d0 : INT32_MAX;
-            if (nd < whi) {
-#pragma unroll
-              for (int u = 0; u < 16; ++u) {
-                if (nd == wlo + u) {
-                  sc[u] = sc[u] + bm25_contrib(idf, (uint32_t)post_tf[e], kdr[u]);
-                  ++e;
-                  nd = e < plo + c ? post_doc[e] - (int32_t)d0 : INT32_MAX;
+                  nd = e < c ? pd[e] - (int32_t)d0 : INT32_MAX;
                 }
               }
             }
           }
         }
-      }
-    } else if (headmask) {  // ablation: keep the ring in step
-      for (int j = 0; j < min(L, 64); ++j)
-        if ((headmask >> j) & 1) {
+      } else {  // ablation: keep the ring in step
+        uint64_t m = headmask & (((1ull << kTermLanes) - 1) << base);
+        for (; m; m &= m - 1) {
           n1 = n2;
           n2 = tile_at(c_r, c_m);
           advance(c_r, c_m);
         }
-    }
-    // ---- top-k of this (range, query), pruned by the query's global threshold
-    uint32_t taken = 0;
-    auto local_best = [&](uint64_t &bk, uint32_t &br) {
-      bk = kEmptyKey;
-      br = 0xffffffffu;
+      }
+      // ---- top-k of this (range, query), pruned by the query's global threshold
+      // keys -> the wave's LDS key tile (slot-major: conflict-free), lane best in registers;
+      // only the lane whose best is taken rescans its 16 keys
+      uint64_t bk = kEmptyKey;
+      int bu = 0;
 #pragma unroll
       for (int u = 0; u < 16; ++u) {
-        if (((okmask >> u) & 1u) && !((taken >> u) & 1u)) {
-          const uint64_t key = score_key(sc[u]);
-          if (key < bk) {  // u ascending == row ascending within the lane
-            bk = key;
-            br = (uint32_t)(db + u);
-          }
+        const uint64_t key = ((okmask >> u) & 1u) ? score_key(sc[u]) : kEmptyKey;
+        keys[u * 64 + lane] = key;
+        if (key < bk) {  // u ascending == row ascending within the lane
+          bk = key;
+          bu = u;
         }
       }
-    };
-    uint64_t bk;
-    uint32_t br;
-    local_best(bk, br);
-    const uint64_t T = (dbg & 2) ? 0ull : __hip_atomic_load(tq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    int i = 0;
-    uint64_t last = kEmptyKey;
-    for (; i < k; ++i) {
-      uint64_t mk = bk;
-      uint32_t mr = br;
-      wave_min_pair(mk, mr);
-      if (mr == 0xffffffffu || mk > T) break;  // nothing left that can enter the global top-k
-      if (lane == 0) {
-        const int64_t o = ((int64_t)qi * nr + r) * k + i;
-        cand_key[o] = mk;
-        cand_row[o] = mr;
+      uint32_t br = bk == kEmptyKey ? 0xffffffffu : (uint32_t)db + (uint32_t)bu;
+      const uint64_t T = readlane_u64(Tv, qq);
+      int i = 0;
+      uint64_t last = kEmptyKey;
+      for (; i < k; ++i) {
+        uint64_t mk = bk;
+        uint32_t mr = br;
+        wave_min_pair(mk, mr);
+        if (mr == 0xffffffffu || mk > T) break;  // nothing left that can enter the global top-k
+        if (lane == 0) {
+          const int64_t o = ((int64_t)qi * nr + r) * k + i;
+          cand_key[o] = mk;
+          cand_row[o] = mr;
+        }
+        last = mk;
+        if (br == mr && bk == mk) {
+          keys[(int)(mr - (uint32_t)db) * 64 + lane] = kEmptyKey;
+          bk = kEmptyKey;
+          bu = 0;
+          for (int u = 0; u < 16; ++u) {
+            const uint64_t key = keys[u * 64 + lane];
+            if (key < bk) {
+              bk = key;
+              bu = u;
+            }
+          }
+          br = bk == kEmptyKey ? 0xffffffffu : (uint32_t)db + (uint32_t)bu;
+        }
       }
-      last = mk;
-      if (br == mr && bk == mk) {
-        taken |= 1u << (mr - (uint32_t)db);
-        local_best(bk, br);
+      for (int j = i + lane; j < k; j += 64) {
+        const int64_t o = ((int64_t)qi * nr + r) * k + j;
+        cand_key[o] = kEmptyKey;
+        cand_row[o] = 0xffffffffu;
       }
+      if (i == k && lane == 0 && last < T) atomicMin(thr_key + qi, (unsigned long long)last);
     }
-    for (int j = i + lane; j < k; j += 64) {
-      const int64_t o = ((int64_t)qi * nr + r) * k + j;
-      cand_key[o] = kEmptyKey;
-      cand_row[o] = 0xffffffffu;
-    }
-    if (i == k && lane == 0 && last < T) atomicMin(tq, (unsigned long long)last);
     my_lo = nx_lo;
     my_hi = nx_hi;
     wave_lds_sync();  // LDS slice reused by the next range
   }
 }
 
-// Dense head-term tiles: tf[h][doc] (uint8, 255 = saturated) from the CSR.
+// Dense head-term tiles: tf[h][doc] (uint8; heads never have tf >= 255) from the CSR.
 __global__ void bm25_head_fill_kernel(const int32_t *__restrict__ head_terms, int nhead,
                                       const int64_t *__restrict__ term_off, const int32_t *__restrict__ post_doc,
                                       const uint16_t *__restrict__ post_tf, uint8_t *__restrict__ headtf,
@@ -503,7 +567,29 @@ __global__ void bm25_head_fill_kernel(const int32_t *__restrict__ head_terms, in
   const int64_t lo = term_off[t], hi = term_off[t + 1];
   uint8_t *row = headtf + (int64_t)h * npad;
   for (int64_t p = lo + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < hi; p += (int64_t)gridDim.x * blockDim.x)
-    row[post_doc[p]] = (uint8_t)min((int)post_tf[p], 255);
+    row[post_doc[p]] = (uint8_t)post_tf[p];  // < 255: saturating terms are never heads
+}
+
+// Histogram of live document lengths < 65536 (K2 ratio-table window choice).
+__global__ void bm25_dl_hist_kernel(const int32_t *__restrict__ dl, int64_t ndocs, uint32_t *__restrict__ hist) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < ndocs; i += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t d = dl[i];
+    if (d >= 0 && d < 65536) atomicAdd(hist + d, 1u);
+  }
+}
+
+// sat[c] != 0 iff candidate head term c has a posting with tf >= 255 (it then stays
+// on the postings path: head tiles hold exact tf bytes only).
+__global__ void bm25_head_sat_kernel(const int32_t *__restrict__ cand, int ncand, const int64_t *__restrict__ term_off,
+                                     const uint16_t *__restrict__ post_tf, int32_t *__restrict__ sat) {
+  const int c = blockIdx.y;
+  if (c >= ncand) return;
+  const int32_t t = cand[c];
+  const int64_t lo = term_off[t], hi = term_off[t + 1];
+  bool any = false;
+  for (int64_t p = lo + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < hi; p += (int64_t)gridDim.x * blockDim.x)
+    any |= post_tf[p] >= 255;
+  if (__any(any) && (threadIdx.x & 63) == 0) atomicOr(sat + c, 1);
 }
 
 // Tournament merge of nr sorted per-range lists per query.
@@ -712,6 +798,7 @@ struct cm_bm25 {
   DevBuf headtf, head_id;  // dense tf tiles for high-df terms (K2 fast path)
   int32_t nhead = 0;
   int64_t npad = 0;
+  int32_t lut_dmin = 0;                  // first doc length of K2's ratio table window
   double head_min_frac = 1.0 / 64.0;      // df > ndocs * frac qualifies
   int64_t head_max_bytes = 8ll << 30;    // tile memory budget
   std::vector<double> idf_host;
@@ -754,19 +841,64 @@ int compute_idf_table(cm_bm25 *h, const std::vector<int32_t> &df, const std::vec
 
 // Select head terms (df > ndocs * head_min_frac, highest df first, within the
 // byte budget) and build their dense uint8 tf tiles on the handle's stream.
+// K2 ratio-table window: the kLutW consecutive document lengths holding the most documents.
+int choose_lut_window(cm_bm25 *h) {
+  h->lut_dmin = 0;
+  if (h->ndocs == 0) return CM_OK;
+  int rc;
+  if ((rc = h->tmp.ensure(65536 * 4))) return rc;
+  CM_HIP(hipMemsetAsync(h->tmp.ptr, 0, 65536 * 4, h->stream));
+  hipLaunchKernelGGL(bm25_dl_hist_kernel, dim3(1024), dim3(256), 0, h->stream, h->dl.as<int32_t>(), h->ndocs,
+                     h->tmp.as<uint32_t>());
+  CM_HIP(hipGetLastError());
+  std::vector<uint32_t> hist(65536);
+  CM_HIP(hipMemcpyAsync(hist.data(), h->tmp.ptr, 65536 * 4, hipMemcpyDeviceToHost, h->stream));
+  CM_HIP(hipStreamSynchronize(h->stream));
+  uint64_t win = 0, best = 0;
+  for (int d = 0; d < kLutW; ++d) win += hist[d];
+  best = win;
+  for (int d0 = 1; d0 + kLutW <= 65536; ++d0) {
+    win += hist[d0 + kLutW - 1];
+    win -= hist[d0 - 1];
+    if (win > best) {
+      best = win;
+      h->lut_dmin = d0;
+    }
+  }
+  return CM_OK;
+}
+
 int build_head_tiles(cm_bm25 *h, const std::vector<int32_t> &df) {
   h->nhead = 0;
+  int rc0 = choose_lut_window(h);
+  if (rc0) return rc0;
   h->npad = round_up(std::max<int64_t>(h->ndocs, 1), kRange);
   const double thr = (double)h->ndocs * h->head_min_frac;
   std::vector<int32_t> cand;
   for (int32_t t = 0; t < h->vocab; ++t)
     if ((double)df[t] > thr && df[t] > 0) cand.push_back(t);
   std::sort(cand.begin(), cand.end(), [&](int32_t a, int32_t b) { return df[a] > df[b] || (df[a] == df[b] && a < b); });
+  int rc;
+  if (!cand.empty()) {  // drop terms whose tf does not fit a byte
+    if ((rc = h->tmp.ensure(cand.size() * 8))) return rc;
+    int32_t *dcand = h->tmp.as<int32_t>(), *dsat = dcand + cand.size();
+    CM_HIP(hipMemcpyAsync(dcand, cand.data(), cand.size() * 4, hipMemcpyHostToDevice, h->stream));
+    CM_HIP(hipMemsetAsync(dsat, 0, cand.size() * 4, h->stream));
+    hipLaunchKernelGGL(bm25_head_sat_kernel, dim3(16, (unsigned)cand.size()), dim3(256), 0, h->stream, dcand,
+                       (int)cand.size(), h->term_off.as<int64_t>(), h->post_tf.as<uint16_t>(), dsat);
+    CM_HIP(hipGetLastError());
+    std::vector<int32_t> sat(cand.size());
+    CM_HIP(hipMemcpyAsync(sat.data(), dsat, cand.size() * 4, hipMemcpyDeviceToHost, h->stream));
+    CM_HIP(hipStreamSynchronize(h->stream));
+    size_t o = 0;
+    for (size_t i = 0; i < cand.size(); ++i)
+      if (!sat[i]) cand[o++] = cand[i];
+    cand.resize(o);
+  }
   const int64_t max_h = h->head_max_bytes / h->npad;
   if ((int64_t)cand.size() > max_h) cand.resize((size_t)std::max<int64_t>(max_h, 0));
   std::vector<int32_t> hid((size_t)std::max(h->vocab, 1), -1);
   for (size_t i = 0; i < cand.size(); ++i) hid[cand[i]] = (int32_t)i;
-  int rc;
   if ((rc = h->head_id.ensure((size_t)std::max(h->vocab, 1) * 4))) return rc;
   CM_HIP(hipMemcpyAsync(h->head_id.ptr, hid.data(), (size_t)std::max(h->vocab, 1) * 4, hipMemcpyHostToDevice,
                         h->stream));
@@ -796,6 +928,7 @@ int bm25_debug_flags() {
 
 struct BmWs {
   unsigned long long *thr;
+  double *lut;
   double *q_idf;
   int64_t *bounds;
   uint64_t *cand_key;
@@ -810,6 +943,8 @@ BmWs bm_ws_layout(const cm_bm25 *h, int nq, int total_terms, int k, void *base) 
   size_t off = 0;
   w.thr = reinterpret_cast<unsigned long long *>(p + off);
   off += round_up((int64_t)std::max(nq, 1) * 8, 256);
+  w.lut = reinterpret_cast<double *>(p + off);
+  off += round_up((int64_t)kLutW * kLutTF * 8, 256);
   w.q_idf = reinterpret_cast<double *>(p + off);
   off += round_up((int64_t)std::max(total_terms, 1) * 8, 256);
   w.bounds = reinterpret_cast<int64_t *>(p + off);
@@ -837,16 +972,19 @@ int bm25_launch_core(cm_bm25 *h, const int32_t *q_terms_dev, const int32_t *q_of
     CM_HIP(hipGetLastError());
   }
   CM_HIP(hipMemsetAsync(w.thr, 0xff, (size_t)nq * 8, st));  // no threshold yet
-  // ranges per wave: enough waves to fill 256 CUs several times over, long runs otherwise
-  const int64_t work = (int64_t)nq * nr;
-  const int rpw = (int)std::min<int64_t>(kMaxRangesPerWave, std::max<int64_t>(1, work / (256 * 4 * 48)));
-  const int64_t nblk = (int64_t)ceil_div(nq, kQPerBlock) * ceil_div(nr, rpw);
+  hipLaunchKernelGGL(bm25_lut_kernel, dim3(kLutW * kLutTF / 256), dim3(256), 0, st, avgdl, h->lut_dmin, w.lut);
+  CM_HIP(hipGetLastError());
+  // ranges per wave: enough waves to fill 256 CUs many times over, long runs otherwise
+  const int64_t nqg = ceil_div(nq, kQPerWave);
+  const int rpw = (int)std::min<int64_t>(kMaxRangesPerWave, std::max<int64_t>(1, nqg * nr / (256 * 4 * 24)));
+  const int64_t nwaves = nqg * ceil_div(nr, rpw);
+  const int64_t nblk = ceil_div(nwaves, kBmThreads / 64);
   if (nblk > INT32_MAX) CM_FAIL(CM_EUNSUPPORTED, "BM25 batch too large");
   hipLaunchKernelGGL(bm25_range_kernel<uint16_t>, dim3((unsigned)nblk), dim3(kBmThreads), 0, st, q_terms_dev,
                      q_off_dev, nq, w.q_idf, w.bounds, nr, rpw, h->term_off.as<int64_t>(), h->post_doc.as<int32_t>(), h->post_tf.as<uint16_t>(),
                      h->nhead ? h->head_id.as<int32_t>() : (const int32_t *)nullptr, h->headtf.as<uint8_t>(),
-                     h->npad, h->dl.as<int32_t>(), h->live.as<uint32_t>(), allow_dev, h->ndocs, avgdl, k,
-                     w.cand_key, w.cand_row, w.thr, bm25_debug_flags());
+                     h->npad, h->dl.as<int32_t>(), h->live.as<uint32_t>(), allow_dev, h->ndocs, avgdl, w.lut,
+                     h->lut_dmin, k, w.cand_key, w.cand_row, w.thr, bm25_debug_flags());
   CM_HIP(hipGetLastError());
   hipLaunchKernelGGL(bm25_merge_kernel, dim3(nq), dim3(kMergeThreads), 0, st, w.cand_key, w.cand_row, nr, k,
                      score_dev, row_dev);

@@ -282,6 +282,304 @@ __global__ void __launch_bounds__(kThreads, 2)
   (void)qg;
 }
 
+// ---------------------------------------------------------------------------
+// K1b: batched cosine top-k on f16x3 split planes (batches of >= 64 queries,
+// k <= 32).  xn.qn = xh.qh + xh.ql + xl.qh (+ xl.ql, dropped: |err| <= 2^-22
+// relative per product, products exact in the f32 accumulator), so three
+// v_mfma_f32_16x16x32_f16 per 16x16x32 block give f32-grade distances at 16/3x
+// the f32-MFMA rate.
+//
+// One 512-thread workgroup per (corpus range, pass of 256 queries): the whole
+// query pass is resident (wave w owns queries 32w..32w+31, fragments streamed
+// from L2 one 32-deep k-chunk ahead), so every corpus byte is read from HBM
+// once per pass.  Corpus 128-row x 32-k chunks (both planes, 16 KiB) are staged
+// through double-buffered LDS (global->VGPR prefetch one chunk ahead).  After
+// each 128-row tile every wave filters its 32 x 128 distances against its
+// queries' running k-th keys and rank-merges survivors into per-query sorted
+// lists in LDS; the per-range lists go to dense_merge_kernel.
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+constexpr int kBRows = 128;                 // corpus rows per tile
+constexpr int kBPad = 40;                   // f16 per LDS row (32 + 8 pad: conflict-free b128 reads)
+constexpr int kBQPass = 256;                // queries per pass (8 waves x 32)
+constexpr int kBQWave = 32;
+constexpr int kBSlots = 48;                 // per query: sorted list (len <= k) then unmerged survivors
+constexpr int kBMaxK = 32;                  // k <= 32 leaves >= 16 buffer slots (one sub-tile's worst case)
+constexpr int kBXBuf = 2 * kBRows * kBPad;  // f16 per LDS stage buffer (2 planes)
+
+struct K1bLds {
+  int xs, thr, thrd, cnt, len, list, buf, total;
+};
+__host__ __device__ inline K1bLds k1b_lds_layout() {
+  K1bLds L;
+  int off = 0;
+  L.xs = off;
+  off += 2 * kBXBuf * 2;
+  L.thr = off;
+  off += kBQPass * 8;
+  L.list = off;
+  off += kBQPass * kBSlots * 8;
+  L.buf = off;
+  L.thrd = off;
+  off += kBQPass * 4;
+  L.cnt = off;
+  off += kBQPass * 4;
+  L.len = off;
+  off += kBQPass * 4;
+  L.total = off;
+  return L;
+}
+
+// Normalise + split queries into Qh/Ql [nq_pad][ld] (zero rows beyond nq).
+__global__ void __launch_bounds__(256) dense_prep_planes(const float *__restrict__ q, int nq, int dim, int ld,
+                                                         _Float16 *__restrict__ Qh, _Float16 *__restrict__ Ql) {
+  const int qi = blockIdx.x;
+  const float *src = q + (int64_t)qi * dim;
+  float s = 0.f;
+  for (int i = threadIdx.x; i < dim; i += 256) {
+    const float v = qi < nq ? src[i] : 0.f;
+    s += v * v;
+  }
+  __shared__ float red[4];
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  const float t = (red[0] + red[1]) + (red[2] + red[3]);
+  const float inv = 1.0f / (sqrtf(t) + 1e-30f);
+  for (int i = threadIdx.x; i < ld; i += 256) {
+    const float v = (qi < nq && i < dim) ? src[i] * inv : 0.f;
+    const _Float16 hi = (_Float16)v;
+    Qh[(int64_t)qi * ld + i] = hi;
+    Ql[(int64_t)qi * ld + i] = (_Float16)(v - (float)hi);
+  }
+}
+
+__global__ void __launch_bounds__(512, 1)
+    dense_f16x3_kernel(const _Float16 *__restrict__ Xh, const _Float16 *__restrict__ Xl, int ld,
+                       const uint32_t *__restrict__ live, const uint32_t *__restrict__ allow, int64_t n_words,
+                       const _Float16 *__restrict__ Qh, const _Float16 *__restrict__ Ql, int nq, int k,
+                       int64_t rows_per_wg, int64_t rows_end, int n_wg, uint64_t *__restrict__ cand, int dbg) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  const K1bLds L = k1b_lds_layout();
+  _Float16 *xs = reinterpret_cast<_Float16 *>(lds + L.xs);
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4;
+  const int j = lane & 15;
+  const int wg = blockIdx.x % n_wg;
+  const int qp = blockIdx.x / n_wg;
+  const int qw0 = wave * kBQWave;            // wave's first query within the pass
+  const int qg0 = qp * kBQPass + qw0;        // ... globally
+  uint64_t *thr = reinterpret_cast<uint64_t *>(lds + L.thr) + qw0;
+  float *thrd = reinterpret_cast<float *>(lds + L.thrd) + qw0;
+  uint32_t *cnt = reinterpret_cast<uint32_t *>(lds + L.cnt) + qw0;
+  uint32_t *len = reinterpret_cast<uint32_t *>(lds + L.len) + qw0;
+  uint64_t *list = reinterpret_cast<uint64_t *>(lds + L.list) + (int64_t)qw0 * kBSlots;
+  if (lane < kBQWave) {
+    const bool real = qg0 + lane < nq;
+    thr[lane] = real ? kEmptyKey : 0ull;  // padded queries accept nothing
+    thrd[lane] = real ? __builtin_inff() : -__builtin_inff();
+    cnt[lane] = 0;
+    len[lane] = 0;
+  }
+  const int64_t r_begin = (int64_t)wg * rows_per_wg;
+  const int64_t r_end = min(r_begin + rows_per_wg, rows_end);
+  const int ntiles = r_begin < r_end ? (int)((r_end - r_begin) / kBRows) : 0;
+  const int KC = ld / 32;
+  const int total = ntiles * KC;
+
+  // staging pieces of a chunk: 1024 x 16 B (plane, row, 8-f16 part); thread takes tid and tid + 512
+  auto xsrc = [&](int gc, int p) -> const f16x8 * {
+    const int t = gc / KC, c = gc - t * KC;
+    const int plane = p >> 9, row = (p & 511) >> 2, part = p & 3;
+    const _Float16 *X = plane ? Xl : Xh;
+    return reinterpret_cast<const f16x8 *>(X + (r_begin + (int64_t)t * kBRows + row) * ld + c * 32 + part * 8);
+  };
+  auto xdst = [&](int b, int p) -> f16x8 * {
+    const int plane = p >> 9, row = (p & 511) >> 2, part = p & 3;
+    return reinterpret_cast<f16x8 *>(xs + b * kBXBuf + plane * kBRows * kBPad + row * kBPad + part * 8);
+  };
+  // query fragments (B operand): lane (g, j) of q-tile qt holds q[qt*16 + j][32c + 8g .. +7]
+  auto qload = [&](f16x8 (&qh)[2], f16x8 (&ql)[2], int gc) {
+    const int c = gc % KC;
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) {
+      const int64_t o = (int64_t)(qg0 + qt * 16 + j) * ld + c * 32 + g * 8;
+      qh[qt] = *reinterpret_cast<const f16x8 *>(Qh + o);
+      ql[qt] = *reinterpret_cast<const f16x8 *>(Ql + o);
+    }
+  };
+  f32x4 acc[8][2];
+#pragma unroll
+  for (int rt = 0; rt < 8; ++rt) acc[rt][0] = acc[rt][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // rank-merge query q's slots [0, len + cnt) in place into its sorted list (<= k): one key per lane
+  auto merge = [&](int q) {
+    uint64_t *sl = list + q * kBSlots;
+    const uint32_t n = len[q] + cnt[q];
+    const uint64_t key = (uint32_t)lane < n ? sl[lane] : kEmptyKey;
+    uint32_t rank = 0;
+    for (uint32_t i = 0; i < n; ++i) rank += (sl[i] < key) ? 1u : 0u;
+    __builtin_amdgcn_wave_barrier();  // every lane has read the old slots
+    if ((uint32_t)lane < n && rank < (uint32_t)k) {
+      sl[rank] = key;
+      if (rank == (uint32_t)k - 1) {
+        thr[q] = key;
+        thrd[q] = f32_unorder((uint32_t)(key >> 32));
+      }
+    }
+    if (lane == 0) {
+      len[q] = min(n, (uint32_t)k);
+      cnt[q] = 0;
+    }
+  };
+  auto wave_lds_sync = [] {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  };
+  // merge every query of the wave whose free slots could not take another sub-tile (or all
+  // queries with anything buffered, at the end)
+  auto merge_pending = [&](bool all) {
+    wave_lds_sync();
+    bool need = false;
+    if (lane < kBQWave) {
+      const uint32_t c = cnt[lane];
+      need = all ? c > 0 : len[lane] + c + 16 > (uint32_t)kBSlots;
+    }
+    uint64_t m = __ballot(need);
+    while (m) {
+      const int q = __builtin_ctzll(m);
+      m &= m - 1;
+      merge(q);
+      wave_lds_sync();
+    }
+  };
+  // epilogue of tile t (wave-private queries, no block barrier): survivors of the running
+  // k-th key are appended to the query's free slots; a sub-tile adds <= 16 per query (4 lanes
+  // x 4 rows), and queries are merged only when fewer than 16 slots remain
+  auto epilogue = [&](int t) {
+    const int64_t row0 = r_begin + (int64_t)t * kBRows;
+    uint32_t bits[4];
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      const int64_t wi = (row0 >> 5) + w;
+      bits[w] = wi < n_words ? (live[wi] & (allow ? allow[wi] : 0xffffffffu)) : 0u;
+    }
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) {
+      const int ql_ = qt * 16 + j;
+#pragma unroll
+      for (int rt = 0; rt < 8; ++rt) {
+        const float td = thrd[ql_];
+        const uint64_t tk = thr[ql_];
+        bool added = false;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int rr = rt * 16 + 4 * g + r;  // row within the tile
+          const float dist = 1.0f - acc[rt][qt][r];
+          if (((bits[rr >> 5] >> (rr & 31)) & 1u) && dist <= td) {
+            const uint64_t key = ((uint64_t)f32_order(dist) << 32) | (uint64_t)(uint32_t)(row0 + rr);
+            if (key < tk) {
+              list[ql_ * kBSlots + len[ql_] + atomicAdd(&cnt[ql_], 1u)] = key;
+              added = true;
+            }
+          }
+        }
+        if (__ballot(added)) merge_pending(false);
+      }
+    }
+#pragma unroll
+    for (int rt = 0; rt < 8; ++rt) acc[rt][0] = acc[rt][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+  };
+
+  if (total > 0) {
+    // X chunks gc+1..gc+4 in flight in a 4-deep register ring (HBM latency ~ 3-4 chunks of
+    // MFMA work); query fragments one chunk ahead (L2).  KC is a multiple of 4 (ld % 128
+    // == 0), so a tile is a whole number of ring turns and the epilogue (no vector-memory
+    // loads) sits outside the unrolled bodies: every wait is a counted vmcnt, not a drain.
+    f16x8 qh[2], ql[2], nqh[2], nql[2];
+    f16x8 ra0, ra1, rb0, rb1, rc0, rc1, rd0, rd1;
+    auto xload = [&](f16x8 &x0, f16x8 &x1, int gc) {
+      const int gl = min(gc, total - 1);  // clamped: one control path
+      x0 = *xsrc(gl, tid);
+      x1 = *xsrc(gl, tid + 512);
+    };
+    xload(ra0, ra1, 0);
+    *xdst(0, tid) = ra0;
+    *xdst(0, tid + 512) = ra1;
+    qload(qh, ql, 0);
+    xload(ra0, ra1, 1);
+    xload(rb0, rb1, 2);
+    xload(rc0, rc1, 3);
+    xload(rd0, rd1, 4);
+    __syncthreads();
+    auto body = [&](int gc, f16x8 &x0, f16x8 &x1) {
+      qload(nqh, nql, min(gc + 1, total - 1));
+      const _Float16 *xb = xs + (gc & 1) * kBXBuf;
+      auto frag = [&](int rt, int plane) -> f16x8 {
+        return *reinterpret_cast<const f16x8 *>(xb + plane * kBRows * kBPad + (rt * 16 + j) * kBPad + g * 8);
+      };
+      // LDS fragments one 16-row sub-tile ahead of the MFMAs that use them
+      f16x8 xh = frag(0, 0), xl = frag(0, 1);
+#pragma unroll
+      for (int rt = 0; rt < 8; ++rt) {
+        f16x8 nh = xh, nl = xl;
+        if (rt < 7) {
+          nh = frag(rt + 1, 0);
+          nl = frag(rt + 1, 1);
+        }
+#pragma unroll
+        for (int qt = 0; qt < 2; ++qt) {
+          acc[rt][qt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xh, qh[qt], acc[rt][qt], 0, 0, 0);
+          acc[rt][qt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xh, ql[qt], acc[rt][qt], 0, 0, 0);
+          acc[rt][qt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xl, qh[qt], acc[rt][qt], 0, 0, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        xh = nh;
+        xl = nl;
+      }
+      *xdst((gc + 1) & 1, tid) = x0;  // chunk gc+1 (loaded four chunks ago)
+      *xdst((gc + 1) & 1, tid + 512) = x1;
+      xload(x0, x1, gc + 5);
+      __syncthreads();
+#pragma unroll
+      for (int qt = 0; qt < 2; ++qt) {
+        qh[qt] = nqh[qt];
+        ql[qt] = nql[qt];
+      }
+    };
+    for (int t = 0; t < ntiles; ++t) {
+      for (int c = 0; c < KC; c += 4) {
+        const int gc = t * KC + c;
+        body(gc, ra0, ra1);
+        body(gc + 1, rb0, rb1);
+        body(gc + 2, rc0, rc1);
+        body(gc + 3, rd0, rd1);
+      }
+      if (dbg & 1) {  // ablation: consume the accumulators without the top-k epilogue
+        float z = 0.f;
+#pragma unroll
+        for (int rt = 0; rt < 8; ++rt)
+#pragma unroll
+          for (int qt = 0; qt < 2; ++qt) z += acc[rt][qt][0] + acc[rt][qt][3];
+        if (z == 12345.f) thrd[lane & 31] = z;
+#pragma unroll
+        for (int rt = 0; rt < 8; ++rt) acc[rt][0] = acc[rt][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+      } else {
+        epilogue(t);
+      }
+    }
+  }
+  merge_pending(true);
+  // this range's sorted lists (layout of dense_merge_kernel with QB = kBQPass)
+  for (int idx = lane; idx < kBQWave * k; idx += 64) {
+    const int q = idx / k, i = idx - q * k;
+    const uint64_t v = (uint32_t)i < len[q] ? list[q * kBSlots + i] : kEmptyKey;
+    cand[(((int64_t)qp * n_wg + wg) * kBQPass + qw0 + q) * k + i] = v;
+  }
+}
+
 // Tournament merge of n_cblocks sorted lists per query -> final top-k.
 __global__ void __launch_bounds__(256) dense_merge_kernel(const uint64_t *__restrict__ cand, int n_cblocks, int QB,
                                                           int k, int nq, float *__restrict__ out_dist,
@@ -336,11 +634,14 @@ __global__ void __launch_bounds__(256) dense_merge_kernel(const uint64_t *__rest
   }
 }
 
-// Scatter n rows (staging n x dim) into C at rows[i] (or row0+i), set invc + live.
+// Scatter n rows (staging n x dim) into C at rows[i] (or row0+i), set invc + live,
+// and the row's normalised fp16 split planes (K1b): xn = x * invc (hnswlib
+// normalize_vector), Xh = f16(xn), Xl = f16(xn - Xh).
 __global__ void __launch_bounds__(256) dense_scatter_kernel(const float *__restrict__ src, const int64_t *__restrict__ rows,
                                                             int64_t row0, int64_t n, int dim, int ld,
                                                             float *__restrict__ C, float *__restrict__ invc,
-                                                            uint32_t *__restrict__ live) {
+                                                            uint32_t *__restrict__ live, _Float16 *__restrict__ Xh,
+                                                            _Float16 *__restrict__ Xl) {
   const int64_t i = blockIdx.x;
   if (i >= n) return;
   const int64_t r = rows ? rows[i] : row0 + i;
@@ -356,10 +657,17 @@ __global__ void __launch_bounds__(256) dense_scatter_kernel(const float *__restr
   for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
   __syncthreads();
+  const float t = (red[0] + red[1]) + (red[2] + red[3]);
+  const float inv = 1.0f / (sqrtf(t) + 1e-30f);
   if (threadIdx.x == 0) {
-    const float t = (red[0] + red[1]) + (red[2] + red[3]);
-    invc[r] = 1.0f / (sqrtf(t) + 1e-30f);
+    invc[r] = inv;
     atomicOr(&live[r >> 5], 1u << (r & 31));
+  }
+  for (int c = threadIdx.x; c < ld; c += 256) {
+    const float xn = (c < dim ? s[c] : 0.f) * inv;
+    const _Float16 hi = (_Float16)xn;
+    Xh[r * ld + c] = hi;
+    Xl[r * ld + c] = (_Float16)(xn - (float)hi);
   }
 }
 
@@ -401,6 +709,7 @@ struct cm_dense {
   int64_t size = 0;        // high-water row count
   float *C = nullptr;
   float *invc = nullptr;
+  _Float16 *Xh = nullptr, *Xl = nullptr;  // normalised f16 split planes (K1b)
   uint32_t *live = nullptr;
   hipStream_t stream = nullptr;
   DevBuf staging, rows_buf, allow_buf, ws, out_buf;
@@ -514,28 +823,119 @@ int dense_grow(cm_dense *h, int64_t need_rows) {
   cap = round_up(std::max<int64_t>(cap, kStepRows), kStepRows);
   float *C2 = nullptr, *ic2 = nullptr;
   uint32_t *lv2 = nullptr;
-  if (hipMalloc(&C2, (size_t)cap * h->ld * 4) != hipSuccess) CM_FAIL(CM_ENOMEM, "dense: out of device memory");
-  if (hipMalloc(&ic2, (size_t)cap * 4) != hipSuccess || hipMalloc(&lv2, (size_t)cap / 8) != hipSuccess) {
-    (void)hipFree(C2);
-    if (ic2) (void)hipFree(ic2);
+  _Float16 *xh2 = nullptr, *xl2 = nullptr;
+  const size_t nel = (size_t)cap * h->ld;
+  if (hipMalloc(&C2, nel * 4) != hipSuccess || hipMalloc(&ic2, (size_t)cap * 4) != hipSuccess ||
+      hipMalloc(&lv2, (size_t)cap / 8) != hipSuccess || hipMalloc(&xh2, nel * 2) != hipSuccess ||
+      hipMalloc(&xl2, nel * 2) != hipSuccess) {
+    for (void *p : {(void *)C2, (void *)ic2, (void *)lv2, (void *)xh2, (void *)xl2})
+      if (p) (void)hipFree(p);
     CM_FAIL(CM_ENOMEM, "dense: out of device memory");
   }
-  CM_HIP(hipMemsetAsync(C2, 0, (size_t)cap * h->ld * 4, h->stream));
+  CM_HIP(hipMemsetAsync(C2, 0, nel * 4, h->stream));
   CM_HIP(hipMemsetAsync(ic2, 0, (size_t)cap * 4, h->stream));
   CM_HIP(hipMemsetAsync(lv2, 0, (size_t)cap / 8, h->stream));
+  CM_HIP(hipMemsetAsync(xh2, 0, nel * 2, h->stream));
+  CM_HIP(hipMemsetAsync(xl2, 0, nel * 2, h->stream));
   if (h->rows_alloc) {
-    CM_HIP(hipMemcpyAsync(C2, h->C, (size_t)h->rows_alloc * h->ld * 4, hipMemcpyDeviceToDevice, h->stream));
+    const size_t old = (size_t)h->rows_alloc * h->ld;
+    CM_HIP(hipMemcpyAsync(C2, h->C, old * 4, hipMemcpyDeviceToDevice, h->stream));
     CM_HIP(hipMemcpyAsync(ic2, h->invc, (size_t)h->rows_alloc * 4, hipMemcpyDeviceToDevice, h->stream));
     CM_HIP(hipMemcpyAsync(lv2, h->live, (size_t)h->rows_alloc / 8, hipMemcpyDeviceToDevice, h->stream));
+    CM_HIP(hipMemcpyAsync(xh2, h->Xh, old * 2, hipMemcpyDeviceToDevice, h->stream));
+    CM_HIP(hipMemcpyAsync(xl2, h->Xl, old * 2, hipMemcpyDeviceToDevice, h->stream));
   }
   CM_HIP(hipStreamSynchronize(h->stream));
-  if (h->C) (void)hipFree(h->C);
-  if (h->invc) (void)hipFree(h->invc);
-  if (h->live) (void)hipFree(h->live);
+  for (void *p : {(void *)h->C, (void *)h->invc, (void *)h->live, (void *)h->Xh, (void *)h->Xl})
+    if (p) (void)hipFree(p);
   h->C = C2;
   h->invc = ic2;
   h->live = lv2;
+  h->Xh = xh2;
+  h->Xl = xl2;
   h->rows_alloc = cap;
+  return CM_OK;
+}
+
+// CM_DENSE_DEBUG (ablation only): bit0 skip K1b's top-k epilogue.
+int dense_debug_flags() {
+  static const int f = [] {
+    const char *e = getenv("CM_DENSE_DEBUG");
+    return e ? atoi(e) : 0;
+  }();
+  return f;
+}
+
+// K1b (f16x3 planes, all queries of a pass resident) for large batches.
+bool use_k1b(const cm_dense *h, int nq, int k) {
+  static const int force = [] {
+    const char *e = getenv("CM_DENSE_PATH");  // "f32" / "f16x3": force a path (A/B probes)
+    return e ? (e[0] == 'f' && e[1] == '3' ? 1 : (e[0] == 'f' && e[1] == '1' ? 2 : 0)) : 0;
+  }();
+  if (force == 1) return false;
+  if (k > kBMaxK || h->ld % 32) return false;
+  if (force == 2) return true;
+  return nq >= 64;
+}
+
+struct K1bCfg {
+  int n_wg, n_pass;
+  int64_t rows_per_wg, rows_end;
+};
+K1bCfg k1b_config(const cm_dense *h, int nq) {
+  K1bCfg c{};
+  c.n_pass = (int)ceil_div(nq, kBQPass);
+  c.rows_end = round_up(std::max<int64_t>(h->size, 1), kBRows);
+  const int64_t tiles = c.rows_end / kBRows;
+  const int64_t want = std::max(1, num_cus(h->dev) / c.n_pass);
+  const int64_t per = ceil_div(tiles, std::min<int64_t>(want, tiles));
+  c.rows_per_wg = per * kBRows;
+  c.n_wg = (int)ceil_div(tiles, per);
+  return c;
+}
+
+struct K1bWs {
+  _Float16 *qh, *ql;
+  uint64_t *cand;
+  size_t total;
+};
+K1bWs k1b_ws_layout(const cm_dense *h, const K1bCfg &c, int k, void *base) {
+  K1bWs w{};
+  char *p = reinterpret_cast<char *>(base);
+  size_t off = 0;
+  const int64_t nq_pad = (int64_t)c.n_pass * kBQPass;
+  w.qh = reinterpret_cast<_Float16 *>(p + off);
+  off += round_up(nq_pad * h->ld * 2, 256);
+  w.ql = reinterpret_cast<_Float16 *>(p + off);
+  off += round_up(nq_pad * h->ld * 2, 256);
+  w.cand = reinterpret_cast<uint64_t *>(p + off);
+  off += round_up((int64_t)c.n_pass * c.n_wg * kBQPass * k * 8, 256);
+  w.total = off;
+  return w;
+}
+
+int launch_k1b(cm_dense *h, const float *q_dev, int nq, int k, const uint32_t *allow, float *dist_dev,
+               int64_t *row_dev, void *ws, int64_t ws_bytes, hipStream_t st) {
+  static std::once_flag once;
+  static hipError_t attr_err = hipSuccess;
+  std::call_once(once, [] {
+    attr_err = hipFuncSetAttribute(reinterpret_cast<const void *>(&dense_f16x3_kernel),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, k1b_lds_layout().total);
+  });
+  CM_HIP(attr_err);
+  const K1bCfg c = k1b_config(h, nq);
+  const K1bWs w = k1b_ws_layout(h, c, k, ws);
+  if ((int64_t)w.total > ws_bytes || !ws) CM_FAIL(CM_EINVAL, "dense workspace too small");
+  hipLaunchKernelGGL(dense_prep_planes, dim3(c.n_pass * kBQPass), dim3(256), 0, st, q_dev, nq, h->dim, h->ld, w.qh,
+                     w.ql);
+  CM_HIP(hipGetLastError());
+  hipLaunchKernelGGL(dense_f16x3_kernel, dim3(c.n_wg * c.n_pass), dim3(512), k1b_lds_layout().total, st, h->Xh, h->Xl,
+                     h->ld, h->live, allow, ceil_div(h->size, 32), w.qh, w.ql, nq, k, c.rows_per_wg, c.rows_end,
+                     c.n_wg, w.cand, dense_debug_flags());
+  CM_HIP(hipGetLastError());
+  hipLaunchKernelGGL(dense_merge_kernel, dim3(nq), dim3(256), 0, st, w.cand, c.n_wg, kBQPass, k, nq, dist_dev,
+                     row_dev);
+  CM_HIP(hipGetLastError());
   return CM_OK;
 }
 
@@ -578,6 +978,8 @@ void cm_dense_destroy(cm_dense *h) {
   if (h->C) (void)hipFree(h->C);
   if (h->invc) (void)hipFree(h->invc);
   if (h->live) (void)hipFree(h->live);
+  if (h->Xh) (void)hipFree(h->Xh);
+  if (h->Xl) (void)hipFree(h->Xl);
   h->staging.release();
   h->rows_buf.release();
   h->allow_buf.release();
@@ -614,7 +1016,7 @@ int cm_dense_upsert(cm_dense *h, const float *vecs, const int64_t *rows, int64_t
     CM_HIP(hipMemcpyAsync(h->staging.ptr, vecs + s * h->dim, (size_t)m * h->dim * 4, hipMemcpyHostToDevice, h->stream));
     CM_HIP(hipMemcpyAsync(h->rows_buf.ptr, rows + s, (size_t)m * 8, hipMemcpyHostToDevice, h->stream));
     hipLaunchKernelGGL(dense_scatter_kernel, dim3((unsigned)m), dim3(256), 0, h->stream, h->staging.as<float>(),
-                       h->rows_buf.as<int64_t>(), (int64_t)0, m, h->dim, h->ld, h->C, h->invc, h->live);
+                       h->rows_buf.as<int64_t>(), (int64_t)0, m, h->dim, h->ld, h->C, h->invc, h->live, h->Xh, h->Xl);
     CM_HIP(hipGetLastError());
     CM_HIP(hipStreamSynchronize(h->stream));
   }
@@ -637,7 +1039,8 @@ int cm_dense_upsert_dev(cm_dense *h, const float *vecs_dev, int64_t row0, int64_
   for (int64_t s = 0; s < n; s += batch) {
     const int64_t m = std::min(batch, n - s);
     hipLaunchKernelGGL(dense_scatter_kernel, dim3((unsigned)m), dim3(256), 0, st, vecs_dev + s * h->dim,
-                       (const int64_t *)nullptr, row0 + s, m, h->dim, h->ld, h->C, h->invc, h->live);
+                       (const int64_t *)nullptr, row0 + s, m, h->dim, h->ld, h->C, h->invc, h->live, h->Xh,
+                       h->Xl);
     CM_HIP(hipGetLastError());
   }
   h->size = std::max(h->size, row0 + n);
@@ -665,6 +1068,8 @@ int cm_dense_reset(cm_dense *h) {
   CM_HIP(hipMemsetAsync(h->live, 0, (size_t)h->rows_alloc / 8, h->stream));
   CM_HIP(hipMemsetAsync(h->invc, 0, (size_t)h->rows_alloc * 4, h->stream));
   CM_HIP(hipMemsetAsync(h->C, 0, (size_t)h->rows_alloc * h->ld * 4, h->stream));
+  CM_HIP(hipMemsetAsync(h->Xh, 0, (size_t)h->rows_alloc * h->ld * 2, h->stream));
+  CM_HIP(hipMemsetAsync(h->Xl, 0, (size_t)h->rows_alloc * h->ld * 2, h->stream));
   CM_HIP(hipStreamSynchronize(h->stream));
   h->size = 0;
   return CM_OK;
@@ -691,6 +1096,7 @@ int64_t cm_dense_live_count(cm_dense *h) {
 
 int64_t cm_dense_search_workspace(cm_dense *h, int32_t nq, int32_t k) {
   if (!h || nq <= 0 || k <= 0 || k > kMaxTopK) return -1;
+  if (use_k1b(h, nq, k)) return (int64_t)k1b_ws_layout(h, k1b_config(h, nq), k, nullptr).total;
   DenseCfg c = dense_config(h, nq, k);
   return (int64_t)dense_ws_layout(h, c, nq, k, nullptr).total;
 }
@@ -703,6 +1109,7 @@ int cm_dense_search_dev(cm_dense *h, const float *q_dev, int32_t nq, int32_t k, 
   if (k <= 0 || k > kMaxTopK) CM_FAIL(CM_EINVAL, "k must be in [1, " + std::to_string(kMaxTopK) + "]");
   DeviceGuard dg(h->dev);
   hipStream_t st = (hipStream_t)stream;  // NULL = the null stream (torch default)
+  if (use_k1b(h, nq, k)) return launch_k1b(h, q_dev, nq, k, allow_dev, dist_dev, row_dev, workspace_dev, workspace_bytes, st);
   DenseCfg c = dense_config(h, nq, k);
   if (c.lds > 163840) CM_FAIL(CM_EUNSUPPORTED, "dim/k too large for the LDS-resident query tile");
   DenseWs w = dense_ws_layout(h, c, nq, k, workspace_dev);

@@ -101,6 +101,29 @@ def test_dense_shapes(eng, n, nq, k, dim):
     _check_dense(dist, rows, emb, q, k)
 
 
+@pytest.mark.parametrize("n,nq,k,dim", [(30000, 64, 24, 768), (12345, 100, 10, 384), (5000, 300, 32, 100),
+                                        (40000, 256, 1, 768), (257, 80, 32, 64)])
+def test_dense_batched_f16x3_path(eng, n, nq, k, dim):
+    """Batches of >= 64 queries with k <= 32 take K1b (f16x3 split planes, all
+    queries of a pass resident); distances within 1e-4, sets/order as the oracle,
+    deletes and filters honoured, multiple query passes (nq > 256)."""
+    rng = np.random.default_rng(n + nq + k)
+    emb = rng.standard_normal((n, dim)).astype(np.float32) * rng.uniform(0.1, 10, (n, 1)).astype(np.float32)
+    q = rng.standard_normal((nq, dim)).astype(np.float32)
+    q[: nq // 2] = emb[rng.integers(0, n, nq // 2)] + 0.05 * q[: nq // 2]
+    idx = eng.DenseIndex(dim)
+    idx.upsert(emb, np.arange(n))
+    dist, rows = idx.search(q, k)
+    _check_dense(dist, rows, emb, q, k)
+    allow = rng.random(n) < 0.3
+    dele = np.nonzero(rng.random(n) < 0.1)[0]
+    idx.delete(dele)
+    live = allow.copy()
+    live[dele] = False
+    dist, rows = idx.search(q, k, _bits(allow))
+    _check_dense(dist, rows, emb, q, k, live)
+
+
 def test_dense_device_path_and_gather(eng):
     import torch
     rng = np.random.default_rng(5)
