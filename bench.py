@@ -37,7 +37,10 @@ for _p in (str(REPO), str(REPO / "classmate-rag_amd")):
 
 METRIC = "hybrid queries/sec + recall@10 vs reference, 10M×768 chunks, 1/2/4/8 GPU"
 PEAK_F32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 matrix (dense)
+PEAK_F16_MFMA_TFLOPS = 2500.0  # MI355X_MICROARCH.md: BF16/F16 matrix, dense (no sparsity)
 PEAK_HBM_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E spec
+DENSE_KINDS = {1: "K1 fp32 MFMA (dense_topk_kernel)", 2: "K1b f16x3 split planes (dense_split_kernel<2>)",
+               3: "K1c coarse f16 scan (dense_split_kernel<1>) + certified fp64 re-rank"}
 
 
 def parse_args():
@@ -235,6 +238,9 @@ def main():
     for _ in range(args.warmup):
         res = step()
     torch.cuda.synchronize()
+    dense.timing(True)
+    if bm25 is not None:
+        bm25.timing(True)
     if ws > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
@@ -246,35 +252,36 @@ def main():
         torch.distributed.barrier()
     elapsed = time.perf_counter() - t0
     elapsed = parallel.max_over_ranks(elapsed, device=dev)
-    dense_ms = sum(e[0].elapsed_time(e[1]) for e in ev) / len(ev)
-    bm25_ms = sum(e[2].elapsed_time(e[3]) for e in ev) / len(ev) if args.mode == "hybrid" else None
+    search_ms = sum(e[0].elapsed_time(e[1]) for e in ev) / len(ev)
+    bsearch_ms = sum(e[2].elapsed_time(e[3]) for e in ev) / len(ev) if args.mode == "hybrid" else None
+    # scan-kernel launch times: HIP events the library records on the launch stream
+    kt = dense.timing_drain()
+    dense_ms = sum(kt) / len(kt)
+    bm25_ms = None
+    if bm25 is not None:
+        bt = bm25.timing_drain()
+        bm25_ms = sum(bt) / len(bt)
+    kind = dense.search_kind(B, P)
+    fallbacks = dense.workspace_fallbacks(B, P, dws)
     qps = B * args.steps / elapsed
-    log(f"{args.steps} steps in {elapsed:.3f}s -> {qps:.1f} q/s; dense kernel {dense_ms:.3f} ms/launch"
-        + (f", bm25 {bm25_ms:.3f} ms/launch" if bm25_ms is not None else ""))
+    log(f"{args.steps} steps in {elapsed:.3f}s -> {qps:.1f} q/s; dense search {search_ms:.3f} ms "
+        f"(scan kernel {dense_ms:.3f} ms, {DENSE_KINDS[kind]}, {fallbacks} exact re-runs)"
+        + (f", bm25 search {bsearch_ms:.3f} ms (K2 {bm25_ms:.3f} ms)" if bm25_ms is not None else ""))
 
-    # roofline of the dominant kernel: dense cosine top-k (K1)
-    flops = 2.0 * N * D * B
-    bytes_ = N * D * 4 + N * 4 + B * D * 4
-    mfma_bound = flops / (PEAK_F32_MFMA_TFLOPS * 1e12) >= bytes_ / (PEAK_HBM_GBS * 1e9)
-    traffic = _pmc_traffic(args)
-    if mfma_bound:
-        roof = dict(bound="mfma", achieved=flops / (dense_ms * 1e-3) / 1e12, peak=PEAK_F32_MFMA_TFLOPS,
-                    unit="TFLOP/s")
-    else:
-        roof = dict(bound="hbm", achieved=bytes_ / (dense_ms * 1e-3) / 1e9, peak=PEAK_HBM_GBS, unit="GB/s")
-    roof["frac"] = roof["achieved"] / roof["peak"]
-    roof["traffic"] = traffic
-    roof["kernel"] = "dense_topk_kernel (K1) via cm_dense_search_dev"
-    roof["algorithmic_per_launch"] = dict(flops=flops, bytes=bytes_, rows=N, queries=B, dim=D)
-    roof["avg_launch_ms"] = dense_ms
+    roofs = {"dense": _dense_roofline(kind, N, D, B, dense_ms, _pmc_traffic(args, "dense"))}
+    if bm25 is not None:
+        roofs["bm25"] = _bm25_roofline(bm25, q_terms, N, bm25_ms, _pmc_traffic(args, "bm25"))
+    dominant = max(roofs, key=lambda n: roofs[n]["avg_launch_ms"])
+    roof = roofs[dominant]
 
     out = {
         "metric": METRIC if args.mode == "hybrid" else f"dense cosine top-{P} queries/sec, {N}x{D} fp32",
         "value": qps, "unit": "queries/s", "n_gpus": ws, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
-        "vs_baseline": None, "dtype": "f32",
-        "dtypes": {"dense_knn": "f32 (MFMA)", "bm25": "f64", "e5_forward": "bf16" if use_e5 else None,
-                   "fusion": "f64"},
+        "vs_baseline": None, "dtype": "f16+f64",
+        "dtypes": {"dense_knn": {1: "f32 (MFMA)", 2: "f16x3 split (MFMA, f32-grade)",
+                                 3: "f16 coarse (MFMA) + fp64 exact re-rank of the certified band"}[kind],
+                   "bm25": "f64", "e5_forward": "bf16" if use_e5 else None, "fusion": "f64"},
         "data": "synthetic (seeded): unit-norm Gaussian chunk embeddings, Zipf BM25 postings, random-init "
                 "E5-base weights (no checkpoint offline)",
         "config": {"workload": ("hybrid retrieve: E5 query encode + cosine top-24 + MMR-10 + BM25 top-10 + RRF "
@@ -283,8 +290,11 @@ def main():
                    "bm25_vocab": args.vocab, "zipf_s": args.zipf, "chunk_len_mean": args.avg_len,
                    "query_terms": args.q_terms, "e5_query_tokens": args.q_tokens if use_e5 else None,
                    "parallelism": f"corpus-shard x{ws}"},
-        "breakdown_ms": {"dense_search": dense_ms, "bm25_search": bm25_ms},
+        "breakdown_ms": {"dense_search": search_ms, "dense_scan_kernel": dense_ms, "bm25_search": bsearch_ms,
+                         "bm25_k2_kernel": bm25_ms},
+        "dense_exact_reruns": fallbacks,
         "roofline": roof,
+        "rooflines": roofs,
     }
     if rank == 0 and ws == 1 and args.cpu_baseline and args.mode == "hybrid":
         cpu, recall = cpu_baseline_and_recall(args, dense, bm25, res, q_terms, emb, ids if use_e5 else None,
@@ -304,13 +314,54 @@ def main():
         torch.distributed.destroy_process_group()
 
 
-def _pmc_traffic(args):
-    """HBM bytes per K1 launch from a committed rocprofv3 --pmc summary of this config (or None)."""
-    p = REPO / "profiles" / "pmc_dense_traffic.json"
+def _roof(bytes_, flops, peak_tflops, ms):
+    """Bound = the larger of the HBM and MFMA floors; achieved in that unit."""
+    if flops / (peak_tflops * 1e12) >= bytes_ / (PEAK_HBM_GBS * 1e9):
+        r = dict(bound="mfma", achieved=flops / (ms * 1e-3) / 1e12, peak=peak_tflops, unit="TFLOP/s")
+    else:
+        r = dict(bound="hbm", achieved=bytes_ / (ms * 1e-3) / 1e9, peak=PEAK_HBM_GBS, unit="GB/s")
+    r["frac"] = r["achieved"] / r["peak"]
+    return r
+
+
+def _dense_roofline(kind, N, D, B, ms, traffic):
+    """Algorithmic work of one scan launch: corpus bytes in the kernel's own
+    storage format + live bitmap + query planes; flops as executed on the MFMA units."""
+    if kind == 1:      # fp32 rows + invc
+        bytes_, flops, peak = N * D * 4 + N * 4 + N / 8 + B * D * 4, 2.0 * N * D * B, PEAK_F32_MFMA_TFLOPS
+    elif kind == 2:    # hi + lo f16 planes, 3 products per block
+        bytes_, flops, peak = N * D * 4 + N / 8 + B * D * 4, 3 * 2.0 * N * D * B, PEAK_F16_MFMA_TFLOPS
+    else:              # hi plane only, 1 product per block
+        bytes_, flops, peak = N * D * 2 + N / 8 + B * D * 2, 2.0 * N * D * B, PEAK_F16_MFMA_TFLOPS
+    r = _roof(bytes_, flops, peak, ms)
+    r.update(traffic=traffic, kernel=DENSE_KINDS[kind], avg_launch_ms=ms,
+             algorithmic_per_launch=dict(bytes=bytes_, flops=flops, rows=N, queries=B, dim=D),
+             fp32_equivalent_GBps=N * D * 4 / (ms * 1e-3) / 1e9)
+    return r
+
+
+def _bm25_roofline(bm25, q_terms, N, ms, traffic):
+    """K2's compulsory bytes for the batch: every distinct query term's postings read once in
+    the cheaper of its two encodings (CSR: 4 B doc + 2 B tf per posting; head tile: 1 B per
+    doc) plus the doc lengths.  K2 is latency/VALU-bound, so this fraction is low by nature."""
+    import numpy as np
+    df, _ = bm25.term_stats()
+    t = np.unique(q_terms.cpu().numpy())
+    t = t[(t >= 0) & (t < df.shape[0])]
+    bytes_ = float(np.minimum(6.0 * df[t].astype(np.float64), float(N)).sum()) + 4.0 * N
+    r = _roof(bytes_, 0.0, 1.0, ms)
+    r.update(traffic=traffic, kernel="K2 bm25_range_kernel", avg_launch_ms=ms,
+             algorithmic_per_launch=dict(bytes=bytes_, distinct_terms=int(t.shape[0]), docs=N))
+    return r
+
+
+def _pmc_traffic(args, which):
+    """HBM bytes per launch (FETCH_SIZE x 2, the gfx950 correction) from a committed rocprofv3
+    --pmc summary of this config (profiles/pmc_traffic.json), or None."""
+    p = REPO / "profiles" / "pmc_traffic.json"
     try:
         d = json.loads(p.read_text())
-        key = f"{args.docs_per_gpu}x{args.dim}_B{args.batch}"
-        return d.get(key)
+        return d.get(f"{which}_{args.docs_per_gpu}x{args.dim}_B{args.batch}")
     except Exception:
         return None
 

@@ -62,6 +62,14 @@ SIGNATURES = {
     "cm_dense_dim": (c_i32, c_vp),
     "cm_dense_search": (c_int, c_vp, c_vp, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp),
     "cm_dense_search_workspace": (c_i64, c_vp, c_i32, c_i32),
+    "cm_dense_search_kind": (c_i32, c_vp, c_i32, c_i32),
+    "cm_dense_set_path": (c_int, c_vp, c_i32),
+    "cm_dense_workspace_fallbacks": (c_i32, c_vp, c_i32, c_i32, c_vp),
+    "cm_dense_last_fallbacks": (c_i32, c_vp),
+    "cm_dense_timing": (c_int, c_vp, c_i32),
+    "cm_dense_timing_drain": (c_i32, c_vp, c_vp, c_i32),
+    "cm_bm25_timing": (c_int, c_vp, c_i32),
+    "cm_bm25_timing_drain": (c_i32, c_vp, c_vp, c_i32),
     "cm_dense_search_dev": (c_int, c_vp, c_vp, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp),
     "cm_dense_export": (c_int, c_vp, c_i64, c_i64, c_vp, c_vp),
     "cm_dense_gather_dev": (c_int, c_vp, c_vp, c_i64, c_vp, c_vp),

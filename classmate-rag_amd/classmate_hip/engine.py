@@ -133,6 +133,36 @@ class DenseIndex:
         mask = np.unpackbits(live.view(np.uint8), bitorder="little")[:n].astype(bool)
         return out, mask
 
+    # scan kernels (cm_dense_search_kind / cm_dense_set_path)
+    PATH_AUTO, PATH_F32, PATH_F16X3, PATH_COARSE = 0, 1, 2, 3
+
+    def set_path(self, kind: int):
+        """Force the scan kernel (0 auto, 1 fp32 K1, 2 f16x3 K1b, 3 coarse+re-rank K1c)."""
+        L.check(L.fn["cm_dense_set_path"](self._h, int(kind)), "cm_dense_set_path")
+
+    def search_kind(self, nq: int, k: int) -> int:
+        return int(L.fn["cm_dense_search_kind"](self._h, int(nq), int(k)))
+
+    def last_fallbacks(self) -> int:
+        """K1c queries re-run by the exact pass in the last host search()."""
+        return int(L.fn["cm_dense_last_fallbacks"](self._h))
+
+    def timing(self, enable: bool = True):
+        """Record HIP events around every search's scan kernel (see timing_drain)."""
+        L.check(L.fn["cm_dense_timing"](self._h, int(bool(enable))), "cm_dense_timing")
+
+    def timing_drain(self, cap: int = 4096) -> list:
+        """Synchronise on the recorded events -> per-launch scan-kernel times (ms)."""
+        buf = np.zeros(cap, np.float32)
+        n = int(L.fn["cm_dense_timing_drain"](self._h, L.ptr(buf), int(cap)))
+        if n < 0:
+            raise RuntimeError(L.last_error())
+        return buf[:min(n, cap)].tolist()
+
+    def workspace_fallbacks(self, nq: int, k: int, workspace) -> int:
+        """K1c queries re-run by the exact pass in the last search_dev() that used `workspace`."""
+        return int(L.fn["cm_dense_workspace_fallbacks"](self._h, int(nq), int(k), L.ptr(workspace)))
+
     def workspace_bytes(self, nq: int, k: int) -> int:
         n = int(L.fn["cm_dense_search_workspace"](self._h, int(nq), int(k)))
         if n < 0:
@@ -232,6 +262,17 @@ class BM25Index:
     def set_head_policy(self, min_df_frac: float = 1.0 / 64, max_bytes: int = 8 << 30):
         """Dense tf tiles for high-df terms (same results; max_bytes=0 disables)."""
         L.check(L.fn["cm_bm25_set_head_policy"](self._h, float(min_df_frac), int(max_bytes)), "cm_bm25_set_head_policy")
+
+    def timing(self, enable: bool = True):
+        """Record HIP events around every search's K2 launch (see timing_drain)."""
+        L.check(L.fn["cm_bm25_timing"](self._h, int(bool(enable))), "cm_bm25_timing")
+
+    def timing_drain(self, cap: int = 4096) -> list:
+        buf = np.zeros(cap, np.float32)
+        n = int(L.fn["cm_bm25_timing_drain"](self._h, L.ptr(buf), int(cap)))
+        if n < 0:
+            raise RuntimeError(L.last_error())
+        return buf[:min(n, cap)].tolist()
 
     @property
     def num_head_terms(self) -> int:

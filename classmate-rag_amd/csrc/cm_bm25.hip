@@ -803,6 +803,7 @@ struct cm_bm25 {
   int64_t head_max_bytes = 8ll << 30;    // tile memory budget
   std::vector<double> idf_host;
   DevBuf ws, qbuf, obuf, allow_buf, tmp;
+  KernelTimer timer;  // K2 events (cm_bm25_timing)
 };
 
 namespace {
@@ -980,11 +981,13 @@ int bm25_launch_core(cm_bm25 *h, const int32_t *q_terms_dev, const int32_t *q_of
   const int64_t nwaves = nqg * ceil_div(nr, rpw);
   const int64_t nblk = ceil_div(nwaves, kBmThreads / 64);
   if (nblk > INT32_MAX) CM_FAIL(CM_EUNSUPPORTED, "BM25 batch too large");
+  h->timer.begin(st);
   hipLaunchKernelGGL(bm25_range_kernel<uint16_t>, dim3((unsigned)nblk), dim3(kBmThreads), 0, st, q_terms_dev,
                      q_off_dev, nq, w.q_idf, w.bounds, nr, rpw, h->term_off.as<int64_t>(), h->post_doc.as<int32_t>(), h->post_tf.as<uint16_t>(),
                      h->nhead ? h->head_id.as<int32_t>() : (const int32_t *)nullptr, h->headtf.as<uint8_t>(),
                      h->npad, h->dl.as<int32_t>(), h->live.as<uint32_t>(), allow_dev, h->ndocs, avgdl, w.lut,
                      h->lut_dmin, k, w.cand_key, w.cand_row, w.thr, bm25_debug_flags());
+  h->timer.end(st);
   CM_HIP(hipGetLastError());
   hipLaunchKernelGGL(bm25_merge_kernel, dim3(nq), dim3(kMergeThreads), 0, st, w.cand_key, w.cand_row, nr, k,
                      score_dev, row_dev);
@@ -1022,6 +1025,7 @@ void cm_bm25_destroy(cm_bm25 *h) {
   DeviceGuard dg(h->dev);
   if (h->stream) (void)hipStreamSynchronize(h->stream);
   bm25_free(h);
+  h->timer.release();
   if (h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
 }
@@ -1318,6 +1322,21 @@ int cm_bm25_set_head_policy(cm_bm25 *h, double min_df_frac, int64_t max_bytes) {
 }
 
 int32_t cm_bm25_num_head_terms(cm_bm25 *h) { return h ? h->nhead : -1; }
+
+int cm_bm25_timing(cm_bm25 *h, int32_t enable) {
+  if (!h) CM_FAIL(CM_EINVAL, "null handle");
+  h->timer.on = enable != 0;
+  h->timer.used = 0;
+  return CM_OK;
+}
+
+int32_t cm_bm25_timing_drain(cm_bm25 *h, float *ms_out, int32_t cap) {
+  if (!h) CM_FAIL(CM_EINVAL, "null handle");
+  DeviceGuard dg(h->dev);
+  const int n = h->timer.drain(ms_out, cap);
+  if (n < 0) CM_FAIL(CM_EDEVICE, "event query failed");
+  return n;
+}
 
 int cm_bm25_set_stats(cm_bm25 *h, const double *idf, int32_t vocab, int64_t n_live, int64_t sum_len, double eps) {
   if (!h || !idf) CM_FAIL(CM_EINVAL, "NULL argument");

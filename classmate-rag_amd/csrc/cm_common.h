@@ -6,6 +6,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <string>
+#include <vector>
 
 #include "classmate_hip.h"
 
@@ -91,6 +92,50 @@ __host__ __device__ inline double f64_unorder(uint64_t u) {
   u = (u & 0x8000000000000000ull) ? (u & 0x7fffffffffffffffull) : ~u;
   return __builtin_bit_cast(double, u);
 }
+
+// Optional per-handle kernel timer: HIP events recorded on the launch stream
+// around the dominant kernel of each search (bench roofline); drained after a sync.
+struct KernelTimer {
+  bool on = false, armed = false;
+  std::vector<hipEvent_t> ev;  // begin/end pairs
+  size_t used = 0;
+  void begin(hipStream_t st) {
+    armed = false;
+    if (!on) return;
+    grow();
+    armed = ev.size() >= used + 2 && hipEventRecord(ev[used], st) == hipSuccess;
+  }
+  void end(hipStream_t st) {
+    if (!armed) return;
+    armed = false;
+    if (hipEventRecord(ev[used + 1], st) == hipSuccess) used += 2;
+  }
+  void grow() {
+    while (ev.size() < used + 2) {
+      hipEvent_t e;
+      if (hipEventCreate(&e) != hipSuccess) return;
+      ev.push_back(e);
+    }
+  }
+  // elapsed ms of the recorded pairs (up to cap) -> out; returns the pair count or < 0
+  int drain(float *out, int cap) {
+    int n = 0;
+    for (size_t i = 0; i + 1 < used; i += 2) {
+      if (hipEventSynchronize(ev[i + 1]) != hipSuccess) return CM_EDEVICE;
+      float ms = 0.f;
+      if (hipEventElapsedTime(&ms, ev[i], ev[i + 1]) != hipSuccess) return CM_EDEVICE;
+      if (n < cap && out) out[n] = ms;
+      ++n;
+    }
+    used = 0;
+    return n;
+  }
+  void release() {
+    for (hipEvent_t e : ev) (void)hipEventDestroy(e);
+    ev.clear();
+    used = 0;
+  }
+};
 
 constexpr uint64_t kEmptyKey = ~0ull;
 constexpr int kMaxTopK = 256;

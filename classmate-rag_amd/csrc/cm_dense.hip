@@ -283,31 +283,50 @@ __global__ void __launch_bounds__(kThreads, 2)
 }
 
 // ---------------------------------------------------------------------------
-// K1b: batched cosine top-k on f16x3 split planes (batches of >= 64 queries,
-// k <= 32).  xn.qn = xh.qh + xh.ql + xl.qh (+ xl.ql, dropped: |err| <= 2^-22
-// relative per product, products exact in the f32 accumulator), so three
-// v_mfma_f32_16x16x32_f16 per 16x16x32 block give f32-grade distances at 16/3x
-// the f32-MFMA rate.
+// K1b / K1c: batched cosine top-k on normalised fp16 planes, one template.
+//   xn = c * invc (hnswlib normalize_vector), Xh = f16(xn), Xl = f16(xn - Xh).
+//   NPL = 2 (K1b, "f16x3"): reads both planes; xn.qn = xh.qh + xh.ql + xl.qh
+//       (+ xl.ql dropped, <= 2^-22 relative) -> f32-grade distances.
+//   NPL = 1 (K1c, "coarse"): reads only Xh (2 B per element, half of K1/K1b's
+//       HBM bytes) and one product xh.qh per block; the lists hold k' = k + 4
+//       coarse keys per range and dense_rerank_kernel certifies them with a
+//       rigorous error bound before re-ranking the band exactly.
+// A chunk is always 1024 x 16 B = 128 rows x 2 sub-blocks x 32 f16 staged
+// through double-buffered LDS: for NPL = 2 the sub-blocks are the two planes of
+// one 32-deep k slice, for NPL = 1 the two halves of one 64-deep k slice of Xh,
+// so both variants share the LDS image, the load pattern and the fragment reads.
 //
 // One 512-thread workgroup per (corpus range, pass of 256 queries): the whole
 // query pass is resident (wave w owns queries 32w..32w+31, fragments streamed
-// from L2 one 32-deep k-chunk ahead), so every corpus byte is read from HBM
-// once per pass.  Corpus 128-row x 32-k chunks (both planes, 16 KiB) are staged
-// through double-buffered LDS (global->VGPR prefetch one chunk ahead).  After
-// each 128-row tile every wave filters its 32 x 128 distances against its
-// queries' running k-th keys and rank-merges survivors into per-query sorted
-// lists in LDS; the per-range lists go to dense_merge_kernel.
+// from L2 one chunk ahead), so every corpus byte is read from HBM once per pass.
+// After each 128-row tile every wave filters its 32 x 128 distances against its
+// queries' running k-th keys (a per-query max over the lane's 32 values first, so
+// tiles without a survivor cost one compare per query) and rank-merges survivors
+// into per-query sorted lists in LDS.
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+// Plane layout (Xh, Xl): tile-major, so every 128-row x 64-f16 chunk the scans stream is one
+// contiguous 16 KB block (row-major planes made each chunk 128 row segments 1.5 KB apart and
+// reopened every DRAM page once per chunk):  element (row, k) of a plane with row pitch ld lives
+// at ((row / 128) * (ld / 64) + k / 64) * 8192 + (row % 128) * 64 + k % 64.
+__host__ __device__ inline int64_t plane_off(int64_t row, int k, int ld) {
+  return (((row >> 7) * (ld >> 6) + (k >> 6)) << 13) + ((row & 127) << 6) + (k & 63);
+}
 constexpr int kBRows = 128;                 // corpus rows per tile
-constexpr int kBPad = 40;                   // f16 per LDS row (32 + 8 pad: conflict-free b128 reads)
+constexpr int kBPad = 32;                   // f16 per LDS row (unpadded; 16-B chunks XOR-swizzled, see lds_swz)
 constexpr int kBQPass = 256;                // queries per pass (8 waves x 32)
 constexpr int kBQWave = 32;
-constexpr int kBSlots = 48;                 // per query: sorted list (len <= k) then unmerged survivors
-constexpr int kBMaxK = 32;                  // k <= 32 leaves >= 16 buffer slots (one sub-tile's worst case)
-constexpr int kBXBuf = 2 * kBRows * kBPad;  // f16 per LDS stage buffer (2 planes)
+constexpr int kBSlots = 60;                 // per query: sorted list (len <= k) then unmerged survivors
+constexpr int kBMaxK = 32;                  // k <= 32 leaves >= 28 buffer slots (one sub-tile adds <= 16)
+constexpr int kBXBuf = 2 * kBRows * kBPad;  // f16 per LDS stage buffer (2 sub-blocks)
+// 16-B chunk swizzle of an LDS row: chunk c of row r lives at c ^ lds_swz(r).  Conflict-free for
+// both the MFMA fragment reads (ds_read_b128: lanes (g, j) read chunk g of row j; gfx950 serves
+// lane groups {0-3,12-15,20-27}, ... in one cycle each) and the staging writes (ds_write_b128,
+// 8 contiguous lanes = two rows x four chunks), checked exhaustively on the host.
+__host__ __device__ inline int lds_swz(int row) { return ((row >> 3) & 1) << 1; }
+constexpr int kRerankCap = 1024;            // certified band size per query handled by the re-rank kernel
 
 struct K1bLds {
-  int xs, thr, thrd, cnt, len, list, buf, total;
+  int xs, thr, thrd, cnt, len, list, buf, act, total;
 };
 __host__ __device__ inline K1bLds k1b_lds_layout() {
   K1bLds L;
@@ -325,13 +344,17 @@ __host__ __device__ inline K1bLds k1b_lds_layout() {
   off += kBQPass * 4;
   L.len = off;
   off += kBQPass * 4;
+  L.act = off;
+  off += 16;
   L.total = off;
   return L;
 }
 
-// Normalise + split queries into Qh/Ql [nq_pad][ld] (zero rows beyond nq).
+// Normalise + split queries into Qh/Ql [nq_pad][ld] (zero rows beyond nq) and
+// record per query {||q||, ||qh||, ||ql||} (fp32, for K1c's error bound).
 __global__ void __launch_bounds__(256) dense_prep_planes(const float *__restrict__ q, int nq, int dim, int ld,
-                                                         _Float16 *__restrict__ Qh, _Float16 *__restrict__ Ql) {
+                                                         _Float16 *__restrict__ Qh, _Float16 *__restrict__ Ql,
+                                                         float *__restrict__ qnorm) {
   const int qi = blockIdx.x;
   const float *src = q + (int64_t)qi * dim;
   float s = 0.f;
@@ -339,25 +362,48 @@ __global__ void __launch_bounds__(256) dense_prep_planes(const float *__restrict
     const float v = qi < nq ? src[i] : 0.f;
     s += v * v;
   }
-  __shared__ float red[4];
+  __shared__ float red[3][4];
   for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  if ((threadIdx.x & 63) == 0) red[0][threadIdx.x >> 6] = s;
   __syncthreads();
-  const float t = (red[0] + red[1]) + (red[2] + red[3]);
+  const float t = (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]);
   const float inv = 1.0f / (sqrtf(t) + 1e-30f);
+  float sh = 0.f, sl = 0.f;
   for (int i = threadIdx.x; i < ld; i += 256) {
     const float v = (qi < nq && i < dim) ? src[i] * inv : 0.f;
     const _Float16 hi = (_Float16)v;
+    const _Float16 lo = (_Float16)(v - (float)hi);
     Qh[(int64_t)qi * ld + i] = hi;
-    Ql[(int64_t)qi * ld + i] = (_Float16)(v - (float)hi);
+    Ql[(int64_t)qi * ld + i] = lo;
+    sh += (float)hi * (float)hi;
+    sl += (float)lo * (float)lo;
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    sh += __shfl_xor(sh, o);
+    sl += __shfl_xor(sl, o);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    red[1][threadIdx.x >> 6] = sh;
+    red[2][threadIdx.x >> 6] = sl;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0 && qnorm) {
+    qnorm[4 * qi + 0] = sqrtf(t);
+    qnorm[4 * qi + 1] = sqrtf((red[1][0] + red[1][1]) + (red[1][2] + red[1][3]));
+    qnorm[4 * qi + 2] = sqrtf((red[2][0] + red[2][1]) + (red[2][2] + red[2][3]));
+    qnorm[4 * qi + 3] = 0.f;
   }
 }
 
+// qmask (nullable): only queries with qmask[q] != 0 are searched (K1c's fallback
+// pass); a workgroup whose pass has none exits before touching the corpus.
+template <int NPL>
 __global__ void __launch_bounds__(512, 1)
-    dense_f16x3_kernel(const _Float16 *__restrict__ Xh, const _Float16 *__restrict__ Xl, int ld,
+    dense_split_kernel(const _Float16 *__restrict__ Xh, const _Float16 *__restrict__ Xl, int ld,
                        const uint32_t *__restrict__ live, const uint32_t *__restrict__ allow, int64_t n_words,
-                       const _Float16 *__restrict__ Qh, const _Float16 *__restrict__ Ql, int nq, int k,
-                       int64_t rows_per_wg, int64_t rows_end, int n_wg, uint64_t *__restrict__ cand, int dbg) {
+                       const _Float16 *__restrict__ Qh, const _Float16 *__restrict__ Ql, int nq,
+                       const int32_t *__restrict__ qmask, int k, int64_t rows_per_wg, int64_t rows_end, int n_wg,
+                       uint64_t *__restrict__ cand, int dbg) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   const K1bLds L = k1b_lds_layout();
   _Float16 *xs = reinterpret_cast<_Float16 *>(lds + L.xs);
@@ -375,9 +421,19 @@ __global__ void __launch_bounds__(512, 1)
   uint32_t *cnt = reinterpret_cast<uint32_t *>(lds + L.cnt) + qw0;
   uint32_t *len = reinterpret_cast<uint32_t *>(lds + L.len) + qw0;
   uint64_t *list = reinterpret_cast<uint64_t *>(lds + L.list) + (int64_t)qw0 * kBSlots;
+  int32_t *act = reinterpret_cast<int32_t *>(lds + L.act);
+  if (qmask) {
+    if (tid == 0) act[0] = 0;
+    __syncthreads();
+    const int qq = qp * kBQPass + tid;
+    if (tid < kBQPass && qq < nq && qmask[qq]) act[0] = 1;
+    __syncthreads();
+    if (act[0] == 0) return;  // whole workgroup: no query of this pass is active
+  }
   if (lane < kBQWave) {
-    const bool real = qg0 + lane < nq;
-    thr[lane] = real ? kEmptyKey : 0ull;  // padded queries accept nothing
+    const int qq = qg0 + lane;
+    const bool real = qq < nq && (!qmask || qmask[qq]);
+    thr[lane] = real ? kEmptyKey : 0ull;  // padded / inactive queries accept nothing
     thrd[lane] = real ? __builtin_inff() : -__builtin_inff();
     cnt[lane] = 0;
     len[lane] = 0;
@@ -385,28 +441,35 @@ __global__ void __launch_bounds__(512, 1)
   const int64_t r_begin = (int64_t)wg * rows_per_wg;
   const int64_t r_end = min(r_begin + rows_per_wg, rows_end);
   const int ntiles = r_begin < r_end ? (int)((r_end - r_begin) / kBRows) : 0;
-  const int KC = ld / 32;
+  const int KC = ld / (32 * (3 - NPL));  // chunks per tile: 32-deep (NPL 2) or 64-deep (NPL 1)
   const int total = ntiles * KC;
 
-  // staging pieces of a chunk: 1024 x 16 B (plane, row, 8-f16 part); thread takes tid and tid + 512
+  // staging pieces of a chunk: 1024 x 16 B (sub-block, row, 8-f16 part); thread takes tid and tid + 512
   auto xsrc = [&](int gc, int p) -> const f16x8 * {
     const int t = gc / KC, c = gc - t * KC;
-    const int plane = p >> 9, row = (p & 511) >> 2, part = p & 3;
-    const _Float16 *X = plane ? Xl : Xh;
-    return reinterpret_cast<const f16x8 *>(X + (r_begin + (int64_t)t * kBRows + row) * ld + c * 32 + part * 8);
+    const int sb = p >> 9, row = (p & 511) >> 2, part = p & 3;
+    const int64_t rg = r_begin + (int64_t)t * kBRows + row;
+    if (NPL == 2) return reinterpret_cast<const f16x8 *>((sb ? Xl : Xh) + plane_off(rg, c * 32 + part * 8, ld));
+    return reinterpret_cast<const f16x8 *>(Xh + plane_off(rg, c * 64 + sb * 32 + part * 8, ld));
   };
   auto xdst = [&](int b, int p) -> f16x8 * {
-    const int plane = p >> 9, row = (p & 511) >> 2, part = p & 3;
-    return reinterpret_cast<f16x8 *>(xs + b * kBXBuf + plane * kBRows * kBPad + row * kBPad + part * 8);
+    const int sb = p >> 9, row = (p & 511) >> 2, part = p & 3;
+    return reinterpret_cast<f16x8 *>(xs + b * kBXBuf + sb * kBRows * kBPad + row * kBPad + (part ^ lds_swz(row)) * 8);
   };
-  // query fragments (B operand): lane (g, j) of q-tile qt holds q[qt*16 + j][32c + 8g .. +7]
-  auto qload = [&](f16x8 (&qh)[2], f16x8 (&ql)[2], int gc) {
+  // query fragments (B operand): lane (g, j) of q-tile qt holds q[qt*16 + j][.. + 8g .. +7] of
+  // sub-block 0 (qa) and 1 (qb): NPL 2 -> (Qh, Ql) of the 32-deep slice, NPL 1 -> Qh halves
+  auto qload = [&](f16x8 (&qa)[2], f16x8 (&qb)[2], int gc) {
     const int c = gc % KC;
 #pragma unroll
     for (int qt = 0; qt < 2; ++qt) {
-      const int64_t o = (int64_t)(qg0 + qt * 16 + j) * ld + c * 32 + g * 8;
-      qh[qt] = *reinterpret_cast<const f16x8 *>(Qh + o);
-      ql[qt] = *reinterpret_cast<const f16x8 *>(Ql + o);
+      const int64_t rb = (int64_t)(qg0 + qt * 16 + j) * ld;
+      if (NPL == 2) {
+        qa[qt] = *reinterpret_cast<const f16x8 *>(Qh + rb + c * 32 + g * 8);
+        qb[qt] = *reinterpret_cast<const f16x8 *>(Ql + rb + c * 32 + g * 8);
+      } else {
+        qa[qt] = *reinterpret_cast<const f16x8 *>(Qh + rb + c * 64 + g * 8);
+        qb[qt] = *reinterpret_cast<const f16x8 *>(Qh + rb + c * 64 + 32 + g * 8);
+      }
     }
   };
   f32x4 acc[8][2];
@@ -469,6 +532,13 @@ __global__ void __launch_bounds__(512, 1)
 #pragma unroll
     for (int qt = 0; qt < 2; ++qt) {
       const int ql_ = qt * 16 + j;
+      // quick reject: the lane's best of its 32 rows for this query against the running k-th
+      float mx = acc[0][qt][0];
+#pragma unroll
+      for (int rt = 0; rt < 8; ++rt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) mx = fmaxf(mx, acc[rt][qt][r]);
+      if (__ballot(1.0f - mx <= thrd[ql_]) == 0) continue;
 #pragma unroll
       for (int rt = 0; rt < 8; ++rt) {
         const float td = thrd[ql_];
@@ -480,7 +550,7 @@ __global__ void __launch_bounds__(512, 1)
           const float dist = 1.0f - acc[rt][qt][r];
           if (((bits[rr >> 5] >> (rr & 31)) & 1u) && dist <= td) {
             const uint64_t key = ((uint64_t)f32_order(dist) << 32) | (uint64_t)(uint32_t)(row0 + rr);
-            if (key < tk) {
+            if (key < tk && !(dbg & 16)) {
               list[ql_ * kBSlots + len[ql_] + atomicAdd(&cnt[ql_], 1u)] = key;
               added = true;
             }
@@ -495,10 +565,10 @@ __global__ void __launch_bounds__(512, 1)
 
   if (total > 0) {
     // X chunks gc+1..gc+4 in flight in a 4-deep register ring (HBM latency ~ 3-4 chunks of
-    // MFMA work); query fragments one chunk ahead (L2).  KC is a multiple of 4 (ld % 128
-    // == 0), so a tile is a whole number of ring turns and the epilogue (no vector-memory
+    // MFMA work); query fragments one chunk ahead (L2).  KC is a multiple of 4 (checked on
+    // the host), so a tile is a whole number of ring turns and the epilogue (no vector-memory
     // loads) sits outside the unrolled bodies: every wait is a counted vmcnt, not a drain.
-    f16x8 qh[2], ql[2], nqh[2], nql[2];
+    f16x8 qa[2], qb[2], nqa[2], nqb[2];
     f16x8 ra0, ra1, rb0, rb1, rc0, rc1, rd0, rd1;
     auto xload = [&](f16x8 &x0, f16x8 &x1, int gc) {
       const int gl = min(gc, total - 1);  // clamped: one control path
@@ -508,36 +578,42 @@ __global__ void __launch_bounds__(512, 1)
     xload(ra0, ra1, 0);
     *xdst(0, tid) = ra0;
     *xdst(0, tid + 512) = ra1;
-    qload(qh, ql, 0);
+    qload(qa, qb, 0);
     xload(ra0, ra1, 1);
     xload(rb0, rb1, 2);
     xload(rc0, rc1, 3);
     xload(rd0, rd1, 4);
     __syncthreads();
     auto body = [&](int gc, f16x8 &x0, f16x8 &x1) {
-      qload(nqh, nql, min(gc + 1, total - 1));
+      qload(nqa, nqb, min(gc + 1, total - 1));
       const _Float16 *xb = xs + (gc & 1) * kBXBuf;
-      auto frag = [&](int rt, int plane) -> f16x8 {
-        return *reinterpret_cast<const f16x8 *>(xb + plane * kBRows * kBPad + (rt * 16 + j) * kBPad + g * 8);
+      auto frag = [&](int rt, int sb) -> f16x8 {
+        return *reinterpret_cast<const f16x8 *>(xb + sb * kBRows * kBPad + (rt * 16 + j) * kBPad +
+                                                (g ^ lds_swz(j)) * 8);
       };
       // LDS fragments one 16-row sub-tile ahead of the MFMAs that use them
-      f16x8 xh = frag(0, 0), xl = frag(0, 1);
+      f16x8 xa = frag(0, 0), xb1 = frag(0, 1);
 #pragma unroll
       for (int rt = 0; rt < 8; ++rt) {
-        f16x8 nh = xh, nl = xl;
+        f16x8 na = xa, nb = xb1;
         if (rt < 7) {
-          nh = frag(rt + 1, 0);
-          nl = frag(rt + 1, 1);
+          na = frag(rt + 1, 0);
+          nb = frag(rt + 1, 1);
         }
 #pragma unroll
         for (int qt = 0; qt < 2; ++qt) {
-          acc[rt][qt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xh, qh[qt], acc[rt][qt], 0, 0, 0);
-          acc[rt][qt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xh, ql[qt], acc[rt][qt], 0, 0, 0);
-          acc[rt][qt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xl, qh[qt], acc[rt][qt], 0, 0, 0);
+          if (NPL == 2) {
+            acc[rt][qt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xa, qa[qt], acc[rt][qt], 0, 0, 0);
+            acc[rt][qt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xa, qb[qt], acc[rt][qt], 0, 0, 0);
+            acc[rt][qt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xb1, qa[qt], acc[rt][qt], 0, 0, 0);
+          } else {
+            acc[rt][qt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xa, qa[qt], acc[rt][qt], 0, 0, 0);
+            acc[rt][qt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xb1, qb[qt], acc[rt][qt], 0, 0, 0);
+          }
         }
         __builtin_amdgcn_sched_barrier(0);
-        xh = nh;
-        xl = nl;
+        xa = na;
+        xb1 = nb;
       }
       *xdst((gc + 1) & 1, tid) = x0;  // chunk gc+1 (loaded four chunks ago)
       *xdst((gc + 1) & 1, tid + 512) = x1;
@@ -545,8 +621,8 @@ __global__ void __launch_bounds__(512, 1)
       __syncthreads();
 #pragma unroll
       for (int qt = 0; qt < 2; ++qt) {
-        qh[qt] = nqh[qt];
-        ql[qt] = nql[qt];
+        qa[qt] = nqa[qt];
+        qb[qt] = nqb[qt];
       }
     };
     for (int t = 0; t < ntiles; ++t) {
@@ -580,12 +656,442 @@ __global__ void __launch_bounds__(512, 1)
   }
 }
 
+constexpr int kCQWave = 64;  // queries per wave in the resident-query scan
+
+// K1c's per-query error bound E (see dense_rerank_kernel).
+__device__ inline float coarse_err(const float *qnorm, int qi, const float *row_norms, int dim) {
+  const float qh = qnorm[4 * qi + 1], qlo = qnorm[4 * qi + 2];
+  const float mxh = row_norms[0], mxl = row_norms[1];
+  return (qlo * mxh + mxl * qh + mxl * qlo + (float)dim * 5.9604645e-8f * mxh * qh + 2e-6f) * 1.001f;
+}
+
+// ---------------------------------------------------------------------------
+// K1c scan (coarse f16, Xh plane only), resident-query form for ld = 64 KC.
+// 256 threads, one wave per SIMD; wave w owns queries 64w..64w+63 of the 256-query pass and
+// keeps their Qh fragments resident -- chunks 0..KC-NQL-1 in registers (32 VGPRs each), the last
+// NQL chunks in LDS -- so the corpus is the only memory stream: 64-row x 64-f16 chunks (8 KB; one
+// glds wave-instruction = 8 rows x 128 B, full lines) LDS-DMA'd into a kRRing-slot ring, retired
+// by a counted vmcnt and published by a raw s_barrier: no vmcnt(0) and no query reloads in the
+// loop.  The ring image is 128-B rows with 16-B chunks XOR-swizzled by (row >> 1) & 7 on the glds
+// SOURCE address (the DMA writes lane-linearly) and on the ds_read address: conflict-free
+// fragment reads (checked exhaustively on the host).  Compute tiles are 64 rows.
+//   MINONLY (sample pre-pass): per query, the minimum coarse distance over the workgroup's
+//     live+allowed rows -> out_min[pass][wg][q].
+//   main pass: every live+allowed row with coarse distance <= seed[q] is appended to the
+//     (range, query) candidate buffer out_keys[pass][wg][q][kCBufCap] (LDS slot counter);
+//     out_cnt[pass][wg][q] = appended count (> kCBufCap: the buffer overflowed).
+#ifndef K1C_RING
+#define K1C_RING 12
+#endif
+constexpr int kRRing = K1C_RING;  // LDS ring slots (8 KB each): kRRing - 1 chunks in flight per CU
+constexpr int kRRows = 64;      // rows per compute tile / chunk
+constexpr int kCBufCap = 64;    // candidate slots per (range, query)
+
+template <int NQL>
+struct K1rLds {
+  static constexpr int ring = 0;
+  static constexpr int qf = ring + kRRing * 8192;          // [NQL][4 waves][8 frags][64 lanes] x 16 B
+  static constexpr int total = qf + NQL * 4 * 8 * 1024;
+};
+__device__ inline int ring_swz(int row) { return (row >> 1) & 7; }
+
+template <int KC, int NQL, bool MINONLY>
+__global__ void __launch_bounds__(256, 1)
+    dense_coarse_scan_kernel(const _Float16 *__restrict__ Xh, const uint32_t *__restrict__ live,
+                             const uint32_t *__restrict__ allow, int64_t n_words, const _Float16 *__restrict__ Qh,
+                             int nq, const float *__restrict__ seed, int64_t rows_per_wg, int64_t rows_end, int n_wg,
+                             uint64_t *__restrict__ out_keys, uint32_t *__restrict__ out_cnt,
+                             float *__restrict__ out_min) {
+  constexpr int ld = 64 * KC;
+  constexpr int KR = KC - NQL;  // register-resident query chunks
+  using LL = K1rLds<NQL>;
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4;
+  const int j = lane & 15;
+  const int wg = blockIdx.x % n_wg;
+  const int qp = blockIdx.x / n_wg;
+  const int64_t r_begin = (int64_t)wg * rows_per_wg;
+  const int64_t r_end = min(r_begin + rows_per_wg, rows_end);
+  const int ntiles = r_begin < r_end ? (int)((r_end - r_begin) / kRRows) : 0;
+  const int total = ntiles * KC;
+  const int qc0 = wave * kCQWave;
+  const int qg0 = qp * kBQPass + qc0;
+
+  // resident query fragments (B operand): lane (g, j) of q-tile qt, chunk c, half sb holds
+  // q[qt*16 + j][64c + 32sb + 8g .. +7]
+  f16x8 qres[KR][4][2];
+  auto qsrc = [&](int c, int qt, int sb) -> const f16x8 * {
+    return reinterpret_cast<const f16x8 *>(Qh + (int64_t)(qg0 + qt * 16 + j) * ld + c * 64 + sb * 32 + g * 8);
+  };
+#pragma unroll
+  for (int c = 0; c < KR; ++c)
+#pragma unroll
+    for (int qt = 0; qt < 4; ++qt)
+#pragma unroll
+      for (int sb = 0; sb < 2; ++sb) qres[c][qt][sb] = *qsrc(c, qt, sb);
+#pragma unroll
+  for (int c = 0; c < NQL; ++c)
+#pragma unroll
+    for (int f = 0; f < 8; ++f)
+      *reinterpret_cast<f16x8 *>(lds + LL::qf + ((c * 4 + wave) * 8 + f) * 1024 + lane * 16) =
+          *qsrc(KR + c, f >> 1, f & 1);
+  // per-lane seeds of the lane's 4 queries (qt*16 + j)
+  float sd[4];
+#pragma unroll
+  for (int qt = 0; qt < 4; ++qt) {
+    const int qq = qg0 + qt * 16 + j;
+    sd[qt] = MINONLY ? 0.f : (qq < nq ? seed[qq] : -__builtin_inff());  // padded queries accept nothing
+  }
+  float best[4] = {__builtin_inff(), __builtin_inff(), __builtin_inff(), __builtin_inff()};
+  uint32_t qcnt[4] = {0u, 0u, 0u, 0u};  // lanes g == 0: candidates appended for query qt*16 + j
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();  // LDS query fragments ready; no DMA in flight yet
+
+  // glds source of wave-instruction i (0, 1) of chunk gc: ring cell o16 = 256 i + tid holds the
+  // 16-B piece (row o16 >> 3, logical chunk (o16 & 7) ^ ring_swz(row)) of the tile-major plane
+  auto issue = [&](int gc) __attribute__((always_inline)) {
+    const int gl = min(gc, total - 1);  // clamped: one control path past the end
+    const int t = gl / KC, c = gl - t * KC;
+    const int64_t R0 = r_begin + (int64_t)t * kRRows;
+    unsigned char *slot = lds + LL::ring + (gc % kRRing) * 8192;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int o16 = 256 * i + tid;
+      const int row = o16 >> 3, lg = (o16 & 7) ^ ring_swz(row);
+      const _Float16 *src = Xh + ((((R0 >> 7) * KC + c) << 13) + (((R0 & 127) + row) << 6) + lg * 8);
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)src,
+                                       (__attribute__((address_space(3))) void *)(slot + i * 4096 + wave * 1024), 16,
+                                       0, 0);
+    }
+  };
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int rt = 0; rt < 4; ++rt)
+#pragma unroll
+    for (int qt = 0; qt < 4; ++qt) acc[rt][qt] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto epilogue = [&](int t) __attribute__((always_inline)) {
+    const int64_t row0 = r_begin + (int64_t)t * kRRows;
+    const int64_t w0 = row0 >> 5;  // wave-uniform: scalar loads, outside the DMA's vmcnt queue
+    const uint32_t b0 = w0 < n_words ? (live[w0] & (allow ? allow[w0] : 0xffffffffu)) : 0u;
+    const uint32_t b1 = w0 + 1 < n_words ? (live[w0 + 1] & (allow ? allow[w0 + 1] : 0xffffffffu)) : 0u;
+    // lane (g, j) holds rows rt*16 + 4g + r: bit (16 rt + 4 g + r) of the 64-bit tile mask
+    const uint64_t tmask = ((uint64_t)b1 << 32) | b0;
+#pragma unroll
+    for (int qt = 0; qt < 4; ++qt) {
+      if (MINONLY) {
+        float m = __builtin_inff();
+#pragma unroll
+        for (int rt = 0; rt < 4; ++rt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if ((tmask >> (rt * 16 + 4 * g + r)) & 1u) m = fminf(m, 1.0f - acc[rt][qt][r]);
+        best[qt] = fminf(best[qt], m);
+      } else {
+        float mx = -__builtin_inff();
+#pragma unroll
+        for (int rt = 0; rt < 4; ++rt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) mx = fmaxf(mx, acc[rt][qt][r]);
+        if (__ballot(1.0f - mx <= sd[qt]) == 0) continue;  // no row of the tile under any seed
+        // slots by ballot + popcount among the 4 lanes (g = 0..3) sharing query j; the count
+        // lives in lane j's register (no LDS atomics: those would wait for the ring's DMAs)
+        const int q = qc0 + qt * 16 + j;
+        const uint64_t samej = 0x0001000100010001ull << j;
+        uint64_t *dst = out_keys + (((int64_t)qp * n_wg + wg) * kBQPass + q) * kCBufCap;
+#pragma unroll
+        for (int rt = 0; rt < 4; ++rt) {
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int rr = rt * 16 + 4 * g + r;
+            const float dist = 1.0f - acc[rt][qt][r];
+            const bool pred = ((tmask >> rr) & 1u) && dist <= sd[qt];
+            const uint64_t m = __ballot(pred);
+            if (m == 0) continue;
+            const uint32_t base = __shfl(qcnt[qt], j);
+            const uint32_t slot = base + (uint32_t)__popcll(m & samej & ((1ull << lane) - 1ull));
+            if (pred && slot < (uint32_t)kCBufCap)
+              dst[slot] = ((uint64_t)f32_order(dist) << 32) | (uint64_t)(uint32_t)(row0 + rr);
+            if (g == 0) qcnt[qt] += (uint32_t)__popcll(m & samej);
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int rt = 0; rt < 4; ++rt)
+#pragma unroll
+      for (int qt = 0; qt < 4; ++qt) acc[rt][qt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  };
+
+  if (total > 0) {
+#pragma unroll
+    for (int p = 0; p < kRRing - 1; ++p) issue(p);
+    for (int t = 0; t < ntiles; ++t) {
+#pragma unroll
+      for (int c = 0; c < KC; ++c) {
+        const int gc = t * KC + c;
+        // chunk gc landed (this wave's part; the 2 (kRRing - 2) younger DMAs may stay in flight),
+        // then the barrier publishes every wave's part and retires all reads of slot (gc-1) % kRRing
+        // vmcnt count = 2 DMAs x (ring - 2) chunks
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * (kRRing - 2)) : "memory");
+        __builtin_amdgcn_s_barrier();
+        issue(gc + kRRing - 1);
+        const unsigned char *slot = lds + LL::ring + (gc % kRRing) * 8192;
+        auto frag = [&](int rt, int sb) -> f16x8 {
+          const int row = rt * 16 + j;
+          return *reinterpret_cast<const f16x8 *>(slot + row * 128 + (((sb * 4 + g) ^ ring_swz(row)) << 4));
+        };
+        f16x8 qv[4][2];
+#pragma unroll
+        for (int qt = 0; qt < 4; ++qt)
+#pragma unroll
+          for (int sb = 0; sb < 2; ++sb)
+            qv[qt][sb] = c < KR ? qres[c < KR ? c : 0][qt][sb]
+                                : *reinterpret_cast<const f16x8 *>(
+                                      lds + LL::qf + (((c - KR) * 4 + wave) * 8 + qt * 2 + sb) * 1024 + lane * 16);
+        f16x8 xa = frag(0, 0), xb = frag(0, 1);
+#pragma unroll
+        for (int rt = 0; rt < 4; ++rt) {
+          f16x8 na = xa, nb = xb;
+          if (rt < 3) {
+            na = frag(rt + 1, 0);
+            nb = frag(rt + 1, 1);
+          }
+#pragma unroll
+          for (int qt = 0; qt < 4; ++qt)
+            acc[rt][qt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xa, qv[qt][0], acc[rt][qt], 0, 0, 0);
+#pragma unroll
+          for (int qt = 0; qt < 4; ++qt)
+            acc[rt][qt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xb, qv[qt][1], acc[rt][qt], 0, 0, 0);
+          xa = na;
+          xb = nb;
+        }
+      }
+      epilogue(t);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // clamped tail DMAs land before the LDS is released
+  }
+  if (MINONLY) {
+#pragma unroll
+    for (int qt = 0; qt < 4; ++qt) {
+      float m = best[qt];
+      m = fminf(m, __shfl_xor(m, 16));
+      m = fminf(m, __shfl_xor(m, 32));
+      if (g == 0) out_min[((int64_t)qp * n_wg + wg) * kBQPass + qc0 + qt * 16 + j] = m;
+    }
+  } else if (g == 0) {
+#pragma unroll
+    for (int qt = 0; qt < 4; ++qt) out_cnt[((int64_t)qp * n_wg + wg) * kBQPass + qc0 + qt * 16 + j] = qcnt[qt];
+  }
+}
+
+// K1c seed from the sample pre-pass: the k-th smallest of the n_wg per-workgroup minima bounds the
+// k-th smallest coarse distance of the whole corpus (k distinct rows lie at or under it); + 2E.
+// +inf when fewer than k groups hold an allowed row.
+__global__ void __launch_bounds__(256) dense_seed_kernel(const float *__restrict__ mins, int n_wg, int k, int nq,
+                                                         const float *__restrict__ qnorm,
+                                                         const float *__restrict__ row_norms, int dim,
+                                                         float *__restrict__ seed) {
+  const int qi = blockIdx.x;
+  if (qi >= nq) return;
+  const int qp = qi / kBQPass, ql = qi - qp * kBQPass;
+  __shared__ float v[2048];
+  const int n = min(n_wg, 2048);
+  for (int i = threadIdx.x; i < n; i += 256) v[i] = mins[((int64_t)qp * n_wg + i) * kBQPass + ql];
+  __syncthreads();
+  // the k-th smallest by rank counting (n <= 2048, ties broken by index)
+  __shared__ float kth;
+  if (threadIdx.x == 0) kth = __builtin_inff();
+  __syncthreads();
+  for (int i = threadIdx.x; i < n; i += 256) {
+    const float x = v[i];
+    if (!(x < __builtin_inff())) continue;
+    int rank = 0;
+    for (int m = 0; m < n; ++m) rank += (v[m] < x || (v[m] == x && m < i)) ? 1 : 0;
+    if (rank == k - 1) kth = x;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) seed[qi] = kth < __builtin_inff() ? kth + 2.0f * coarse_err(qnorm, qi, row_norms, dim)
+                                                           : __builtin_inff();
+}
+
+// Block-wide radix select: the k-th smallest (0-based kk) of n u32 values in LDS (4 x 8-bit digits).
+__device__ inline uint32_t block_select_u32(const uint32_t *vals, int n, int kk, uint32_t *hist /*[256]*/) {
+  __shared__ uint32_t s_prefix, s_rem;
+  if (threadIdx.x == 0) {
+    s_prefix = 0;
+    s_rem = (uint32_t)kk;
+  }
+  for (int shift = 24; shift >= 0; shift -= 8) {
+    for (int b = threadIdx.x; b < 256; b += blockDim.x) hist[b] = 0;
+    __syncthreads();
+    const uint32_t prefix = s_prefix;
+    const uint32_t hmask = shift == 24 ? 0u : (0xffffffffu << (shift + 8));
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+      const uint32_t x = vals[i];
+      if ((x & hmask) == (prefix & hmask)) atomicAdd(&hist[(x >> shift) & 255u], 1u);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      uint32_t rem = s_rem, b = 0;
+      while (hist[b] <= rem) rem -= hist[b++];
+      s_prefix = prefix | (b << shift);
+      s_rem = rem;
+    }
+    __syncthreads();
+  }
+  return s_prefix;
+}
+
+// K1c certification + exact re-rank, one 256-thread workgroup per query.
+//   For every row |c - d| <= E with
+//     E = ||ql|| max||xh|| + max||xl|| ||qh|| + max||xl|| ||ql|| + dim 2^-24 max||xh|| ||qh|| + 2e-6
+//   (xn.qn = xh.qh + xh.ql + xl.qh + xl.ql, products exact in f32, accumulation error bounded by
+//   the recursive-summation bound, 2e-6 for the normalisations).  With c_k the k-th smallest
+//   coarse distance, every row of the exact top-k has c <= T = c_k + 2E <= seed, so it sits in
+//   one of the n_wg candidate buffers unless that buffer overflowed (or the band exceeds
+//   kRerankCap): then the query is flagged for the exact K1b pass.  Otherwise the band's rows are
+//   re-ranked with fp64 dot products of the stored fp32 rows,
+//   d = 1 - (c.q) / ((||c|| + 1e-30)(||q|| + 1e-30)), ties -> lower row.
+constexpr int kGatherCap = 8192;  // candidates gathered per query
+__global__ void __launch_bounds__(256) dense_rerank_kernel(
+    const uint64_t *__restrict__ keys, const uint32_t *__restrict__ cnts, int n_wg, int k, int nq,
+    const float *__restrict__ C, int ld, int dim, const float *__restrict__ q, const float *__restrict__ qnorm,
+    const float *__restrict__ row_norms, float *__restrict__ out_dist, int64_t *__restrict__ out_row,
+    int32_t *__restrict__ fb_mask, int32_t *__restrict__ fb_count) {
+  const int qi = blockIdx.x;
+  if (qi >= nq) return;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int qp = qi / kBQPass, ql = qi - qp * kBQPass;
+  extern __shared__ __attribute__((aligned(16))) unsigned char dyn[];
+  uint64_t *s_keys = reinterpret_cast<uint64_t *>(dyn);                        // [kGatherCap]
+  uint32_t *s_dist = reinterpret_cast<uint32_t *>(dyn + kGatherCap * 8);      // [kGatherCap]
+  __shared__ uint32_t s_off[2049];
+  __shared__ uint32_t hist[256];
+  __shared__ float s_q[2048];
+  __shared__ int s_flag, s_total, s_band;
+  __shared__ uint32_t s_rows[kRerankCap];
+  __shared__ uint64_t s_ex[kRerankCap];
+  if (tid == 0) {
+    s_flag = 0;
+    s_band = 0;
+  }
+  // 1. buffer sizes -> offsets (serial scan by one wave: n_wg <= 2048)
+  __syncthreads();
+  if (wave == 0) {
+    uint32_t run = 0;
+    for (int b0 = 0; b0 < n_wg; b0 += 64) {
+      const int b = b0 + lane;
+      uint32_t c = b < n_wg ? cnts[((int64_t)qp * n_wg + b) * kBQPass + ql] : 0u;
+      if (c > (uint32_t)kCBufCap) {
+        s_flag = 1;
+        c = kCBufCap;
+      }
+      uint32_t incl = c;
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t v = __shfl_up(incl, o);
+        if (lane >= o) incl += v;
+      }
+      if (b < n_wg) s_off[b] = run + incl - c;
+      run += __shfl(incl, 63);
+    }
+    if (lane == 0) {
+      s_off[n_wg] = run;
+      s_total = (int)run;
+    }
+  }
+  __syncthreads();
+  const int total = s_total;
+  if (s_flag || total > kGatherCap) {
+    if (tid == 0) {
+      fb_mask[qi] = 1;
+      atomicAdd(fb_count, 1);
+    }
+    return;  // the K1b pass writes this query's results
+  }
+  // 2. gather the candidates
+  for (int b = wave; b < n_wg; b += 4) {
+    const uint32_t o = s_off[b], c = s_off[b + 1] - o;
+    const uint64_t *src = keys + (((int64_t)qp * n_wg + b) * kBQPass + ql) * kCBufCap;
+    for (uint32_t i = lane; i < c; i += 64) {
+      const uint64_t key = src[i];
+      s_keys[o + i] = key;
+      s_dist[o + i] = (uint32_t)(key >> 32);
+    }
+  }
+  for (int i = tid; i < dim; i += 256) s_q[i] = q[(int64_t)qi * dim + i];
+  __syncthreads();
+  // 3. band threshold from the k-th smallest coarse distance
+  uint32_t tkey = 0xffffffffu;  // fewer than k candidates: all of them
+  if (total >= k) {
+    const uint32_t ck = block_select_u32(s_dist, total, k - 1, hist);
+    tkey = f32_order(f32_unorder(ck) + 2.0f * coarse_err(qnorm, qi, row_norms, dim));
+  }
+  for (int i = tid; i < total; i += 256) {
+    if (s_dist[i] <= tkey) {
+      const int p = atomicAdd(&s_band, 1);
+      if (p < kRerankCap) s_rows[p] = (uint32_t)s_keys[i];
+    }
+  }
+  __syncthreads();
+  const int band = s_band;
+  if (band > kRerankCap) {
+    if (tid == 0) {
+      fb_mask[qi] = 1;
+      atomicAdd(fb_count, 1);
+    }
+    return;
+  }
+  if (tid == 0) fb_mask[qi] = 0;
+  // 4. exact distances, one wave per band row
+  const double qnrm = (double)qnorm[4 * qi + 0];
+  for (int c = wave; c < band; c += 4) {
+    const uint32_t row = s_rows[c];
+    const float *cr = C + (int64_t)row * ld;
+    double dq = 0.0, dc = 0.0;
+    for (int i = lane; i < dim; i += 64) {
+      const double x = (double)cr[i];
+      dq += x * (double)s_q[i];
+      dc += x * x;
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+      dq += __shfl_xor(dq, o);
+      dc += __shfl_xor(dc, o);
+    }
+    if (lane == 0) {
+      const float dist = (float)(1.0 - dq / ((sqrt(dc) + 1e-30) * (qnrm + 1e-30)));
+      s_ex[c] = ((uint64_t)f32_order(dist) << 32) | row;
+    }
+  }
+  __syncthreads();
+  // 5. top-k of the band by rank
+  for (int c = tid; c < band; c += 256) {
+    const uint64_t key = s_ex[c];
+    int rank = 0;
+    for (int i = 0; i < band; ++i) rank += s_ex[i] < key ? 1 : 0;
+    if (rank < k) {
+      out_dist[(int64_t)qi * k + rank] = f32_unorder((uint32_t)(key >> 32));
+      out_row[(int64_t)qi * k + rank] = (int64_t)(uint32_t)key;
+    }
+  }
+  for (int i = band + tid; i < k; i += 256) {
+    out_dist[(int64_t)qi * k + i] = 0.f;
+    out_row[(int64_t)qi * k + i] = -1;
+  }
+}
+
 // Tournament merge of n_cblocks sorted lists per query -> final top-k.
+// qmask (nullable): only queries with qmask[q] != 0 are written.
 __global__ void __launch_bounds__(256) dense_merge_kernel(const uint64_t *__restrict__ cand, int n_cblocks, int QB,
-                                                          int k, int nq, float *__restrict__ out_dist,
+                                                          int k, int nq, const int32_t *__restrict__ qmask,
+                                                          float *__restrict__ out_dist,
                                                           int64_t *__restrict__ out_row) {
   const int q = blockIdx.x;
-  if (q >= nq) return;
+  if (q >= nq || (qmask && !qmask[q])) return;
   const int qg = q / QB;
   const int ql = q - qg * QB;
   constexpr int kPer = 8;  // lists per thread (n_cblocks <= 2048)
@@ -641,7 +1147,7 @@ __global__ void __launch_bounds__(256) dense_scatter_kernel(const float *__restr
                                                             int64_t row0, int64_t n, int dim, int ld,
                                                             float *__restrict__ C, float *__restrict__ invc,
                                                             uint32_t *__restrict__ live, _Float16 *__restrict__ Xh,
-                                                            _Float16 *__restrict__ Xl) {
+                                                            _Float16 *__restrict__ Xl, uint32_t *__restrict__ rnorm) {
   const int64_t i = blockIdx.x;
   if (i >= n) return;
   const int64_t r = rows ? rows[i] : row0 + i;
@@ -663,11 +1169,34 @@ __global__ void __launch_bounds__(256) dense_scatter_kernel(const float *__restr
     invc[r] = inv;
     atomicOr(&live[r >> 5], 1u << (r & 31));
   }
+  float sh = 0.f, sl = 0.f;
   for (int c = threadIdx.x; c < ld; c += 256) {
     const float xn = (c < dim ? s[c] : 0.f) * inv;
     const _Float16 hi = (_Float16)xn;
-    Xh[r * ld + c] = hi;
-    Xl[r * ld + c] = (_Float16)(xn - (float)hi);
+    const _Float16 lo = (_Float16)(xn - (float)hi);
+    Xh[plane_off(r, c, ld)] = hi;
+    Xl[plane_off(r, c, ld)] = lo;
+    sh += (float)hi * (float)hi;
+    sl += (float)lo * (float)lo;
+  }
+  // running maxima of ||Xh_r|| and ||Xl_r|| (K1c's error bound; non-negative floats order as
+  // their bit patterns); never lowered by deletes, so the bound stays conservative
+  for (int o = 32; o > 0; o >>= 1) {
+    sh += __shfl_xor(sh, o);
+    sl += __shfl_xor(sl, o);
+  }
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) {
+    red[threadIdx.x >> 6] = sh;
+  }
+  __shared__ float red2[4];
+  if ((threadIdx.x & 63) == 0) red2[threadIdx.x >> 6] = sl;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float nh = sqrtf((red[0] + red[1]) + (red[2] + red[3]));
+    const float nl = sqrtf((red2[0] + red2[1]) + (red2[2] + red2[3]));
+    atomicMax(&rnorm[0], __float_as_uint(nh));
+    atomicMax(&rnorm[1], __float_as_uint(nl));
   }
 }
 
@@ -709,7 +1238,11 @@ struct cm_dense {
   int64_t size = 0;        // high-water row count
   float *C = nullptr;
   float *invc = nullptr;
-  _Float16 *Xh = nullptr, *Xl = nullptr;  // normalised f16 split planes (K1b)
+  _Float16 *Xh = nullptr, *Xl = nullptr;  // normalised f16 split planes (K1b/K1c)
+  float *rnorm = nullptr;                  // device {max ||Xh_r||, max ||Xl_r||} (K1c bound)
+  int path = 0;                            // cm_dense_set_path (0 = automatic)
+  int32_t last_fallbacks = -1;             // K1c queries re-run exactly by the last host search
+  KernelTimer timer;                       // scan-kernel events (cm_dense_timing)
   uint32_t *live = nullptr;
   hipStream_t stream = nullptr;
   DevBuf staging, rows_buf, allow_buf, ws, out_buf;
@@ -857,7 +1390,8 @@ int dense_grow(cm_dense *h, int64_t need_rows) {
   return CM_OK;
 }
 
-// CM_DENSE_DEBUG (ablation only): bit0 skip K1b's top-k epilogue.
+// CM_DENSE_DEBUG (ablation only) for the scan kernels: bit0 skip the top-k epilogue, bit4 filter
+// without inserting survivors, bit5 (K1c) no sample pre-pass.
 int dense_debug_flags() {
   static const int f = [] {
     const char *e = getenv("CM_DENSE_DEBUG");
@@ -866,16 +1400,26 @@ int dense_debug_flags() {
   return f;
 }
 
-// K1b (f16x3 planes, all queries of a pass resident) for large batches.
-bool use_k1b(const cm_dense *h, int nq, int k) {
-  static const int force = [] {
-    const char *e = getenv("CM_DENSE_PATH");  // "f32" / "f16x3": force a path (A/B probes)
-    return e ? (e[0] == 'f' && e[1] == '3' ? 1 : (e[0] == 'f' && e[1] == '1' ? 2 : 0)) : 0;
+// Scan kernel for (nq, k): K1c (coarse f16 + certified re-rank) whenever its list length fits,
+// K1b (f16x3) for other batched k <= 32, K1 (fp32) otherwise.  CM_DENSE_PATH=f32|f16x3|coarse
+// forces a path (A/B probes; an ineligible forced path falls back to the default rule).
+int dense_kind(const cm_dense *h, int nq, int k) {
+  static const int env_force = [] {
+    const char *e = getenv("CM_DENSE_PATH");
+    if (!e) return 0;
+    const std::string s(e);
+    return s == "f32" ? CM_DENSE_F32 : s == "f16x3" ? CM_DENSE_F16X3 : s == "coarse" ? CM_DENSE_COARSE : 0;
   }();
-  if (force == 1) return false;
-  if (k > kBMaxK || h->ld % 32) return false;
-  if (force == 2) return true;
-  return nq >= 64;
+  const int force = h->path ? h->path : env_force;
+  // K1c: resident-query scan instances (ld 768 / 384), a sample of >= 1024 rows for the seed
+  const bool coarse_ok = k <= kBMaxK && (h->ld == 768 || h->ld == 384) && h->size >= 16384;
+  const bool split_ok = k <= kBMaxK && h->ld % 128 == 0;
+  if (force == CM_DENSE_F32) return CM_DENSE_F32;
+  if (force == CM_DENSE_F16X3 && split_ok) return CM_DENSE_F16X3;
+  if (force == CM_DENSE_COARSE && coarse_ok) return CM_DENSE_COARSE;
+  if (coarse_ok) return CM_DENSE_COARSE;
+  if (split_ok && nq >= 64) return CM_DENSE_F16X3;
+  return CM_DENSE_F32;
 }
 
 struct K1bCfg {
@@ -894,46 +1438,144 @@ K1bCfg k1b_config(const cm_dense *h, int nq) {
   return c;
 }
 
+// K1c sample pre-pass geometry: a prefix of 1/64 of the rows (1/16 below 1M rows) in 64-row
+// groups, one group range per workgroup, as many workgroups per pass as the main scan.
+struct K1cSample {
+  int n_wg;
+  int64_t rows_per_wg, rows_end;
+};
+K1cSample k1c_sample(const cm_dense *h, const K1bCfg &c) {
+  K1cSample s{};
+  const int64_t frac = c.rows_end >= (1 << 20) ? 64 : 16;
+  s.rows_end = round_up(std::max<int64_t>(c.rows_end / frac, 1), kRRows);
+  const int64_t tiles = s.rows_end / kRRows;
+  const int64_t want = std::max(1, num_cus(h->dev) / c.n_pass);
+  const int64_t per = ceil_div(tiles, std::min<int64_t>(want, tiles));
+  s.rows_per_wg = per * kRRows;
+  s.n_wg = (int)ceil_div(tiles, per);
+  return s;
+}
+
 struct K1bWs {
   _Float16 *qh, *ql;
-  uint64_t *cand;
+  float *qnorm;
+  uint64_t *cand;     // K1b lists (k per range) -- K1c: fallback pass
+  uint64_t *keys;     // K1c candidate buffers [pass][range][query][kCBufCap]
+  uint32_t *cnt;      // K1c buffer fill counts [pass][range][query]
+  float *mins;        // K1c sample minima [pass][sample range][query]
+  float *seed;        // K1c per-query insertion bound from the sample
+  int32_t *fb_mask;   // K1c: queries sent to the fallback pass
+  int32_t *fb_count;
   size_t total;
 };
-K1bWs k1b_ws_layout(const cm_dense *h, const K1bCfg &c, int k, void *base) {
+K1bWs k1b_ws_layout(const cm_dense *h, const K1bCfg &c, int k, bool coarse, void *base) {
   K1bWs w{};
   char *p = reinterpret_cast<char *>(base);
   size_t off = 0;
   const int64_t nq_pad = (int64_t)c.n_pass * kBQPass;
-  w.qh = reinterpret_cast<_Float16 *>(p + off);
-  off += round_up(nq_pad * h->ld * 2, 256);
-  w.ql = reinterpret_cast<_Float16 *>(p + off);
-  off += round_up(nq_pad * h->ld * 2, 256);
-  w.cand = reinterpret_cast<uint64_t *>(p + off);
-  off += round_up((int64_t)c.n_pass * c.n_wg * kBQPass * k * 8, 256);
+  auto take = [&](int64_t bytes) -> char * {
+    char *r = p + off;
+    off += round_up(std::max<int64_t>(bytes, 1), 256);
+    return r;
+  };
+  w.qh = reinterpret_cast<_Float16 *>(take(nq_pad * h->ld * 2));
+  w.ql = reinterpret_cast<_Float16 *>(take(nq_pad * h->ld * 2));
+  w.qnorm = reinterpret_cast<float *>(take(nq_pad * 16));
+  w.cand = reinterpret_cast<uint64_t *>(take((int64_t)c.n_pass * c.n_wg * kBQPass * k * 8));
+  if (coarse) {
+    w.keys = reinterpret_cast<uint64_t *>(take((int64_t)c.n_pass * c.n_wg * kBQPass * kCBufCap * 8));
+    w.cnt = reinterpret_cast<uint32_t *>(take((int64_t)c.n_pass * c.n_wg * kBQPass * 4));
+    const K1cSample sm = k1c_sample(h, c);
+    w.mins = reinterpret_cast<float *>(take((int64_t)c.n_pass * sm.n_wg * kBQPass * 4));
+    w.seed = reinterpret_cast<float *>(take(nq_pad * 4));
+    w.fb_mask = reinterpret_cast<int32_t *>(take(nq_pad * 4));
+    w.fb_count = reinterpret_cast<int32_t *>(take(4));
+  }
   w.total = off;
   return w;
 }
 
-int launch_k1b(cm_dense *h, const float *q_dev, int nq, int k, const uint32_t *allow, float *dist_dev,
-               int64_t *row_dev, void *ws, int64_t ws_bytes, hipStream_t st) {
+template <int NPL>
+int set_split_lds() {
   static std::once_flag once;
-  static hipError_t attr_err = hipSuccess;
+  static hipError_t err = hipSuccess;
   std::call_once(once, [] {
-    attr_err = hipFuncSetAttribute(reinterpret_cast<const void *>(&dense_f16x3_kernel),
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, k1b_lds_layout().total);
+    err = hipFuncSetAttribute(reinterpret_cast<const void *>(&dense_split_kernel<NPL>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, k1b_lds_layout().total);
   });
-  CM_HIP(attr_err);
+  CM_HIP(err);
+  return CM_OK;
+}
+
+// K1b: f16x3 scan of every query + tournament merge.  K1c: coarse scan -> certification and
+// exact re-rank -> f16x3 pass restricted to the queries the certificate rejected (its
+// workgroups exit at once when there are none) -> merge of those queries only.
+int launch_split(cm_dense *h, const float *q_dev, int nq, int k, bool coarse, const uint32_t *allow,
+                 float *dist_dev, int64_t *row_dev, void *ws, int64_t ws_bytes, hipStream_t st) {
+  int rc;
+  if ((rc = set_split_lds<2>())) return rc;
+  if (coarse) {
+    static std::once_flag once;
+    static hipError_t err = hipSuccess;
+    std::call_once(once, [] {
+      const std::pair<const void *, int> fs[] = {
+          {reinterpret_cast<const void *>(&dense_coarse_scan_kernel<12, 2, false>), K1rLds<2>::total},
+          {reinterpret_cast<const void *>(&dense_coarse_scan_kernel<12, 2, true>), K1rLds<2>::total},
+          {reinterpret_cast<const void *>(&dense_coarse_scan_kernel<6, 0, false>), K1rLds<0>::total},
+          {reinterpret_cast<const void *>(&dense_coarse_scan_kernel<6, 0, true>), K1rLds<0>::total},
+          {reinterpret_cast<const void *>(&dense_rerank_kernel), kGatherCap * 12}};
+      for (const auto &f : fs) {
+        const hipError_t e = hipFuncSetAttribute(f.first, hipFuncAttributeMaxDynamicSharedMemorySize, f.second);
+        if (e != hipSuccess) err = e;
+      }
+    });
+    CM_HIP(err);
+  }
   const K1bCfg c = k1b_config(h, nq);
-  const K1bWs w = k1b_ws_layout(h, c, k, ws);
+  const K1bWs w = k1b_ws_layout(h, c, k, coarse, ws);
   if ((int64_t)w.total > ws_bytes || !ws) CM_FAIL(CM_EINVAL, "dense workspace too small");
+  const size_t lds = k1b_lds_layout().total;
+  const int64_t n_words = ceil_div(h->size, 32);
+  const dim3 grid(c.n_wg * c.n_pass);
   hipLaunchKernelGGL(dense_prep_planes, dim3(c.n_pass * kBQPass), dim3(256), 0, st, q_dev, nq, h->dim, h->ld, w.qh,
-                     w.ql);
+                     w.ql, w.qnorm);
   CM_HIP(hipGetLastError());
-  hipLaunchKernelGGL(dense_f16x3_kernel, dim3(c.n_wg * c.n_pass), dim3(512), k1b_lds_layout().total, st, h->Xh, h->Xl,
-                     h->ld, h->live, allow, ceil_div(h->size, 32), w.qh, w.ql, nq, k, c.rows_per_wg, c.rows_end,
-                     c.n_wg, w.cand, dense_debug_flags());
+  const int32_t *mask = nullptr;
+  if (coarse) {
+    CM_HIP(hipMemsetAsync(w.fb_count, 0, 4, st));
+    const K1cSample sm = k1c_sample(h, c);
+    const bool d768 = h->ld == 768;
+    auto scan = [&](bool minonly) {
+      if (d768) return minonly ? &dense_coarse_scan_kernel<12, 2, true> : &dense_coarse_scan_kernel<12, 2, false>;
+      return minonly ? &dense_coarse_scan_kernel<6, 0, true> : &dense_coarse_scan_kernel<6, 0, false>;
+    };
+    const size_t slds = d768 ? K1rLds<2>::total : K1rLds<0>::total;
+    // 1. sample pre-pass (per-group minima) -> seed
+    hipLaunchKernelGGL(scan(true), dim3(sm.n_wg * c.n_pass), dim3(256), slds, st, h->Xh, h->live, allow, n_words,
+                       w.qh, nq, (const float *)nullptr, sm.rows_per_wg, sm.rows_end, sm.n_wg, (uint64_t *)nullptr,
+                       (uint32_t *)nullptr, w.mins);
+    CM_HIP(hipGetLastError());
+    hipLaunchKernelGGL(dense_seed_kernel, dim3(nq), dim3(256), 0, st, w.mins, sm.n_wg, k, nq, w.qnorm, h->rnorm,
+                       h->dim, w.seed);
+    CM_HIP(hipGetLastError());
+    // 2. coarse scan: rows under the seed -> candidate buffers
+    h->timer.begin(st);
+    hipLaunchKernelGGL(scan(false), grid, dim3(256), slds, st, h->Xh, h->live, allow, n_words, w.qh, nq,
+                       (const float *)w.seed, c.rows_per_wg, c.rows_end, c.n_wg, w.keys, w.cnt, (float *)nullptr);
+    h->timer.end(st);
+    CM_HIP(hipGetLastError());
+    // 3. certificate + exact re-rank (failures -> fb_mask)
+    hipLaunchKernelGGL(dense_rerank_kernel, dim3(nq), dim3(256), kGatherCap * 12, st, w.keys, w.cnt, c.n_wg, k, nq,
+                       h->C, h->ld, h->dim, q_dev, w.qnorm, h->rnorm, dist_dev, row_dev, w.fb_mask, w.fb_count);
+    CM_HIP(hipGetLastError());
+    mask = w.fb_mask;
+  }
+  if (!coarse) h->timer.begin(st);
+  hipLaunchKernelGGL(dense_split_kernel<2>, grid, dim3(512), lds, st, h->Xh, h->Xl, h->ld, h->live, allow, n_words,
+                     w.qh, w.ql, nq, mask, k, c.rows_per_wg, c.rows_end, c.n_wg, w.cand, dense_debug_flags());
+  if (!coarse) h->timer.end(st);
   CM_HIP(hipGetLastError());
-  hipLaunchKernelGGL(dense_merge_kernel, dim3(nq), dim3(256), 0, st, w.cand, c.n_wg, kBQPass, k, nq, dist_dev,
+  hipLaunchKernelGGL(dense_merge_kernel, dim3(nq), dim3(256), 0, st, w.cand, c.n_wg, kBQPass, k, nq, mask, dist_dev,
                      row_dev);
   CM_HIP(hipGetLastError());
   return CM_OK;
@@ -962,6 +1604,10 @@ int cm_dense_create(int device, int32_t dim, int64_t capacity, cm_dense **out) {
     delete h;
     CM_FAIL(CM_EDEVICE, "hipStreamCreate failed");
   }
+  if (hipMalloc(&h->rnorm, 8) != hipSuccess || hipMemset(h->rnorm, 0, 8) != hipSuccess) {
+    cm_dense_destroy(h);
+    CM_FAIL(CM_ENOMEM, "dense: out of device memory");
+  }
   int rc = dense_grow(h, std::max<int64_t>(capacity, kStepRows));
   if (rc) {
     cm_dense_destroy(h);
@@ -980,6 +1626,8 @@ void cm_dense_destroy(cm_dense *h) {
   if (h->live) (void)hipFree(h->live);
   if (h->Xh) (void)hipFree(h->Xh);
   if (h->Xl) (void)hipFree(h->Xl);
+  if (h->rnorm) (void)hipFree(h->rnorm);
+  h->timer.release();
   h->staging.release();
   h->rows_buf.release();
   h->allow_buf.release();
@@ -1016,7 +1664,8 @@ int cm_dense_upsert(cm_dense *h, const float *vecs, const int64_t *rows, int64_t
     CM_HIP(hipMemcpyAsync(h->staging.ptr, vecs + s * h->dim, (size_t)m * h->dim * 4, hipMemcpyHostToDevice, h->stream));
     CM_HIP(hipMemcpyAsync(h->rows_buf.ptr, rows + s, (size_t)m * 8, hipMemcpyHostToDevice, h->stream));
     hipLaunchKernelGGL(dense_scatter_kernel, dim3((unsigned)m), dim3(256), 0, h->stream, h->staging.as<float>(),
-                       h->rows_buf.as<int64_t>(), (int64_t)0, m, h->dim, h->ld, h->C, h->invc, h->live, h->Xh, h->Xl);
+                       h->rows_buf.as<int64_t>(), (int64_t)0, m, h->dim, h->ld, h->C, h->invc, h->live, h->Xh, h->Xl,
+                       reinterpret_cast<uint32_t *>(h->rnorm));
     CM_HIP(hipGetLastError());
     CM_HIP(hipStreamSynchronize(h->stream));
   }
@@ -1040,7 +1689,7 @@ int cm_dense_upsert_dev(cm_dense *h, const float *vecs_dev, int64_t row0, int64_
     const int64_t m = std::min(batch, n - s);
     hipLaunchKernelGGL(dense_scatter_kernel, dim3((unsigned)m), dim3(256), 0, st, vecs_dev + s * h->dim,
                        (const int64_t *)nullptr, row0 + s, m, h->dim, h->ld, h->C, h->invc, h->live, h->Xh,
-                       h->Xl);
+                       h->Xl, reinterpret_cast<uint32_t *>(h->rnorm));
     CM_HIP(hipGetLastError());
   }
   h->size = std::max(h->size, row0 + n);
@@ -1070,6 +1719,7 @@ int cm_dense_reset(cm_dense *h) {
   CM_HIP(hipMemsetAsync(h->C, 0, (size_t)h->rows_alloc * h->ld * 4, h->stream));
   CM_HIP(hipMemsetAsync(h->Xh, 0, (size_t)h->rows_alloc * h->ld * 2, h->stream));
   CM_HIP(hipMemsetAsync(h->Xl, 0, (size_t)h->rows_alloc * h->ld * 2, h->stream));
+  CM_HIP(hipMemsetAsync(h->rnorm, 0, 8, h->stream));
   CM_HIP(hipStreamSynchronize(h->stream));
   h->size = 0;
   return CM_OK;
@@ -1096,9 +1746,50 @@ int64_t cm_dense_live_count(cm_dense *h) {
 
 int64_t cm_dense_search_workspace(cm_dense *h, int32_t nq, int32_t k) {
   if (!h || nq <= 0 || k <= 0 || k > kMaxTopK) return -1;
-  if (use_k1b(h, nq, k)) return (int64_t)k1b_ws_layout(h, k1b_config(h, nq), k, nullptr).total;
+  const int kind = dense_kind(h, nq, k);
+  if (kind != CM_DENSE_F32) return (int64_t)k1b_ws_layout(h, k1b_config(h, nq), k, kind == CM_DENSE_COARSE, nullptr).total;
   DenseCfg c = dense_config(h, nq, k);
   return (int64_t)dense_ws_layout(h, c, nq, k, nullptr).total;
+}
+
+int cm_dense_set_path(cm_dense *h, int32_t kind) {
+  if (!h) CM_FAIL(CM_EINVAL, "null handle");
+  if (kind < 0 || kind > CM_DENSE_COARSE) CM_FAIL(CM_EINVAL, "unknown dense path");
+  h->path = kind;
+  return CM_OK;
+}
+
+int32_t cm_dense_workspace_fallbacks(cm_dense *h, int32_t nq, int32_t k, const void *workspace_dev) {
+  if (!h || !workspace_dev || nq <= 0 || k <= 0 || k > kMaxTopK) return -1;
+  if (dense_kind(h, nq, k) != CM_DENSE_COARSE) return 0;
+  DeviceGuard dg(h->dev);
+  const K1bWs w = k1b_ws_layout(h, k1b_config(h, nq), k, true, const_cast<void *>(workspace_dev));
+  int32_t c = -1;
+  if (hipMemcpy(&c, w.fb_count, 4, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+  return c;
+}
+
+int32_t cm_dense_last_fallbacks(cm_dense *h) { return h ? h->last_fallbacks : -1; }
+
+int cm_dense_timing(cm_dense *h, int32_t enable) {
+  if (!h) CM_FAIL(CM_EINVAL, "null handle");
+  DeviceGuard dg(h->dev);
+  h->timer.on = enable != 0;
+  h->timer.used = 0;
+  return CM_OK;
+}
+
+int32_t cm_dense_timing_drain(cm_dense *h, float *ms_out, int32_t cap) {
+  if (!h) CM_FAIL(CM_EINVAL, "null handle");
+  DeviceGuard dg(h->dev);
+  const int n = h->timer.drain(ms_out, cap);
+  if (n < 0) CM_FAIL(CM_EDEVICE, "event query failed");
+  return n;
+}
+
+int32_t cm_dense_search_kind(cm_dense *h, int32_t nq, int32_t k) {
+  if (!h || nq <= 0 || k <= 0 || k > kMaxTopK) return -1;
+  return dense_kind(h, nq, k);
 }
 
 int cm_dense_search_dev(cm_dense *h, const float *q_dev, int32_t nq, int32_t k, const uint32_t *allow_dev,
@@ -1109,7 +1800,10 @@ int cm_dense_search_dev(cm_dense *h, const float *q_dev, int32_t nq, int32_t k, 
   if (k <= 0 || k > kMaxTopK) CM_FAIL(CM_EINVAL, "k must be in [1, " + std::to_string(kMaxTopK) + "]");
   DeviceGuard dg(h->dev);
   hipStream_t st = (hipStream_t)stream;  // NULL = the null stream (torch default)
-  if (use_k1b(h, nq, k)) return launch_k1b(h, q_dev, nq, k, allow_dev, dist_dev, row_dev, workspace_dev, workspace_bytes, st);
+  const int kind = dense_kind(h, nq, k);
+  if (kind != CM_DENSE_F32)
+    return launch_split(h, q_dev, nq, k, kind == CM_DENSE_COARSE, allow_dev, dist_dev, row_dev, workspace_dev,
+                        workspace_bytes, st);
   DenseCfg c = dense_config(h, nq, k);
   if (c.lds > 163840) CM_FAIL(CM_EUNSUPPORTED, "dim/k too large for the LDS-resident query tile");
   DenseWs w = dense_ws_layout(h, c, nq, k, workspace_dev);
@@ -1117,9 +1811,12 @@ int cm_dense_search_dev(cm_dense *h, const float *q_dev, int32_t nq, int32_t k, 
   const int nq_pad = c.n_qgroups * c.QB;
   hipLaunchKernelGGL(dense_prep_queries, dim3(nq_pad), dim3(256), 0, st, q_dev, nq, h->dim, h->ld, w.qp, w.invq);
   CM_HIP(hipGetLastError());
+  h->timer.begin(st);
   int rc = launch_dense(c, h, allow_dev, w.qp, w.invq, nq, k, w.cand, st);
+  h->timer.end(st);
   if (rc) return rc;
-  hipLaunchKernelGGL(dense_merge_kernel, dim3(nq), dim3(256), 0, st, w.cand, c.n_cblocks, c.QB, k, nq, dist_dev,
+  hipLaunchKernelGGL(dense_merge_kernel, dim3(nq), dim3(256), 0, st, w.cand, c.n_cblocks, c.QB, k, nq,
+                     (const int32_t *)nullptr, dist_dev,
                      row_dev);
   CM_HIP(hipGetLastError());
   return CM_OK;
@@ -1194,6 +1891,11 @@ int cm_dense_search(cm_dense *h, const float *q, int32_t nq, int32_t k, const ui
   CM_HIP(hipMemcpyAsync(out_dist, d_dist, (size_t)nq * k * 4, hipMemcpyDeviceToHost, h->stream));
   CM_HIP(hipMemcpyAsync(out_row, d_row, (size_t)nq * k * 8, hipMemcpyDeviceToHost, h->stream));
   if (out_vec) CM_HIP(hipMemcpyAsync(out_vec, d_vec, vbytes, hipMemcpyDeviceToHost, h->stream));
+  h->last_fallbacks = 0;
+  if (dense_kind(h, nq, k) == CM_DENSE_COARSE) {
+    const K1bWs w = k1b_ws_layout(h, k1b_config(h, nq), k, true, h->ws.ptr);
+    CM_HIP(hipMemcpyAsync(&h->last_fallbacks, w.fb_count, 4, hipMemcpyDeviceToHost, h->stream));
+  }
   CM_HIP(hipStreamSynchronize(h->stream));
   return CM_OK;
 }

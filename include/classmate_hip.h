@@ -86,6 +86,31 @@ int cm_dense_search(cm_dense *h, const float *q, int32_t nq, int32_t k, const ui
                     float *out_dist, int64_t *out_row, float *out_vec);
 /* workspace bytes cm_dense_search_dev needs for (nq, k). */
 int64_t cm_dense_search_workspace(cm_dense *h, int32_t nq, int32_t k);
+/* which scan kernel cm_dense_search[_dev] runs for (nq, k): CM_DENSE_F32
+ * (K1, fp32 MFMA, reads 4 B/element), CM_DENSE_F16X3 (K1b, split-f16
+ * planes, 4 B/element), CM_DENSE_COARSE (K1c, f16 hi plane, 2 B/element,
+ * certified exact re-rank); -1 on error.  Lets callers price the launch
+ * against the right roofline.                                            */
+#define CM_DENSE_F32 1
+#define CM_DENSE_F16X3 2
+#define CM_DENSE_COARSE 3
+int32_t cm_dense_search_kind(cm_dense *h, int32_t nq, int32_t k);
+/* force a scan kernel for this handle (0 = automatic; an ineligible forced
+ * kind falls back to the automatic choice).  Results agree within the 1e-4
+ * distance tolerance on every path; used for A/B probes and parity tests. */
+int cm_dense_set_path(cm_dense *h, int32_t kind);
+/* K1c: number of queries of the search that last used `workspace_dev` whose
+ * certificate failed and that were re-run by the exact f16x3 pass
+ * (synchronous read; 0 for other paths, -1 on error).                    */
+int32_t cm_dense_workspace_fallbacks(cm_dense *h, int32_t nq, int32_t k, const void *workspace_dev);
+/* same, for the last host-array cm_dense_search on this handle. */
+int32_t cm_dense_last_fallbacks(cm_dense *h);
+/* kernel timing (bench roofline): while enabled, every search records HIP
+ * events on its launch stream around its scan kernel (K1 / K1b / K1c coarse
+ * scan); _drain synchronises on them, writes up to cap elapsed ms values and
+ * returns how many were recorded (< 0 on error).                         */
+int cm_dense_timing(cm_dense *h, int32_t enable);
+int32_t cm_dense_timing_drain(cm_dense *h, float *ms_out, int32_t cap);
 int cm_dense_search_dev(cm_dense *h, const float *q_dev, int32_t nq, int32_t k, const uint32_t *allow_dev,
                         float *dist_dev, int64_t *row_dev, void *workspace_dev, int64_t workspace_bytes,
                         void *stream);
@@ -128,6 +153,10 @@ int cm_bm25_stats(cm_bm25 *h, int64_t *n_live, int64_t *sum_len, double *avgdl, 
  * max_bytes = 0 disables.  Results are identical either way. */
 int cm_bm25_set_head_policy(cm_bm25 *h, double min_df_frac, int64_t max_bytes);
 int32_t cm_bm25_num_head_terms(cm_bm25 *h);
+/* kernel timing (bench roofline): events around every search's K2 launch;
+ * same contract as cm_dense_timing / cm_dense_timing_drain.              */
+int cm_bm25_timing(cm_bm25 *h, int32_t enable);
+int32_t cm_bm25_timing_drain(cm_bm25 *h, float *ms_out, int32_t cap);
 /* Sharding support: local df per term and the first posting's
  * (row << 32 | first position) key (0xff..ff when absent), so ranks can
  * all-reduce df (sum) and first keys (min, after offsetting rows) and agree

@@ -65,9 +65,14 @@ def test_dense_golden_corpus(eng, corpus, golden):
         np.testing.assert_allclose(dist[i], [w[1] for w in want], atol=DIST_TOL)
 
 
-def test_dense_filtered_and_deleted(eng, corpus):
+PATHS = [0, 1, 2, 3]   # auto, K1 fp32, K1b f16x3, K1c coarse + certified re-rank
+
+
+@pytest.mark.parametrize("path", PATHS[1:])
+def test_dense_filtered_and_deleted(eng, corpus, path):
     emb, qv = corpus["emb"], corpus["qvecs"]
     idx = eng.DenseIndex(768)
+    idx.set_path(path)
     idx.upsert(emb, np.arange(emb.shape[0]))
     allow = np.array([m.get("course") == "cs101" for m in corpus["metas"]])
     dist, rows = idx.search(qv, 24, _bits(allow))
@@ -89,12 +94,14 @@ def test_dense_filtered_and_deleted(eng, corpus):
 
 @pytest.mark.parametrize("n,nq,k,dim", [(20000, 1, 10, 768), (20000, 48, 24, 768), (9000, 64, 10, 384),
                                         (5000, 7, 100, 768), (3000, 3, 256, 256), (777, 33, 5, 1000)])
-def test_dense_shapes(eng, n, nq, k, dim):
+@pytest.mark.parametrize("path", PATHS)
+def test_dense_shapes(eng, n, nq, k, dim, path):
     rng = np.random.default_rng(n + nq + k)
     emb = rng.standard_normal((n, dim)).astype(np.float32)
     q = rng.standard_normal((nq, dim)).astype(np.float32)
     q[: nq // 2] = emb[rng.integers(0, n, nq // 2)] + 0.05 * q[: nq // 2]
     idx = eng.DenseIndex(dim)
+    idx.set_path(path)
     perm = rng.permutation(n)       # scattered upsert order
     idx.upsert(emb[perm], perm)
     dist, rows = idx.search(q, k)
@@ -103,15 +110,17 @@ def test_dense_shapes(eng, n, nq, k, dim):
 
 @pytest.mark.parametrize("n,nq,k,dim", [(30000, 64, 24, 768), (12345, 100, 10, 384), (5000, 300, 32, 100),
                                         (40000, 256, 1, 768), (257, 80, 32, 64)])
-def test_dense_batched_f16x3_path(eng, n, nq, k, dim):
-    """Batches of >= 64 queries with k <= 32 take K1b (f16x3 split planes, all
-    queries of a pass resident); distances within 1e-4, sets/order as the oracle,
+@pytest.mark.parametrize("path", [2, 3])
+def test_dense_batched_split_paths(eng, n, nq, k, dim, path):
+    """K1b (f16x3 split planes) and K1c (coarse f16 scan + certified exact re-rank),
+    all queries of a pass resident: distances within 1e-4, sets/order as the oracle,
     deletes and filters honoured, multiple query passes (nq > 256)."""
     rng = np.random.default_rng(n + nq + k)
     emb = rng.standard_normal((n, dim)).astype(np.float32) * rng.uniform(0.1, 10, (n, 1)).astype(np.float32)
     q = rng.standard_normal((nq, dim)).astype(np.float32)
     q[: nq // 2] = emb[rng.integers(0, n, nq // 2)] + 0.05 * q[: nq // 2]
     idx = eng.DenseIndex(dim)
+    idx.set_path(path)
     idx.upsert(emb, np.arange(n))
     dist, rows = idx.search(q, k)
     _check_dense(dist, rows, emb, q, k)
@@ -122,6 +131,33 @@ def test_dense_batched_f16x3_path(eng, n, nq, k, dim):
     live[dele] = False
     dist, rows = idx.search(q, k, _bits(allow))
     _check_dense(dist, rows, emb, q, k, live)
+
+
+def test_dense_coarse_certificate(eng):
+    """K1c: on well-separated data every query is certified (no exact re-run); on a
+    cluster of near-duplicates wider than the coarse lists the certificate fails and
+    the exact f16x3 pass takes over -- results stay within tolerance either way."""
+    rng = np.random.default_rng(77)
+    n, dim = 30000, 768
+    emb = rng.standard_normal((n, dim)).astype(np.float32)
+    q = rng.standard_normal((64, dim)).astype(np.float32)
+    idx = eng.DenseIndex(dim)
+    idx.set_path(3)
+    idx.upsert(emb, np.arange(n))
+    assert idx.search_kind(64, 24) == 3
+    dist, rows = idx.search(q, 24)
+    _check_dense(dist, rows, emb, q, 24)
+    assert idx.last_fallbacks() == 0
+    # 600 near-duplicates of one vector (cosine gaps ~1e-8, far inside the 2E band)
+    base = rng.standard_normal(dim).astype(np.float32)
+    dup = base + 1e-4 * rng.standard_normal((600, dim)).astype(np.float32)
+    emb2 = np.concatenate([emb, dup])
+    idx.upsert(dup, np.arange(n, n + 600))
+    q2 = np.concatenate([q[:8], base + 0.01 * rng.standard_normal((8, dim)).astype(np.float32)])
+    dist, rows = idx.search(q2, 24)
+    _check_dense(dist, rows, emb2, q2, 24)
+    assert idx.last_fallbacks() >= 8
+    assert (rows[8:] >= n).all()
 
 
 def test_dense_device_path_and_gather(eng):

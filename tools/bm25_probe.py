@@ -29,6 +29,13 @@ b.set_head_policy(a.head_frac, a.head_bytes)
 qt = sample_query_terms(tok, off, a.batch, 8, seed=10)
 q_terms = qt.reshape(-1).contiguous()
 q_off = (torch.arange(a.batch + 1, device="cuda", dtype=torch.int32) * 8).contiguous()
+df, _ = b.term_stats()
+qh = qt.cpu().numpy()
+qdf = df[qh].astype("int64")                                  # (B, 8)
+head = qdf > a.docs * a.head_frac
+print(f"workload: mean head terms/query {head.sum(1).mean():.2f}, mean head df sum/query {(qdf * head).sum(1).mean():.4g}, "
+      f"mean tail df sum/query {(qdf * ~head).sum(1).mean():.4g}, distinct head terms in batch "
+      f"{len(set(qh[head].tolist()))}, head tiles {b.num_head_terms}", flush=True)
 out = b.search_dev(q_terms, q_off, 10)
 torch.cuda.synchronize()
 ts = []

@@ -1,17 +1,11 @@
 #!/bin/bash
-# GPU: dense K1 timing + kernel trace + HBM traffic (FETCH_SIZE, separate pass).
+# GPU: kernel trace of the dense probe (per-kernel durations of one search pipeline).
 set -o pipefail
-mkdir -p gpurun_out; export TMPDIR=/tmp
-timeout -k 10 300 python tools/dense_probe.py > gpurun_out/dprobe.log 2>&1 || { tail -20 gpurun_out/dprobe.log; exit 1; }
-tail -1 gpurun_out/dprobe.log
-timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/dpmc -o pmc --output-format csv -- python3 tools/dense_probe.py --reps 2 > gpurun_out/dpmc.log 2>&1 || { tail -20 gpurun_out/dpmc.log; exit 1; }
+cd "${GRAFT_REPO_ROOT:-.}"; mkdir -p gpurun_out; export TMPDIR=/tmp
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/dprof -o dp --output-format csv -- python3 tools/dense_probe.py --path ${DPATH:-3} --reps 5 > gpurun_out/dprof.log 2>&1 || { tail -20 gpurun_out/dprof.log; exit 1; }
+f=$(find gpurun_out/dprof -name '*kernel_stats.csv' | head -1); cp "$f" gpurun_out/dense_kernel_stats.csv
 python3 - <<'PY'
-import csv, glob, collections
-f = glob.glob('gpurun_out/dpmc/**/*counter_collection.csv', recursive=True)[0]
-agg = collections.defaultdict(list)
-for r in csv.DictReader(open(f)):
-    agg[r['Kernel_Name'][:60]].append(float(r['Counter_Value']))
-for k, v in agg.items():
-    if 'dense' in k:
-        print(k, 'launches', len(v), 'FETCH_SIZE KB/launch avg', sum(v) / len(v))
+import csv
+for r in csv.DictReader(open('gpurun_out/dense_kernel_stats.csv')):
+    print(f"{r['Name'][:70]:70s} calls={r['Calls']:>4s} avg_us={float(r['AverageNs'])/1e3:10.1f}")
 PY
