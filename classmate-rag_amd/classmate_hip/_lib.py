@@ -84,6 +84,9 @@ SIGNATURES = {
     "cm_bm25_export": (c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp),
     "cm_bm25_set_head_policy": (c_int, c_vp, c_f64, c_i64),
     "cm_bm25_num_head_terms": (c_i32, c_vp),
+    "cm_bm25_set_path": (c_int, c_vp, c_i32),
+    "cm_bm25_workspace_rescored": (c_i32, c_vp, c_i32, c_i32, c_i32, c_vp),
+    "cm_bm25_last_rescored": (c_i32, c_vp),
     "cm_bm25_term_stats": (c_int, c_vp, c_vp, c_vp),
     "cm_bm25_set_stats": (c_int, c_vp, c_vp, c_i32, c_i64, c_i64, c_f64),
     "cm_bm25_search": (c_int, c_vp, c_vp, c_vp, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp),

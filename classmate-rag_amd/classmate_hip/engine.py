@@ -263,8 +263,24 @@ class BM25Index:
         """Dense tf tiles for high-df terms (same results; max_bytes=0 disables)."""
         L.check(L.fn["cm_bm25_set_head_policy"](self._h, float(min_df_frac), int(max_bytes)), "cm_bm25_set_head_policy")
 
+    # search strategy (cm_bm25_set_path): identical results either way
+    PATH_AUTO, PATH_FULL, PATH_PRUNED = 0, 1, 2
+
+    def set_path(self, kind: int):
+        """0 auto (pruned), 1 full K2 scan of every (query, range), 2 tail pass + bounded re-score."""
+        L.check(L.fn["cm_bm25_set_path"](self._h, int(kind)), "cm_bm25_set_path")
+
+    def last_rescored(self) -> int:
+        """(query, range) pairs K2 re-scored by the last host search() (-1 on the full path)."""
+        return int(L.fn["cm_bm25_last_rescored"](self._h))
+
+    def workspace_rescored(self, nq: int, total_terms: int, k: int, workspace) -> int:
+        """Same for the last search_dev() that used `workspace`."""
+        return int(L.fn["cm_bm25_workspace_rescored"](self._h, int(nq), int(total_terms), int(k),
+                                                      L.ptr(workspace)))
+
     def timing(self, enable: bool = True):
-        """Record HIP events around every search's K2 launch (see timing_drain)."""
+        """Record HIP events around every search's scoring launches (see timing_drain)."""
         L.check(L.fn["cm_bm25_timing"](self._h, int(bool(enable))), "cm_bm25_timing")
 
     def timing_drain(self, cap: int = 4096) -> list:

@@ -258,7 +258,8 @@ __global__ void __launch_bounds__(kBmThreads) __attribute__((amdgpu_waves_per_eu
                       const uint32_t *__restrict__ live, const uint32_t *__restrict__ allow, int64_t ndocs,
                       double avgdl, const double *__restrict__ lut, int lut_dmin, int k,
                       uint64_t *__restrict__ cand_key, uint32_t *__restrict__ cand_row,
-                      unsigned long long *__restrict__ thr_key, int dbg) {
+                      unsigned long long *__restrict__ thr_key, const uint8_t *__restrict__ need, int32_t vocab,
+                      int dbg) {
   __shared__ double s_lut[kLutW * kLutTF];
   __shared__ int32_t s_pdoc[kBmThreads / 64][kTailCapW];
   __shared__ uint16_t s_ptf[kBmThreads / 64][kTailCapW];
@@ -274,11 +275,22 @@ __global__ void __launch_bounds__(kBmThreads) __attribute__((amdgpu_waves_per_eu
   const int lb = (x < rem ? x * (per + 1) : rem * (per + 1) + (x - rem) * per) + y;
   const int nqg = (nq + kQPerWave - 1) / kQPerWave;
   const int wid = lb * (kBmThreads / 64) + wave;
-  const int q0 = (wid % nqg) * kQPerWave;
+  const int qg = wid % nqg;
+  const int q0 = qg * kQPerWave;
   const int rg = wid / nqg;
   const int r0 = rg * rpw, r1 = min(r0 + rpw, nr);
   if (r0 >= r1) return;  // whole wave
   const int nqw = min(kQPerWave, nq - q0);
+  // re-score mode (need != NULL, pruned search): only (range, query) pairs whose bit is set
+  // in need[qg * nr + r] are scored; the others keep the tail pass's lists
+  auto need_at = [&](int r) -> uint32_t {
+    return need ? (uint32_t)__builtin_amdgcn_readfirstlane((int)need[(int64_t)qg * nr + r]) : 0xfu;
+  };
+  if (need) {  // nothing to re-score in this wave's ranges (the common case): leave at once
+    uint32_t any = 0;
+    for (int r = r0; r < r1; ++r) any |= need_at(r);
+    if (!any) return;
+  }
   int32_t *pdoc = s_pdoc[wave];
   uint16_t *ptf = s_ptf[wave];
   uint64_t *keys = s_keys[wave];
@@ -297,15 +309,23 @@ __global__ void __launch_bounds__(kBmThreads) __attribute__((amdgpu_waves_per_eu
   int64_t my_lo = 0, my_hi = 0;
   if (has_term) {
     my_t = q_terms[my_i];
+    if (my_t >= vocab) my_t = -1;
     my_idf = q_idf[my_i];
     my_h = (my_t >= 0 && head_id) ? head_id[my_t] : -1;
     my_lo = bounds[(int64_t)my_i * bstride + r0];
     my_hi = bounds[(int64_t)my_i * bstride + r0 + 1];
   }
   const uint64_t headmask = __ballot(has_term && my_t >= 0 && my_h >= 0);
-  // ---- head-tile prefetch ring over the (range, query, head term) sequence
-  int c_r = r0;
-  uint64_t c_m = headmask;
+  // ---- head-tile prefetch ring over the (range, scored query, head term) sequence
+  auto head_at = [&](int r) -> uint64_t {
+    if (!need) return headmask;
+    const uint32_t nbits = need_at(r);
+    uint64_t qm = 0;
+#pragma unroll
+    for (int qq = 0; qq < kQPerWave; ++qq)
+      if ((nbits >> qq) & 1u) qm |= ((1ull << kTermLanes) - 1) << (kTermLanes * qq);
+    return headmask & qm;
+  };
   auto tile_at = [&](int r, uint64_t m) -> uint4 {
     if (m == 0 || r >= r1) return uint4{0, 0, 0, 0};
     const int j = __builtin_ctzll(m);
@@ -313,16 +333,19 @@ __global__ void __launch_bounds__(kBmThreads) __attribute__((amdgpu_waves_per_eu
     return *reinterpret_cast<const uint4 *>(headtf + (int64_t)h * npad + (int64_t)r * kRange + 16 * lane);
   };
   auto advance = [&](int &r, uint64_t &m) {
-    m &= m - 1;
-    if (m == 0) {
+    if (m) m &= m - 1;
+    while (m == 0 && r < r1) {
       ++r;
-      m = headmask;
+      m = r < r1 ? head_at(r) : 0;
     }
   };
+  int c_r = r0;
+  uint64_t c_m = head_at(r0);
+  if (c_m == 0) advance(c_r, c_m);
   uint4 n1 = tile_at(c_r, c_m);
-  if (headmask) advance(c_r, c_m);
+  advance(c_r, c_m);
   uint4 n2 = tile_at(c_r, c_m);
-  if (headmask) advance(c_r, c_m);
+  advance(c_r, c_m);
   // ---- range words (loaded one range ahead)
   int4 dlq[4];
   uint32_t lw = 0, aw = 0xffffffffu;
@@ -343,8 +366,19 @@ __global__ void __launch_bounds__(kBmThreads) __attribute__((amdgpu_waves_per_eu
     lw = live[w];
     aw = allow ? allow[w] : 0xffffffffu;
   };
-  load_range_words(r0);
+  if (need_at(r0)) load_range_words(r0);
   for (int r = r0; r < r1; ++r) {
+    const uint32_t nbits = need_at(r);
+    if (nbits == 0) {  // re-score mode, nothing to score here: keep the tail-bounds chain moving
+      int64_t nx_hi = my_hi;
+      if (r + 1 < r1) {
+        if (need_at(r + 1)) load_range_words(r + 1);
+        if (has_term) nx_hi = bounds[(int64_t)my_i * bstride + r + 2];
+      }
+      my_lo = my_hi;
+      my_hi = nx_hi;
+      continue;
+    }
     const int64_t d0 = (int64_t)r * kRange;
     const int64_t db = d0 + 16 * lane;
     // thresholds of the wave's queries (lanes 0..nqw-1); latency hidden behind K_d
@@ -404,12 +438,13 @@ __global__ void __launch_bounds__(kBmThreads) __attribute__((amdgpu_waves_per_eu
     }
     int64_t nx_lo = my_hi, nx_hi = my_hi;
     if (r + 1 < r1) {
-      load_range_words(r + 1);
+      if (need_at(r + 1)) load_range_words(r + 1);
       if (has_term) nx_hi = bounds[(int64_t)my_i * bstride + r + 2];
     }
     wave_lds_sync();
     const int32_t wlo = (int32_t)(db - d0), whi = wlo + 16;  // this lane's window, range-relative
     for (int qq = 0; qq < nqw; ++qq) {
+      if (!((nbits >> qq) & 1u)) continue;  // this pair keeps the tail pass's list
       const int qi = q0 + qq;
       const int base = qq * kTermLanes;
       const int L = __builtin_amdgcn_readlane(my_L, base);
@@ -555,6 +590,8 @@ __global__ void __launch_bounds__(kBmThreads) __attribute__((amdgpu_waves_per_eu
     wave_lds_sync();  // LDS slice reused by the next range
   }
 }
+
+#include "cm_bm25_prune.inc"
 
 // Dense head-term tiles: tf[h][doc] (uint8; heads never have tf >= 255) from the CSR.
 __global__ void bm25_head_fill_kernel(const int32_t *__restrict__ head_terms, int nhead,
@@ -796,6 +833,10 @@ struct cm_bm25 {
   bool empty_vocab = false;  // live docs exist but no tokens (ZeroDivisionError on search)
   DevBuf term_off, post_doc, post_tf, post_pos, dl, live, idf;
   DevBuf headtf, head_id;  // dense tf tiles for high-df terms (K2 fast path)
+  DevBuf head_maxtf, range_mindl;  // pruned search: per-(head, range) max tf, per-range min length
+  DevBuf blk_maxtf, blk_mindl;     // the same per 64-doc block
+  int32_t path = 0;                // 0 auto (pruned), 1 full K2 scan, 2 pruned
+  int32_t last_rescored = 0;       // (query, range) pairs K2 re-scored in the last host search
   int32_t nhead = 0;
   int64_t npad = 0;
   int32_t lut_dmin = 0;                  // first doc length of K2's ratio table window
@@ -915,6 +956,28 @@ int build_head_tiles(cm_bm25 *h, const std::vector<int32_t> &df) {
     CM_HIP(hipStreamSynchronize(h->stream));  // tmp is reused by later calls
   }
   h->nhead = (int32_t)cand.size();
+  // pruned-search bounds: shortest document per range, largest head tf byte per (head, range)
+  const int64_t nr = std::max<int64_t>(1, ceil_div(h->ndocs, kRange));
+  if ((rc = h->range_mindl.ensure((size_t)nr * 4))) return rc;
+  hipLaunchKernelGGL(bm25_range_mindl_kernel, dim3((unsigned)ceil_div(nr * 64, 256)), dim3(256), 0, h->stream,
+                     h->dl.as<int32_t>(), h->ndocs, (int)nr, h->range_mindl.as<int32_t>());
+  CM_HIP(hipGetLastError());
+  const int64_t nblk = nr * (kRange / 64);
+  if ((rc = h->blk_mindl.ensure((size_t)nblk * 4))) return rc;
+  hipLaunchKernelGGL(bm25_blk_mindl_kernel, dim3((unsigned)ceil_div(nblk, 256)), dim3(256), 0, h->stream,
+                     h->dl.as<int32_t>(), h->ndocs, nblk, h->blk_mindl.as<int32_t>());
+  CM_HIP(hipGetLastError());
+  if (h->nhead) {
+    if ((rc = h->head_maxtf.ensure((size_t)h->nhead * nr)) || (rc = h->blk_maxtf.ensure((size_t)h->nhead * nblk)))
+      return rc;
+    hipLaunchKernelGGL(bm25_head_max_kernel, dim3((unsigned)ceil_div((int64_t)h->nhead * nr * 64, 256)), dim3(256), 0,
+                       h->stream, h->headtf.as<uint8_t>(), h->npad, (int)nr, h->nhead, h->head_maxtf.as<uint8_t>());
+    CM_HIP(hipGetLastError());
+    hipLaunchKernelGGL(bm25_blk_max_kernel, dim3((unsigned)ceil_div((int64_t)h->nhead * nblk, 256)), dim3(256), 0,
+                       h->stream, h->headtf.as<uint8_t>(), h->npad, nblk, h->nhead, h->blk_maxtf.as<uint8_t>());
+    CM_HIP(hipGetLastError());
+  }
+  CM_HIP(hipStreamSynchronize(h->stream));
   return CM_OK;
 }
 
@@ -934,6 +997,9 @@ struct BmWs {
   int64_t *bounds;
   uint64_t *cand_key;
   uint32_t *cand_row;
+  uint8_t *need;  // [query groups][ranges] re-score bits (pruned search)
+  uint64_t *items;  // K2b work items (pruned search)
+  uint32_t *item_count;
   size_t total;
 };
 
@@ -954,6 +1020,12 @@ BmWs bm_ws_layout(const cm_bm25 *h, int nq, int total_terms, int k, void *base) 
   off += round_up((int64_t)nq * nr * k * 8, 256);
   w.cand_row = reinterpret_cast<uint32_t *>(p + off);
   off += round_up((int64_t)nq * nr * k * 4, 256);
+  w.need = reinterpret_cast<uint8_t *>(p + off);
+  off += round_up(ceil_div(std::max(nq, 1), kQPerWave) * nr, 256);
+  w.items = reinterpret_cast<uint64_t *>(p + off);  // at most one item per (query, range)
+  off += round_up((int64_t)std::max(nq, 1) * nr * 8, 256);
+  w.item_count = reinterpret_cast<uint32_t *>(p + off);
+  off += 256;
   w.total = off;
   return w;
 }
@@ -981,23 +1053,68 @@ int bm25_launch_core(cm_bm25 *h, const int32_t *q_terms_dev, const int32_t *q_of
   const int64_t nwaves = nqg * ceil_div(nr, rpw);
   const int64_t nblk = ceil_div(nwaves, kBmThreads / 64);
   if (nblk > INT32_MAX) CM_FAIL(CM_EUNSUPPORTED, "BM25 batch too large");
+  const int32_t *head_id = h->nhead ? h->head_id.as<int32_t>() : (const int32_t *)nullptr;
+  const bool prune = h->path != 1 && !(bm25_debug_flags() & 4);
   h->timer.begin(st);
+  if (prune) {
+    // K2a: exact scores of the tail candidates -> per-range lists; merged lists give each
+    // query's k-th best tail score, against which the head-only bound marks the pairs
+    // K2 must re-score (cm_bm25_prune.inc)
+    hipLaunchKernelGGL(bm25_tail_kernel<uint16_t>, dim3((unsigned)nblk), dim3(kBmThreads), 0, st, q_terms_dev,
+                       q_off_dev, nq, h->vocab, w.q_idf, w.bounds, nr, rpw, h->post_doc.as<int32_t>(),
+                       h->post_tf.as<uint16_t>(), head_id, h->headtf.as<uint8_t>(), h->npad, h->dl.as<int32_t>(),
+                       h->live.as<uint32_t>(), allow_dev, avgdl, k, w.cand_key, w.cand_row, w.thr, w.need);
+    CM_HIP(hipGetLastError());
+    hipLaunchKernelGGL(bm25_merge_kernel, dim3(nq), dim3(kMergeThreads), 0, st, w.cand_key, w.cand_row, nr, k,
+                       score_dev, row_dev);
+    CM_HIP(hipGetLastError());
+    CM_HIP(hipMemsetAsync(w.item_count, 0, 4, st));
+    hipLaunchKernelGGL(bm25_plan_kernel, dim3((unsigned)ceil_div(nqg * nr, 256)), dim3(256), 0, st, q_terms_dev,
+                       q_off_dev, nq, h->vocab, w.q_idf, head_id, h->head_maxtf.as<uint8_t>(),
+                       h->range_mindl.as<int32_t>(), h->blk_maxtf.as<uint8_t>(), h->blk_mindl.as<int32_t>(), nr,
+                       (int64_t)nr * (kRange / 64), avgdl, k, score_dev, row_dev, w.need, w.items, w.item_count);
+    CM_HIP(hipGetLastError());
+    // K2b: head-only documents of the planned blocks, merged into the tail pass's lists
+    hipLaunchKernelGGL(bm25_block_kernel, dim3(2048), dim3(256), 0, st, w.items, w.item_count, q_terms_dev,
+                       q_off_dev, h->vocab, w.q_idf, w.bounds, nr, h->post_doc.as<int32_t>(), head_id,
+                       h->headtf.as<uint8_t>(), h->npad, h->dl.as<int32_t>(), h->live.as<uint32_t>(), allow_dev,
+                       h->ndocs, avgdl, k, score_dev, w.cand_key, w.cand_row);
+    CM_HIP(hipGetLastError());
+  }
   hipLaunchKernelGGL(bm25_range_kernel<uint16_t>, dim3((unsigned)nblk), dim3(kBmThreads), 0, st, q_terms_dev,
-                     q_off_dev, nq, w.q_idf, w.bounds, nr, rpw, h->term_off.as<int64_t>(), h->post_doc.as<int32_t>(), h->post_tf.as<uint16_t>(),
-                     h->nhead ? h->head_id.as<int32_t>() : (const int32_t *)nullptr, h->headtf.as<uint8_t>(),
-                     h->npad, h->dl.as<int32_t>(), h->live.as<uint32_t>(), allow_dev, h->ndocs, avgdl, w.lut,
-                     h->lut_dmin, k, w.cand_key, w.cand_row, w.thr, bm25_debug_flags());
-  h->timer.end(st);
+                     q_off_dev, nq, w.q_idf, w.bounds, nr, rpw, h->term_off.as<int64_t>(), h->post_doc.as<int32_t>(),
+                     h->post_tf.as<uint16_t>(), head_id, h->headtf.as<uint8_t>(), h->npad, h->dl.as<int32_t>(),
+                     h->live.as<uint32_t>(), allow_dev, h->ndocs, avgdl, w.lut, h->lut_dmin, k, w.cand_key,
+                     w.cand_row, w.thr, prune ? (const uint8_t *)w.need : (const uint8_t *)nullptr, h->vocab,
+                     bm25_debug_flags());
   CM_HIP(hipGetLastError());
   hipLaunchKernelGGL(bm25_merge_kernel, dim3(nq), dim3(kMergeThreads), 0, st, w.cand_key, w.cand_row, nr, k,
                      score_dev, row_dev);
+  h->timer.end(st);
   CM_HIP(hipGetLastError());
   return CM_OK;
 }
 
+// (query, range) pairs re-scored after the tail pass by the pruned search that last used this
+// workspace: whole ranges (K2) plus ranges with planned blocks (K2b).
+int32_t count_rescored(cm_bm25 *h, int nq, const BmWs &w, hipStream_t st) {
+  const int64_t nr = std::max<int64_t>(1, ceil_div(h->ndocs, kRange));
+  const int64_t n = ceil_div(std::max(nq, 1), kQPerWave) * nr;
+  std::vector<uint8_t> v((size_t)n);
+  uint32_t items = 0;
+  if (hipMemcpyAsync(v.data(), w.need, (size_t)n, hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipMemcpyAsync(&items, w.item_count, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipStreamSynchronize(st) != hipSuccess)
+    return -1;
+  int64_t c = items;
+  for (uint8_t b : v) c += __builtin_popcount(b);
+  return (int32_t)std::min<int64_t>(c, INT32_MAX);
+}
+
 void bm25_free(cm_bm25 *h) {
   for (DevBuf *b : {&h->term_off, &h->post_doc, &h->post_tf, &h->post_pos, &h->dl, &h->live, &h->idf, &h->ws,
-                    &h->qbuf, &h->obuf, &h->allow_buf, &h->tmp, &h->headtf, &h->head_id})
+                    &h->qbuf, &h->obuf, &h->allow_buf, &h->tmp, &h->headtf, &h->head_id, &h->head_maxtf,
+                    &h->range_mindl, &h->blk_maxtf, &h->blk_mindl})
     b->release();
 }
 
@@ -1323,6 +1440,23 @@ int cm_bm25_set_head_policy(cm_bm25 *h, double min_df_frac, int64_t max_bytes) {
 
 int32_t cm_bm25_num_head_terms(cm_bm25 *h) { return h ? h->nhead : -1; }
 
+int cm_bm25_set_path(cm_bm25 *h, int32_t kind) {
+  if (!h) CM_FAIL(CM_EINVAL, "null handle");
+  if (kind < 0 || kind > 2) CM_FAIL(CM_EINVAL, "BM25 path must be 0 (auto), 1 (full scan) or 2 (pruned)");
+  h->path = kind;
+  return CM_OK;
+}
+
+int32_t cm_bm25_workspace_rescored(cm_bm25 *h, int32_t nq, int32_t total_terms, int32_t k, const void *workspace_dev) {
+  if (!h || !workspace_dev || nq <= 0 || k <= 0) return -1;
+  if (h->path == 1) return -1;
+  DeviceGuard dg(h->dev);
+  const BmWs w = bm_ws_layout(h, nq, total_terms, k, const_cast<void *>(workspace_dev));
+  return count_rescored(h, nq, w, h->stream);
+}
+
+int32_t cm_bm25_last_rescored(cm_bm25 *h) { return h ? h->last_rescored : -1; }
+
 int cm_bm25_timing(cm_bm25 *h, int32_t enable) {
   if (!h) CM_FAIL(CM_EINVAL, "null handle");
   h->timer.on = enable != 0;
@@ -1502,6 +1636,7 @@ int cm_bm25_search(cm_bm25 *h, const int32_t *q_terms, const int32_t *q_off, int
   int64_t *d_row = reinterpret_cast<int64_t *>(d_score + (size_t)nq * k);
   rc = bm25_launch_core(h, d_terms, d_off, nq, total, k, allow_dev, avgdl, w, d_score, d_row, h->stream);
   if (rc) return rc;
+  h->last_rescored = h->path == 1 ? -1 : count_rescored(h, nq, w, h->stream);
   CM_HIP(hipMemcpyAsync(out_score, d_score, (size_t)nq * k * 8, hipMemcpyDeviceToHost, h->stream));
   CM_HIP(hipMemcpyAsync(out_row, d_row, (size_t)nq * k * 8, hipMemcpyDeviceToHost, h->stream));
   CM_HIP(hipStreamSynchronize(h->stream));

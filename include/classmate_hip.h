@@ -153,6 +153,20 @@ int cm_bm25_stats(cm_bm25 *h, int64_t *n_live, int64_t *sum_len, double *avgdl, 
  * max_bytes = 0 disables.  Results are identical either way. */
 int cm_bm25_set_head_policy(cm_bm25 *h, double min_df_frac, int64_t max_bytes);
 int32_t cm_bm25_num_head_terms(cm_bm25 *h);
+/* Search strategy (results are identical on both):
+ *   CM_BM25_FULL   K2 scores every (query, 1024-doc range) pair;
+ *   CM_BM25_PRUNED K2a scores the documents holding a tail (non-head) query
+ *                  term, then K2 re-scores only the (query, range) pairs whose
+ *                  head-only score bound reaches the query's k-th best tail
+ *                  score.  0 = automatic (pruned).          */
+#define CM_BM25_FULL 1
+#define CM_BM25_PRUNED 2
+int cm_bm25_set_path(cm_bm25 *h, int32_t kind);
+/* (query, range) pairs K2 re-scored by the pruned search that last used
+ * `workspace_dev` (synchronous read; -1 on the full path or error), and the
+ * same for the last host-array cm_bm25_search on this handle.            */
+int32_t cm_bm25_workspace_rescored(cm_bm25 *h, int32_t nq, int32_t total_terms, int32_t k, const void *workspace_dev);
+int32_t cm_bm25_last_rescored(cm_bm25 *h);
 /* kernel timing (bench roofline): events around every search's K2 launch;
  * same contract as cm_dense_timing / cm_dense_timing_drain.              */
 int cm_bm25_timing(cm_bm25 *h, int32_t enable);

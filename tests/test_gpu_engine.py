@@ -183,14 +183,19 @@ def _term_ids(token_lists, vocab=None):
     return out, vocab
 
 
-def _build_bm25(eng, tok_lists):
+def _build_bm25(eng, tok_lists, path=0):
     ids, vocab = _term_ids(tok_lists)
     off = np.zeros(len(ids) + 1, np.int64)
     off[1:] = np.cumsum([len(x) for x in ids])
     flat = np.concatenate(ids) if off[-1] else np.zeros(0, np.int32)
     b = eng.BM25Index()
     b.build(flat, off, len(vocab))
+    b.set_path(path)
     return b, vocab
+
+
+# BM25 search strategies: 1 = full K2 scan, 2 = tail pass + bounded re-score (same bits)
+BM25_PATHS = [1, 2]
 
 
 FILTERS = [None, {"course": "cs101", "unit": None, "author": None, "semester": None},
@@ -198,9 +203,10 @@ FILTERS = [None, {"course": "cs101", "unit": None, "author": None, "semester": N
 
 
 @pytest.mark.parametrize("where", FILTERS)
-def test_bm25_bit_exact(eng, corpus, where):
+@pytest.mark.parametrize("path", BM25_PATHS)
+def test_bm25_bit_exact(eng, corpus, where, path):
     toks = [orc.tokenize(t, "en") for t in corpus["texts"]]
-    b, vocab = _build_bm25(eng, toks)
+    b, vocab = _build_bm25(eng, toks, path)
     ora = orc.BM25Oracle()
     ora.upsert_many(corpus["ids"], corpus["texts"], corpus["metas"])
     qs = [[vocab.get(t, -1) for t in orc.tokenize(q, "en")] for q in corpus["qtexts"]]
@@ -214,7 +220,8 @@ def test_bm25_bit_exact(eng, corpus, where):
         assert got == [[w["id"], w["score"]] for w in want]
 
 
-def test_bm25_padding_negative_eps_and_dupes(eng):
+@pytest.mark.parametrize("path", BM25_PATHS)
+def test_bm25_padding_negative_eps_and_dupes(eng, path):
     # many docs share 'common' (negative idf), few match the rest; duplicates in the query
     rng = np.random.default_rng(3)
     words = [f"w{chr(97 + i)}{chr(97 + j)}" for i in range(20) for j in range(20)]
@@ -227,7 +234,7 @@ def test_bm25_padding_negative_eps_and_dupes(eng):
             ws.append("common")
         texts.append(" ".join(ws))
     toks = [orc.tokenize(t, "en") for t in texts]
-    b, vocab = _build_bm25(eng, toks)
+    b, vocab = _build_bm25(eng, toks, path)
     ora = orc.BM25Oracle()
     ids = [f"d{i}" for i in range(len(texts))]
     ora.upsert_many(ids, texts, [{"language": "en"}] * len(texts))
@@ -327,10 +334,11 @@ def test_meanpool_l2norm(eng):
 
 
 @pytest.mark.parametrize("policy", [(1.0 / 64, 8 << 30), (0.0, 8 << 30), (1.0, 0), (0.0, 0)])
-def test_bm25_head_tile_policies_bit_exact(eng, corpus, policy):
+@pytest.mark.parametrize("path", BM25_PATHS)
+def test_bm25_head_tile_policies_bit_exact(eng, corpus, policy, path):
     """Dense head-term tiles (any split of head/tail terms) give the same bits as the oracle."""
     toks = [orc.tokenize(t, "en") for t in corpus["texts"]]
-    b, vocab = _build_bm25(eng, toks)
+    b, vocab = _build_bm25(eng, toks, path)
     b.set_head_policy(*policy)
     if policy[1] == 0:
         assert b.num_head_terms == 0
@@ -349,11 +357,12 @@ def test_bm25_head_tile_policies_bit_exact(eng, corpus, policy):
             assert got == [[w["id"], w["score"]] for w in want]
 
 
-def test_bm25_saturated_tf_slow_path(eng):
+@pytest.mark.parametrize("path", BM25_PATHS)
+def test_bm25_saturated_tf_slow_path(eng, path):
     texts = ["spam " * 300 + "eggs", "spam eggs eggs", "eggs", "spam " * 256, "ham"] * 3
     ids = [f"d{i}" for i in range(len(texts))]
     toks = [orc.tokenize(t, "en") for t in texts]
-    b, vocab = _build_bm25(eng, toks)
+    b, vocab = _build_bm25(eng, toks, path)
     b.set_head_policy(0.0, 1 << 30)               # every term in a tile -> tf 300 saturates the byte
     ora = orc.BM25Oracle()
     ora.upsert_many(ids, texts, [{"language": "en"}] * len(texts))
@@ -365,13 +374,14 @@ def test_bm25_saturated_tf_slow_path(eng):
 
 
 @pytest.mark.parametrize("policy", [(1.0 / 64, 8 << 30), (1.0, 0)])
-def test_bm25_long_queries_and_tail_overflow(eng, corpus, policy):
+@pytest.mark.parametrize("path", BM25_PATHS)
+def test_bm25_long_queries_and_tail_overflow(eng, corpus, policy, path):
     """> 96 query terms per workgroup and > 768 tail postings per range exercise
     K2's global-memory fallbacks; results stay bit-identical."""
     texts = corpus["texts"] * 3                      # 3000 docs -> ranges of 1024 docs
     ids = [f"r{i}" for i in range(len(texts))]
     toks = [orc.tokenize(t, "en") for t in texts]
-    b, vocab = _build_bm25(eng, toks)
+    b, vocab = _build_bm25(eng, toks, path)
     b.set_head_policy(*policy)
     rng = np.random.default_rng(11)
     words = list(vocab)
@@ -388,7 +398,8 @@ def test_bm25_long_queries_and_tail_overflow(eng, corpus, policy):
 
 
 @pytest.mark.parametrize("policy", [(1.0 / 64, 8 << 30), (1.0, 0)])
-def test_bm25_many_ranges_vs_c_oracle(eng, policy):
+@pytest.mark.parametrize("path", BM25_PATHS)
+def test_bm25_many_ranges_vs_c_oracle(eng, policy, path):
     """~150 ranges of 1024 docs: K2's per-query global threshold pruning and the K3
     merge must keep the exact oracle top-k (ties by row, zero-score padding for a
     rare term, k up to the 256 maximum)."""
@@ -403,6 +414,7 @@ def test_bm25_many_ranges_vs_c_oracle(eng, policy):
     b = eng.BM25Index()
     b.build(toks, off, vocab)
     b.set_head_policy(*policy)
+    b.set_path(path)
     csr = corc.build_csr(toks, off, vocab)
     idf, _ = corc.bm25_idf(csr["df"], csr["first_key"], nd)
     avgdl = float(lens.sum()) / nd
@@ -416,3 +428,49 @@ def test_bm25_many_ranges_vs_c_oracle(eng, policy):
             assert nvalid[i] == k
             assert rows[i][:k].tolist() == o_rw[i].tolist(), (k, i)
             assert scores[i][:k].tolist() == o_sc[i].tolist(), (k, i)
+
+
+@pytest.mark.gpu
+def test_bm25_pruned_skips_ranges_and_matches_full_scan(eng):
+    """Bench-shaped workload (Zipf corpus, 8-term queries drawn from documents, head tiles on):
+    the pruned search re-scores only a fraction of the (query, range) pairs and returns the
+    same bits as the full K2 scan and the C oracle, with and without an allow filter."""
+    from oracle import corc
+    rng = np.random.default_rng(21)
+    nd, vocab = 200_000, 50_000
+    lens = np.maximum(rng.poisson(60, nd), 1)
+    off = np.zeros(nd + 1, np.int64)
+    off[1:] = np.cumsum(lens)
+    p = 1.0 / np.arange(1, vocab + 1) ** 1.07
+    toks = rng.choice(vocab, size=int(off[-1]), p=p / p.sum()).astype(np.int32)
+    b = eng.BM25Index()
+    b.build(toks, off, vocab)
+    assert b.num_head_terms > 0
+    tgt = rng.integers(0, nd, 48)
+    queries = [[int(toks[off[d] + rng.integers(0, lens[d])]) for _ in range(8)] for d in tgt]
+    queries += [[0, 1, 2, 3], [5], [vocab - 1, 7]]            # head-only and rare-term queries
+    k = 10
+    csr = corc.build_csr(toks, off, vocab)
+    idf, _ = corc.bm25_idf(csr["df"], csr["first_key"], nd)
+    o_sc, o_rw = corc.bm25_topk(csr, idf, float(lens.sum()) / nd, queries, k)
+    b.set_path(1)
+    s1, r1, _ = b.search(queries, k)
+    assert b.last_rescored() == -1
+    b.set_path(2)
+    s2, r2, _ = b.search(queries, k)
+    n_pairs = ((len(queries) + 3) // 4) * 4 * ((nd + 1023) // 1024)
+    assert 0 <= b.last_rescored() < n_pairs * 0.9, (b.last_rescored(), n_pairs)
+    assert np.array_equal(r1, r2) and np.array_equal(s1, s2)
+    for i in range(len(queries)):
+        assert r2[i].tolist() == o_rw[i].tolist(), i
+        assert s2[i].tolist() == o_sc[i].tolist(), i
+    # filtered: every third document allowed (statistics recomputed over the subset)
+    mask = np.zeros(nd, bool)
+    mask[::3] = True
+    allow = _bits(mask)
+    b.set_path(1)
+    f1 = b.search(queries, k, allow)
+    b.set_path(2)
+    f2 = b.search(queries, k, allow)
+    assert np.array_equal(f1[1], f2[1]) and np.array_equal(f1[0], f2[0])
+    assert all(int(r) % 3 == 0 for r in f2[1].ravel() if r >= 0)

@@ -21,6 +21,7 @@ ap.add_argument("--batch", type=int, default=256)
 ap.add_argument("--reps", type=int, default=5)
 ap.add_argument("--head-frac", type=float, default=1.0 / 64)
 ap.add_argument("--head-bytes", type=int, default=8 << 30)
+ap.add_argument("--paths", default="1,2", help="search strategies to time (1 full K2 scan, 2 pruned)")
 a = ap.parse_args()
 tok, off = gen_tokens(a.docs, 1 << 20, 1.07, 120.0, seed=1500)
 b = engine.BM25Index()
@@ -36,15 +37,26 @@ head = qdf > a.docs * a.head_frac
 print(f"workload: mean head terms/query {head.sum(1).mean():.2f}, mean head df sum/query {(qdf * head).sum(1).mean():.4g}, "
       f"mean tail df sum/query {(qdf * ~head).sum(1).mean():.4g}, distinct head terms in batch "
       f"{len(set(qh[head].tolist()))}, head tiles {b.num_head_terms}", flush=True)
-out = b.search_dev(q_terms, q_off, 10)
-torch.cuda.synchronize()
-ts = []
-for _ in range(a.reps):
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    b.search_dev(q_terms, q_off, 10, out=out)
-    e1.record()
+ref = None
+for path in [int(x) for x in a.paths.split(",")]:
+    b.set_path(path)
+    ws = torch.empty(b.workspace_bytes(a.batch, q_terms.numel(), 10), dtype=torch.uint8, device="cuda")
+    out = b.search_dev(q_terms, q_off, 10, workspace=ws)
     torch.cuda.synchronize()
-    ts.append(e0.elapsed_time(e1))
-print(f"docs={a.docs} B={a.batch} head_terms={b.num_head_terms} dbg={os.environ.get('CM_BM25_DEBUG', '0')} "
-      f"search_ms={sorted(ts)[len(ts) // 2]:.3f} all={['%.2f' % t for t in ts]}", flush=True)
+    ts = []
+    for _ in range(a.reps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        b.search_dev(q_terms, q_off, 10, out=out, workspace=ws)
+        e1.record()
+        torch.cuda.synchronize()
+        ts.append(e0.elapsed_time(e1))
+    res = (out[0].cpu(), out[1].cpu())
+    same = "" if ref is None else f" identical_to_path{ref[2]}={bool(torch.equal(ref[0], res[0]) and torch.equal(ref[1], res[1]))}"
+    if ref is None:
+        ref = (res[0], res[1], path)
+    nr = (a.docs + 1023) // 1024
+    resc = b.workspace_rescored(a.batch, q_terms.numel(), 10, ws)
+    print(f"docs={a.docs} B={a.batch} head_terms={b.num_head_terms} path={path} dbg={os.environ.get('CM_BM25_DEBUG', '0')} "
+          f"search_ms={sorted(ts)[len(ts) // 2]:.3f} rescored={resc}/{a.batch * nr}{same} "
+          f"all={['%.2f' % t for t in ts]}", flush=True)
