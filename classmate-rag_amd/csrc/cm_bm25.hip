@@ -103,9 +103,41 @@ __device__ inline int64_t lower_bound_doc(const int32_t *__restrict__ post_doc, 
   return lo;
 }
 
+// qcand[i] = 1 iff query term i's postings are walked (K2's tail terms, K2a's candidate
+// generators): every known non-head term, and — when designate is set and a query has no such
+// term — every occurrence of its rarest head term (lowest df, then first in query order), so
+// that the pruned search has tail candidates, hence a threshold, for all-head queries too.
+__global__ void bm25_qcand_kernel(const int32_t *__restrict__ q_terms, const int32_t *__restrict__ q_off, int nq,
+                                  int32_t vocab, const int32_t *__restrict__ head_id,
+                                  const int64_t *__restrict__ term_off, int designate, uint8_t *__restrict__ qcand) {
+  const int q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= nq) return;
+  const int tb = q_off[q], te = q_off[q + 1];
+  bool any = false;
+  int32_t best_t = -1;
+  int64_t best_df = INT64_MAX;
+  for (int i = tb; i < te; ++i) {
+    const int32_t t = q_terms[i];
+    const bool valid = t >= 0 && t < vocab;
+    const bool head = valid && head_id && head_id[t] >= 0;
+    qcand[i] = (uint8_t)(valid && !head);
+    any |= valid && !head;
+    if (head) {
+      const int64_t df = term_off[t + 1] - term_off[t];
+      if (df < best_df) {
+        best_df = df;
+        best_t = t;
+      }
+    }
+  }
+  if (designate && !any && best_t >= 0)
+    for (int i = tb; i < te; ++i)
+      if (q_terms[i] == best_t) qcand[i] = 1;
+}
+
 __global__ void bm25_bounds_kernel(const int32_t *__restrict__ q_terms, int n_terms, int32_t vocab, int nr,
                                    const int64_t *__restrict__ term_off, const int32_t *__restrict__ post_doc,
-                                   const int32_t *__restrict__ head_id, int64_t *__restrict__ bounds) {
+                                   const uint8_t *__restrict__ qcand, int64_t *__restrict__ bounds) {
   const int ngroups = (nr + 1 + kBoundsGroup - 1) / kBoundsGroup;
   const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (gid >= (int64_t)n_terms * ngroups) return;
@@ -115,7 +147,7 @@ __global__ void bm25_bounds_kernel(const int32_t *__restrict__ q_terms, int n_te
   int64_t *out = bounds + (int64_t)i * (nr + 1);
   const int r0 = g * kBoundsGroup;
   const int r1 = min(r0 + kBoundsGroup, nr + 1);
-  if (t < 0 || t >= vocab || (head_id && head_id[t] >= 0)) {  // unknown or dense-tile term: no postings walk
+  if (t < 0 || t >= vocab || !qcand[i]) {  // unknown or dense-tile term: no postings walk
     for (int r = r0; r < r1; ++r) out[r] = 0;
     return;
   }
@@ -312,9 +344,12 @@ __global__ void __launch_bounds__(kBmThreads) __attribute__((amdgpu_waves_per_eu
     if (my_t >= vocab) my_t = -1;
     my_idf = q_idf[my_i];
     my_h = (my_t >= 0 && head_id) ? head_id[my_t] : -1;
-    my_lo = bounds[(int64_t)my_i * bstride + r0];
-    my_hi = bounds[(int64_t)my_i * bstride + r0 + 1];
+    if (my_h < 0) {  // a designated head term (K2a's generator) is read from its tile here
+      my_lo = bounds[(int64_t)my_i * bstride + r0];
+      my_hi = bounds[(int64_t)my_i * bstride + r0 + 1];
+    }
   }
+  const bool walk = has_term && my_h < 0;
   const uint64_t headmask = __ballot(has_term && my_t >= 0 && my_h >= 0);
   // ---- head-tile prefetch ring over the (range, scored query, head term) sequence
   auto head_at = [&](int r) -> uint64_t {
@@ -373,7 +408,7 @@ __global__ void __launch_bounds__(kBmThreads) __attribute__((amdgpu_waves_per_eu
       int64_t nx_hi = my_hi;
       if (r + 1 < r1) {
         if (need_at(r + 1)) load_range_words(r + 1);
-        if (has_term) nx_hi = bounds[(int64_t)my_i * bstride + r + 2];
+        if (walk) nx_hi = bounds[(int64_t)my_i * bstride + r + 2];
       }
       my_lo = my_hi;
       my_hi = nx_hi;
@@ -439,7 +474,7 @@ __global__ void __launch_bounds__(kBmThreads) __attribute__((amdgpu_waves_per_eu
     int64_t nx_lo = my_hi, nx_hi = my_hi;
     if (r + 1 < r1) {
       if (need_at(r + 1)) load_range_words(r + 1);
-      if (has_term) nx_hi = bounds[(int64_t)my_i * bstride + r + 2];
+      if (walk) nx_hi = bounds[(int64_t)my_i * bstride + r + 2];
     }
     wave_lds_sync();
     const int32_t wlo = (int32_t)(db - d0), whi = wlo + 16;  // this lane's window, range-relative
@@ -999,6 +1034,7 @@ struct BmWs {
   uint32_t *cand_row;
   uint8_t *need;  // [query groups][ranges] re-score bits (pruned search)
   uint64_t *items;  // K2b work items (pruned search)
+  uint8_t *qcand;   // per query term: postings walked
   uint32_t *item_count;
   size_t total;
 };
@@ -1026,6 +1062,8 @@ BmWs bm_ws_layout(const cm_bm25 *h, int nq, int total_terms, int k, void *base) 
   off += round_up((int64_t)std::max(nq, 1) * nr * 8, 256);
   w.item_count = reinterpret_cast<uint32_t *>(p + off);
   off += 256;
+  w.qcand = reinterpret_cast<uint8_t *>(p + off);
+  off += round_up(std::max(total_terms, 1), 256);
   w.total = off;
   return w;
 }
@@ -1038,10 +1076,15 @@ int bm25_launch_core(cm_bm25 *h, const int32_t *q_terms_dev, const int32_t *q_of
   if (nr > kMergePer * kMergeThreads) CM_FAIL(CM_EUNSUPPORTED, "BM25 shard too large (> 16.7M docs)");
   const int ngroups = (nr + 1 + kBoundsGroup - 1) / kBoundsGroup;
   const int64_t nb = (int64_t)total_terms * ngroups;
+  const bool prune = h->path != 1 && !(bm25_debug_flags() & 4);
   if (nb > 0) {
+    hipLaunchKernelGGL(bm25_qcand_kernel, dim3((unsigned)ceil_div(nq, 256)), dim3(256), 0, st, q_terms_dev, q_off_dev,
+                       nq, h->vocab, h->nhead ? h->head_id.as<int32_t>() : (const int32_t *)nullptr,
+                       h->term_off.as<int64_t>(), (int)prune, w.qcand);
+    CM_HIP(hipGetLastError());
     hipLaunchKernelGGL(bm25_bounds_kernel, dim3((unsigned)ceil_div(nb, 256)), dim3(256), 0, st, q_terms_dev,
-                       total_terms, h->vocab, nr, h->term_off.as<int64_t>(), h->post_doc.as<int32_t>(),
-                       h->nhead ? h->head_id.as<int32_t>() : (const int32_t *)nullptr, w.bounds);
+                       total_terms, h->vocab, nr, h->term_off.as<int64_t>(), h->post_doc.as<int32_t>(), w.qcand,
+                       w.bounds);
     CM_HIP(hipGetLastError());
   }
   CM_HIP(hipMemsetAsync(w.thr, 0xff, (size_t)nq * 8, st));  // no threshold yet
@@ -1054,7 +1097,6 @@ int bm25_launch_core(cm_bm25 *h, const int32_t *q_terms_dev, const int32_t *q_of
   const int64_t nblk = ceil_div(nwaves, kBmThreads / 64);
   if (nblk > INT32_MAX) CM_FAIL(CM_EUNSUPPORTED, "BM25 batch too large");
   const int32_t *head_id = h->nhead ? h->head_id.as<int32_t>() : (const int32_t *)nullptr;
-  const bool prune = h->path != 1 && !(bm25_debug_flags() & 4);
   h->timer.begin(st);
   if (prune) {
     // K2a: exact scores of the tail candidates -> per-range lists; merged lists give each
@@ -1063,7 +1105,7 @@ int bm25_launch_core(cm_bm25 *h, const int32_t *q_terms_dev, const int32_t *q_of
     hipLaunchKernelGGL(bm25_tail_kernel<uint16_t>, dim3((unsigned)nblk), dim3(kBmThreads), 0, st, q_terms_dev,
                        q_off_dev, nq, h->vocab, w.q_idf, w.bounds, nr, rpw, h->post_doc.as<int32_t>(),
                        h->post_tf.as<uint16_t>(), head_id, h->headtf.as<uint8_t>(), h->npad, h->dl.as<int32_t>(),
-                       h->live.as<uint32_t>(), allow_dev, avgdl, k, w.cand_key, w.cand_row, w.thr, w.need);
+                       h->live.as<uint32_t>(), allow_dev, avgdl, k, w.cand_key, w.cand_row, w.thr, w.need, w.qcand);
     CM_HIP(hipGetLastError());
     hipLaunchKernelGGL(bm25_merge_kernel, dim3(nq), dim3(kMergeThreads), 0, st, w.cand_key, w.cand_row, nr, k,
                        score_dev, row_dev);
@@ -1072,13 +1114,14 @@ int bm25_launch_core(cm_bm25 *h, const int32_t *q_terms_dev, const int32_t *q_of
     hipLaunchKernelGGL(bm25_plan_kernel, dim3((unsigned)ceil_div(nqg * nr, 256)), dim3(256), 0, st, q_terms_dev,
                        q_off_dev, nq, h->vocab, w.q_idf, head_id, h->head_maxtf.as<uint8_t>(),
                        h->range_mindl.as<int32_t>(), h->blk_maxtf.as<uint8_t>(), h->blk_mindl.as<int32_t>(), nr,
-                       (int64_t)nr * (kRange / 64), avgdl, k, score_dev, row_dev, w.need, w.items, w.item_count);
+                       (int64_t)nr * (kRange / 64), avgdl, k, score_dev, row_dev, w.need, w.items, w.item_count,
+                       w.qcand);
     CM_HIP(hipGetLastError());
     // K2b: head-only documents of the planned blocks, merged into the tail pass's lists
     hipLaunchKernelGGL(bm25_block_kernel, dim3(2048), dim3(256), 0, st, w.items, w.item_count, q_terms_dev,
                        q_off_dev, h->vocab, w.q_idf, w.bounds, nr, h->post_doc.as<int32_t>(), head_id,
                        h->headtf.as<uint8_t>(), h->npad, h->dl.as<int32_t>(), h->live.as<uint32_t>(), allow_dev,
-                       h->ndocs, avgdl, k, score_dev, w.cand_key, w.cand_row);
+                       h->ndocs, avgdl, k, score_dev, w.cand_key, w.cand_row, w.qcand);
     CM_HIP(hipGetLastError());
   }
   hipLaunchKernelGGL(bm25_range_kernel<uint16_t>, dim3((unsigned)nblk), dim3(kBmThreads), 0, st, q_terms_dev,
