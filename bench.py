@@ -8,10 +8,11 @@ embeddings and BM25 postings (vocabulary 2^20, Zipf 1.07 term draws, chunk
 length ~ Poisson(120)).  One step = one batch of B queries through the whole
 hot path, inputs resident in HBM:
 
-  E5-base query encode (PyTorch-ROCm bf16 forward, random-init weights + HIP
-  mean-pool/L2, K6) -> dense cosine top-24 over the shard (K1, fp32 MFMA)
-  -> MMR to 10 (K4) -> BM25 top-10 (K2/K3, fp64) -> [N>1: RCCL all-gather of
-  per-shard top-k + merge, pool embeddings all-reduce] -> RRF fusion (K5).
+  E5-base query encode (PyTorch-ROCm bf16 forward replayed as one hipGraph,
+  random-init weights + HIP mean-pool/L2, K6) -> dense cosine top-24 over the
+  shard (K1c) -> MMR to 10 (K4) -> [N>1: RCCL all-gather of per-shard top-k +
+  merge, pool embeddings all-reduce] -> RRF fusion (K5).  BM25 top-10 (K2a/K2b/K2,
+  fp64) runs on a second HIP stream concurrently with the encode + dense search.
 
 value = queries/s of the whole job (each query searches all N x shard chunks).
 The CPU baseline is the oracle (oracle/) run on this host on a bounded sample
@@ -61,6 +62,8 @@ def parse_args():
     ap.add_argument("--q-tokens", type=int, default=24)
     ap.add_argument("--e5-layers", type=int, default=12)
     ap.add_argument("--no-e5", action="store_true", help="use perturbed corpus rows as query embeddings")
+    ap.add_argument("--no-graph", action="store_true", help="run the E5 query encode eagerly (no hipGraph)")
+    ap.add_argument("--serial", action="store_true", help="run BM25 on the main stream (no overlap with E5 + dense)")
     ap.add_argument("--seq-len", type=int, default=256, help="ingest mode: tokens per chunk")
     ap.add_argument("--cpu-baseline", type=int, default=1)
     ap.add_argument("--cpu-queries", type=int, default=64)
@@ -176,6 +179,11 @@ def main():
         ids[:, -1] = 2
         mask = torch.ones_like(ids)
         qbuf = torch.empty((B, D), dtype=torch.float32, device=dev)
+        graph = None
+        if not args.no_graph:   # one hipGraph replay per batch instead of ~200 launches
+            g_ids, g_mask, qbuf, graph = emb.capture_graph(B, args.q_tokens)
+            g_ids.copy_(ids)
+            g_mask.copy_(mask)
     else:
         g = torch.Generator(device="cuda").manual_seed(args.seed * 17)
         qfix = torch.randn(B, D, device=dev, generator=g)
@@ -191,12 +199,33 @@ def main():
         bout = (torch.empty((B, K), dtype=torch.float64, device=dev), torch.empty((B, K), dtype=torch.int64, device=dev))
     ev = []
 
+    main = torch.cuda.current_stream(dev)
+    side = torch.cuda.Stream(device=dev) if (bm25 is not None and not args.serial) else main
+
+    def run_bm25(e):
+        # BM25 needs only the query term ids: it runs on its own stream, overlapping the E5
+        # encode and the dense search (joined before fusion)
+        with torch.cuda.stream(side):
+            if e:
+                e[2].record()
+            out = bm25.search_dev(q_terms, q_off, K, out=bout, workspace=bws)
+            if e:
+                e[3].record()
+        return out
+
     def step(record=False):
+        e = [torch.cuda.Event(enable_timing=True) for _ in range(4)] if record else None
+        if bm25 is not None:
+            side.wait_stream(main)          # previous step's fusion has read bout
+            bs, br = run_bm25(e)
         if use_e5:
-            q = emb.encode_token_ids(ids, mask, out=qbuf)
+            if graph is not None:
+                graph.replay()
+                q = qbuf
+            else:
+                q = emb.encode_token_ids(ids, mask, out=qbuf)
         else:
             q = qfix
-        e = [torch.cuda.Event(enable_timing=True) for _ in range(4)] if record else None
         if record:
             e[0].record()
         d, r = dense.search_dev(q, P, out=dout, workspace=dws)
@@ -220,11 +249,8 @@ def main():
         vk = torch.gather(rg, 1, o)
         vd = torch.gather(d, 1, o)
         vn = (order >= 0).sum(1, dtype=torch.int32)
+        main.wait_stream(side)
         if record:
-            e[2].record()
-        bs, br = bm25.search_dev(q_terms, q_off, K, out=bout, workspace=bws)
-        if record:
-            e[3].record()
             ev.append(e)
         if ws > 1:
             brg = torch.where(br >= 0, br + row0, br)
@@ -267,7 +293,7 @@ def main():
     qps = B * args.steps / elapsed
     log(f"{args.steps} steps in {elapsed:.3f}s -> {qps:.1f} q/s; dense search {search_ms:.3f} ms "
         f"(scan kernel {dense_ms:.3f} ms, {DENSE_KINDS[kind]}, {fallbacks} exact re-runs)"
-        + (f", bm25 search {bsearch_ms:.3f} ms (scoring {bm25_ms:.3f} ms, {rescored} (query, range) pairs "
+        + (f", bm25 search {bsearch_ms:.3f} ms (K2a tail pass {bm25_ms:.3f} ms, {rescored} (query, range) pairs "
            f"re-scored)" if bm25_ms is not None else ""))
 
     roofs = {"dense": _dense_roofline(kind, N, D, B, dense_ms, _pmc_traffic(args, "dense"))}
@@ -293,15 +319,14 @@ def main():
                    "query_terms": args.q_terms, "e5_query_tokens": args.q_tokens if use_e5 else None,
                    "parallelism": f"corpus-shard x{ws}"},
         "breakdown_ms": {"dense_search": search_ms, "dense_scan_kernel": dense_ms, "bm25_search": bsearch_ms,
-                         "bm25_k2_kernel": bm25_ms},
+                         "bm25_tail_kernel": bm25_ms},
         "dense_exact_reruns": fallbacks,
         "bm25_rescored_pairs": rescored,
         "roofline": roof,
         "rooflines": roofs,
     }
     if rank == 0 and ws == 1 and args.cpu_baseline and args.mode == "hybrid":
-        cpu, recall = cpu_baseline_and_recall(args, dense, bm25, res, q_terms, emb, ids if use_e5 else None,
-                                              mask if use_e5 else None, qfix if not use_e5 else None)
+        cpu, recall = cpu_baseline_and_recall(args, dense, bm25, res, q_terms, qbuf if use_e5 else qfix)
         out["cpu_baseline"] = cpu
         out["recall_at_10"] = recall
     else:
@@ -344,17 +369,25 @@ def _dense_roofline(kind, N, D, B, ms, traffic):
 
 
 def _bm25_roofline(bm25, q_terms, N, ms, traffic):
-    """K2's compulsory bytes for the batch: every distinct query term's postings read once in
-    the cheaper of its two encodings (CSR: 4 B doc + 2 B tf per posting; head tile: 1 B per
-    doc) plus the doc lengths.  K2 is latency/VALU-bound, so this fraction is low by nature."""
+    """K2a (the pruned search's tail pass, its largest kernel) per launch, algorithmic bytes:
+    every walked posting read once (4 B doc + 2 B tf) and, per posting, the candidate's doc
+    length (4 B) and one tf byte per head term of its query.  Walked terms = non-head terms, or
+    the rarest head term of a query that has none (bm25_qcand_kernel); head terms = df > N/64
+    (the default tile policy).  K2a is latency/issue-bound, so this fraction is low by nature."""
     import numpy as np
     df, _ = bm25.term_stats()
-    t = np.unique(q_terms.cpu().numpy())
-    t = t[(t >= 0) & (t < df.shape[0])]
-    bytes_ = float(np.minimum(6.0 * df[t].astype(np.float64), float(N)).sum()) + 4.0 * N
+    qt = q_terms.view(-1, 8).cpu().numpy() if q_terms.numel() % 8 == 0 else q_terms.view(1, -1).cpu().numpy()
+    bytes_ = 0.0
+    for row in qt:
+        row = row[(row >= 0) & (row < df.shape[0])]
+        d = df[row].astype(np.float64)
+        head = d > N / 64.0
+        walked = d[~head] if (~head).any() else (np.array([d[head].min()]) if head.any() else d[:0])
+        n_post = float(walked.sum())
+        bytes_ += n_post * (6.0 + 4.0 + float(head.sum()))
     r = _roof(bytes_, 0.0, 1.0, ms)
-    r.update(traffic=traffic, kernel="BM25 scoring: K2a tail pass + merge + bound + K2 re-score + merge", avg_launch_ms=ms,
-             algorithmic_per_launch=dict(bytes=bytes_, distinct_terms=int(t.shape[0]), docs=N))
+    r.update(traffic=traffic, kernel="K2a bm25_tail_kernel (pruned BM25 tail pass)", avg_launch_ms=ms,
+             algorithmic_per_launch=dict(bytes=bytes_, queries=int(qt.shape[0]), docs=N))
     return r
 
 
@@ -370,8 +403,9 @@ def _pmc_traffic(args, which):
 
 
 # ---------------------------------------------------------------------------
-def cpu_baseline_and_recall(args, dense, bm25, res, q_terms, emb, ids, mask, qfix):
-    """Time the CPU oracle on a bounded sample of the same queries over the same shard; recall@10."""
+def cpu_baseline_and_recall(args, dense, bm25, res, q_terms, q_dev):
+    """Time the CPU oracle on a bounded sample of the same queries (the step's query embeddings)
+    over the same shard; recall@10."""
     import numpy as np
     import torch
     from oracle import corc
@@ -379,9 +413,7 @@ def cpu_baseline_and_recall(args, dense, bm25, res, q_terms, emb, ids, mask, qfi
 
     Qc = min(args.cpu_queries, args.batch)
     K, P = args.k, args.pool
-    with torch.inference_mode():
-        q = emb.encode_token_ids(ids[:Qc], mask[:Qc]) if emb is not None else qfix[:Qc]
-    qh = q.float().cpu().numpy()
+    qh = q_dev[:Qc].float().cpu().numpy()
     qt = q_terms.view(args.batch, -1)[:Qc].cpu().numpy()
     gpu_keys = res[0][:Qc].cpu().numpy()
     t = time.perf_counter()

@@ -134,6 +134,34 @@ class E5MultilingualEmbedder:
             hidden = self.model(input_ids=input_ids, attention_mask=attention_mask).last_hidden_state
             return engine.meanpool_l2norm(hidden, attention_mask, self.normalize, out=out)
 
+    def capture_graph(self, batch: int, seq_len: int):
+        """HIP-graph the device encode for a fixed (batch, seq_len) (hipGraph via torch.cuda.CUDAGraph:
+        one replay instead of ~200 small launches per batch).  Returns (ids, mask, out, graph): fill
+        ids/mask in place, graph.replay() writes out (B, 768) fp32.  The 2-D mask becomes the 4-D
+        boolean attention mask inside the graph, so no host-side all-ones check runs."""
+        import torch
+        dev = next(self.model.parameters()).device
+        ids = torch.zeros((batch, seq_len), dtype=torch.long, device=dev)
+        mask = torch.ones((batch, seq_len), dtype=torch.long, device=dev)
+        out = torch.empty((batch, self.model.config.hidden_size), dtype=torch.float32, device=dev)
+
+        def fwd():
+            m4 = mask.bool()[:, None, None, :].expand(batch, 1, seq_len, seq_len)
+            hidden = self.model(input_ids=ids, attention_mask=m4).last_hidden_state
+            engine.meanpool_l2norm(hidden, mask, self.normalize, out=out)
+
+        with torch.inference_mode():
+            side = torch.cuda.Stream(device=dev)
+            side.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(side):
+                for _ in range(2):
+                    fwd()
+            torch.cuda.current_stream(dev).wait_stream(side)
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph):
+                fwd()
+        return ids, mask, out, graph
+
     def _encode(self, texts: List[str], batch_size: int = 32) -> np.ndarray:
         import torch
         if not texts:

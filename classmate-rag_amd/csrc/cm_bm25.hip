@@ -1016,7 +1016,8 @@ int build_head_tiles(cm_bm25 *h, const std::vector<int32_t> &df) {
   return CM_OK;
 }
 
-// CM_BM25_DEBUG (ablation only): bit0 skip scoring, bit1 skip the per-range top-k.
+// CM_BM25_DEBUG (ablation only): K2 bit0 skip scoring, bit1 skip the per-range top-k; bit2 full
+// scan instead of the pruned search; K2a bit4 skip candidate scoring, bit5 skip the ranking.
 int bm25_debug_flags() {
   static int f = [] {
     const char *e = getenv("CM_BM25_DEBUG");
@@ -1097,7 +1098,7 @@ int bm25_launch_core(cm_bm25 *h, const int32_t *q_terms_dev, const int32_t *q_of
   const int64_t nblk = ceil_div(nwaves, kBmThreads / 64);
   if (nblk > INT32_MAX) CM_FAIL(CM_EUNSUPPORTED, "BM25 batch too large");
   const int32_t *head_id = h->nhead ? h->head_id.as<int32_t>() : (const int32_t *)nullptr;
-  h->timer.begin(st);
+  h->timer.begin(st);  // the search's dominant scoring kernel: K2a (pruned) or K2 (full)
   if (prune) {
     // K2a: exact scores of the tail candidates -> per-range lists; merged lists give each
     // query's k-th best tail score, against which the head-only bound marks the pairs
@@ -1105,7 +1106,9 @@ int bm25_launch_core(cm_bm25 *h, const int32_t *q_terms_dev, const int32_t *q_of
     hipLaunchKernelGGL(bm25_tail_kernel<uint16_t>, dim3((unsigned)nblk), dim3(kBmThreads), 0, st, q_terms_dev,
                        q_off_dev, nq, h->vocab, w.q_idf, w.bounds, nr, rpw, h->post_doc.as<int32_t>(),
                        h->post_tf.as<uint16_t>(), head_id, h->headtf.as<uint8_t>(), h->npad, h->dl.as<int32_t>(),
-                       h->live.as<uint32_t>(), allow_dev, avgdl, k, w.cand_key, w.cand_row, w.thr, w.need, w.qcand);
+                       h->live.as<uint32_t>(), allow_dev, avgdl, k, w.cand_key, w.cand_row, w.thr, w.need, w.qcand,
+                       bm25_debug_flags());
+    h->timer.end(st);
     CM_HIP(hipGetLastError());
     hipLaunchKernelGGL(bm25_merge_kernel, dim3(nq), dim3(kMergeThreads), 0, st, w.cand_key, w.cand_row, nr, k,
                        score_dev, row_dev);
@@ -1130,10 +1133,10 @@ int bm25_launch_core(cm_bm25 *h, const int32_t *q_terms_dev, const int32_t *q_of
                      h->live.as<uint32_t>(), allow_dev, h->ndocs, avgdl, w.lut, h->lut_dmin, k, w.cand_key,
                      w.cand_row, w.thr, prune ? (const uint8_t *)w.need : (const uint8_t *)nullptr, h->vocab,
                      bm25_debug_flags());
+  if (!prune) h->timer.end(st);
   CM_HIP(hipGetLastError());
   hipLaunchKernelGGL(bm25_merge_kernel, dim3(nq), dim3(kMergeThreads), 0, st, w.cand_key, w.cand_row, nr, k,
                      score_dev, row_dev);
-  h->timer.end(st);
   CM_HIP(hipGetLastError());
   return CM_OK;
 }

@@ -149,3 +149,27 @@ def test_mmr_and_rrf_public_functions(corpus, golden):
     for case in golden["rrf"]:
         got = rrf_fuse(rank_lists=case["lists"], weights=case["weights"], rrf_k=case["rrf_k"])
         assert got == case["out"] and list(got) == list(case["out"])
+
+
+def test_e5_graph_replay_matches_eager():
+    """The hipGraph-captured query encode (bench.py's step) equals the eager device encode:
+    same E5 forward (4-D boolean mask vs 2-D mask -> same attention), same HIP pooling."""
+    import torch
+    from classmate_hip.embeddings import E5MultilingualEmbedder
+    emb = E5MultilingualEmbedder.random_init(seed=0, device="cuda", num_layers=2)
+    B, S = 16, 24
+    g = torch.Generator(device="cuda").manual_seed(5)
+    ids = torch.randint(5, 250002, (B, S), device="cuda", generator=g)
+    ids[:, 0] = 0
+    ids[:, -1] = 2
+    mask = torch.ones_like(ids)
+    mask[3, 20:] = 0                                   # ragged rows: padding is masked out
+    mask[7, 9:] = 0
+    g_ids, g_mask, g_out, graph = emb.capture_graph(B, S)
+    g_ids.copy_(ids)
+    g_mask.copy_(mask)
+    graph.replay()
+    torch.cuda.synchronize()
+    want = emb.encode_token_ids(ids, mask)
+    torch.testing.assert_close(g_out, want, atol=2e-3, rtol=0)
+    assert torch.allclose(g_out.norm(dim=1), torch.ones(B, device="cuda"), atol=1e-5)
