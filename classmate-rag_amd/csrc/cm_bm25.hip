@@ -37,7 +37,7 @@ namespace cm {
 
 constexpr int kRange = 1024;                 // docs per range (one wave's LDS score tile)
 constexpr int kBmThreads = 256;              // 4 waves = 4 queries per K2 workgroup
-constexpr int kBoundsGroup = 64;             // ranges per bounds thread (gallop between them)
+constexpr int kBoundsGroup = 8;              // ranges per bounds thread (gallop between them)
 constexpr int kMergeThreads = 1024;
 constexpr int kMergePer = 16;                // lists per merge thread -> <= 16384 ranges (16.7M docs)
 
