@@ -134,11 +134,14 @@ class E5MultilingualEmbedder:
             hidden = self.model(input_ids=input_ids, attention_mask=attention_mask).last_hidden_state
             return engine.meanpool_l2norm(hidden, attention_mask, self.normalize, out=out)
 
-    def capture_graph(self, batch: int, seq_len: int):
+    def capture_graph(self, batch: int, seq_len: int, unpadded: bool = False):
         """HIP-graph the device encode for a fixed (batch, seq_len) (hipGraph via torch.cuda.CUDAGraph:
         one replay instead of ~200 small launches per batch).  Returns (ids, mask, out, graph): fill
         ids/mask in place, graph.replay() writes out (B, 768) fp32.  The 2-D mask becomes the 4-D
-        boolean attention mask inside the graph, so no host-side all-ones check runs."""
+        boolean attention mask inside the graph, so no host-side all-ones check runs.  unpadded=True
+        (the caller guarantees every mask entry is 1) passes no mask; on transformers 5.x that makes
+        SDPA fall back to its math kernel (slower on this image: tools/e5_probe.py), so the default
+        keeps the mask."""
         import torch
         dev = next(self.model.parameters()).device
         ids = torch.zeros((batch, seq_len), dtype=torch.long, device=dev)
@@ -146,7 +149,7 @@ class E5MultilingualEmbedder:
         out = torch.empty((batch, self.model.config.hidden_size), dtype=torch.float32, device=dev)
 
         def fwd():
-            m4 = mask.bool()[:, None, None, :].expand(batch, 1, seq_len, seq_len)
+            m4 = None if unpadded else mask.bool()[:, None, None, :].expand(batch, 1, seq_len, seq_len)
             hidden = self.model(input_ids=ids, attention_mask=m4).last_hidden_state
             engine.meanpool_l2norm(hidden, mask, self.normalize, out=out)
 

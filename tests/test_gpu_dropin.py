@@ -173,3 +173,11 @@ def test_e5_graph_replay_matches_eager():
     want = emb.encode_token_ids(ids, mask)
     torch.testing.assert_close(g_out, want, atol=2e-3, rtol=0)
     assert torch.allclose(g_out.norm(dim=1), torch.ones(B, device="cuda"), atol=1e-5)
+    # unpadded batches: the maskless graph equals the eager encode
+    mask.fill_(1)
+    u_ids, u_mask, u_out, ugraph = emb.capture_graph(B, S, unpadded=True)
+    u_ids.copy_(ids)
+    u_mask.copy_(mask)
+    ugraph.replay()
+    torch.cuda.synchronize()
+    torch.testing.assert_close(u_out, emb.encode_token_ids(ids, mask), atol=2e-3, rtol=0)
