@@ -681,7 +681,7 @@ __device__ inline float coarse_err(const float *qnorm, int qi, const float *row_
 //     (range, query) candidate buffer out_keys[pass][wg][q][kCBufCap] (LDS slot counter);
 //     out_cnt[pass][wg][q] = appended count (> kCBufCap: the buffer overflowed).
 #ifndef K1C_RING
-#define K1C_RING 12
+#define K1C_RING 8
 #endif
 constexpr int kRRing = K1C_RING;  // LDS ring slots (8 KB each): kRRing - 1 chunks in flight per CU
 constexpr int kRRows = 64;      // rows per compute tile / chunk
@@ -701,7 +701,7 @@ __global__ void __launch_bounds__(256, 1)
                              const uint32_t *__restrict__ allow, int64_t n_words, const _Float16 *__restrict__ Qh,
                              int nq, const float *__restrict__ seed, int64_t rows_per_wg, int64_t rows_end, int n_wg,
                              uint64_t *__restrict__ out_keys, uint32_t *__restrict__ out_cnt,
-                             float *__restrict__ out_min) {
+                             float *__restrict__ out_min, int dbg) {
   constexpr int ld = 64 * KC;
   constexpr int KR = KC - NQL;  // register-resident query chunks
   using LL = K1rLds<NQL>;
@@ -776,10 +776,15 @@ __global__ void __launch_bounds__(256, 1)
   auto epilogue = [&](int t) __attribute__((always_inline)) {
     const int64_t row0 = r_begin + (int64_t)t * kRRows;
     const int64_t w0 = row0 >> 5;  // wave-uniform: scalar loads, outside the DMA's vmcnt queue
-    const uint32_t b0 = w0 < n_words ? (live[w0] & (allow ? allow[w0] : 0xffffffffu)) : 0u;
-    const uint32_t b1 = w0 + 1 < n_words ? (live[w0 + 1] & (allow ? allow[w0 + 1] : 0xffffffffu)) : 0u;
-    // lane (g, j) holds rows rt*16 + 4g + r: bit (16 rt + 4 g + r) of the 64-bit tile mask
-    const uint64_t tmask = ((uint64_t)b1 << 32) | b0;
+    // lane (g, j) holds rows rt*16 + 4g + r: bit (16 rt + 4 g + r) of the 64-bit tile mask.  The
+    // main scan needs it only when some row of the tile passes a seed (rare), so its two scalar
+    // loads (a full memory latency per tile) are issued on that path only
+    auto tile_mask = [&]() -> uint64_t {
+      const uint32_t b0 = w0 < n_words ? (live[w0] & (allow ? allow[w0] : 0xffffffffu)) : 0u;
+      const uint32_t b1 = w0 + 1 < n_words ? (live[w0 + 1] & (allow ? allow[w0 + 1] : 0xffffffffu)) : 0u;
+      return ((uint64_t)b1 << 32) | b0;
+    };
+    const uint64_t tmask = MINONLY ? tile_mask() : 0ull;
 #pragma unroll
     for (int qt = 0; qt < 4; ++qt) {
       if (MINONLY) {
@@ -797,6 +802,7 @@ __global__ void __launch_bounds__(256, 1)
 #pragma unroll
           for (int r = 0; r < 4; ++r) mx = fmaxf(mx, acc[rt][qt][r]);
         if (__ballot(1.0f - mx <= sd[qt]) == 0) continue;  // no row of the tile under any seed
+        const uint64_t tmask = tile_mask();
         // slots by ballot + popcount among the 4 lanes (g = 0..3) sharing query j; the count
         // lives in lane j's register (no LDS atomics: those would wait for the ring's DMAs)
         const int q = qc0 + qt * 16 + j;
@@ -828,50 +834,92 @@ __global__ void __launch_bounds__(256, 1)
   };
 
   if (total > 0) {
+    // Software-pipelined chunk loop.  Chunk gc's 32 MFMAs run in two halves (row tiles 0-1,
+    // 2-3); between them the wave waits for chunk gc+1's DMA pieces, the barrier publishes
+    // chunk gc+1 and retires every read of chunk gc's slot (each wave drains its LDS reads
+    // first), chunk gc + kRRing is issued into that slot and the row fragments 0-1 of chunk gc+1
+    // are read into the registers half 1 has just consumed; fragments 2-3 follow half 2.  Every
+    // barrier, DMA issue and LDS read thus sits behind >= 16 MFMAs instead of in front of them.
+    auto frag = [&](int gc, int rt, int sb) -> f16x8 {
+      const unsigned char *slot = lds + LL::ring + (gc % kRRing) * 8192;
+      const int row = rt * 16 + j;
+      return *reinterpret_cast<const f16x8 *>(slot + row * 128 + (((sb * 4 + g) ^ ring_swz(row)) << 4));
+    };
 #pragma unroll
     for (int p = 0; p < kRRing - 1; ++p) issue(p);
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * (kRRing - 2)) : "memory");
+    __builtin_amdgcn_s_barrier();
+    issue(kRRing - 1);
+    f16x8 xf[4][2];
+#pragma unroll
+    for (int rt = 0; rt < 4; ++rt) {
+      xf[rt][0] = frag(0, rt, 0);
+      xf[rt][1] = frag(0, rt, 1);
+    }
+    f16x8 ql[4][2];  // query fragments of an LDS-resident chunk (c >= KR)
+    if (KR == 0) {
+#pragma unroll
+      for (int qt = 0; qt < 4; ++qt)
+#pragma unroll
+        for (int sb = 0; sb < 2; ++sb)
+          ql[qt][sb] = *reinterpret_cast<const f16x8 *>(lds + LL::qf + ((0 * 4 + wave) * 8 + qt * 2 + sb) * 1024 +
+                                                        lane * 16);
+    }
     for (int t = 0; t < ntiles; ++t) {
 #pragma unroll
       for (int c = 0; c < KC; ++c) {
         const int gc = t * KC + c;
-        // chunk gc landed (this wave's part; the 2 (kRRing - 2) younger DMAs may stay in flight),
-        // then the barrier publishes every wave's part and retires all reads of slot (gc-1) % kRRing
-        // vmcnt count = 2 DMAs x (ring - 2) chunks
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * (kRRing - 2)) : "memory");
-        __builtin_amdgcn_s_barrier();
-        issue(gc + kRRing - 1);
-        const unsigned char *slot = lds + LL::ring + (gc % kRRing) * 8192;
-        auto frag = [&](int rt, int sb) -> f16x8 {
-          const int row = rt * 16 + j;
-          return *reinterpret_cast<const f16x8 *>(slot + row * 128 + (((sb * 4 + g) ^ ring_swz(row)) << 4));
-        };
-        f16x8 qv[4][2];
+        auto qv = [&](int qt, int sb) -> f16x8 { return c < KR ? qres[c < KR ? c : 0][qt][sb] : ql[qt][sb]; };
+        // half 1: row tiles 0, 1
 #pragma unroll
-        for (int qt = 0; qt < 4; ++qt)
-#pragma unroll
-          for (int sb = 0; sb < 2; ++sb)
-            qv[qt][sb] = c < KR ? qres[c < KR ? c : 0][qt][sb]
-                                : *reinterpret_cast<const f16x8 *>(
-                                      lds + LL::qf + (((c - KR) * 4 + wave) * 8 + qt * 2 + sb) * 1024 + lane * 16);
-        f16x8 xa = frag(0, 0), xb = frag(0, 1);
-#pragma unroll
-        for (int rt = 0; rt < 4; ++rt) {
-          f16x8 na = xa, nb = xb;
-          if (rt < 3) {
-            na = frag(rt + 1, 0);
-            nb = frag(rt + 1, 1);
-          }
+        for (int rt = 0; rt < 2; ++rt) {
 #pragma unroll
           for (int qt = 0; qt < 4; ++qt)
-            acc[rt][qt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xa, qv[qt][0], acc[rt][qt], 0, 0, 0);
+            acc[rt][qt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xf[rt][0], qv(qt, 0), acc[rt][qt], 0, 0, 0);
 #pragma unroll
           for (int qt = 0; qt < 4; ++qt)
-            acc[rt][qt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xb, qv[qt][1], acc[rt][qt], 0, 0, 0);
-          xa = na;
-          xb = nb;
+            acc[rt][qt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xf[rt][1], qv(qt, 1), acc[rt][qt], 0, 0, 0);
         }
+        __builtin_amdgcn_sched_barrier(0);
+        // chunk gc+1 landed (this wave's pieces: the 2 (kRRing - 2) younger DMAs may stay in
+        // flight); own LDS reads of slot gc done; the barrier makes both true for every wave
+        asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(2 * (kRRing - 2)) : "memory");
+        __builtin_amdgcn_s_barrier();
+        issue(gc + kRRing);
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt) {
+          xf[rt][0] = frag(gc + 1, rt, 0);
+          xf[rt][1] = frag(gc + 1, rt, 1);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        // half 2: row tiles 2, 3
+#pragma unroll
+        for (int rt = 2; rt < 4; ++rt) {
+#pragma unroll
+          for (int qt = 0; qt < 4; ++qt)
+            acc[rt][qt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xf[rt][0], qv(qt, 0), acc[rt][qt], 0, 0, 0);
+#pragma unroll
+          for (int qt = 0; qt < 4; ++qt)
+            acc[rt][qt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xf[rt][1], qv(qt, 1), acc[rt][qt], 0, 0, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int rt = 2; rt < 4; ++rt) {
+          xf[rt][0] = frag(gc + 1, rt, 0);
+          xf[rt][1] = frag(gc + 1, rt, 1);
+        }
+        const int cn = (c + 1) % KC;  // next chunk's query fragments, when LDS-resident
+        if (cn >= KR) {
+#pragma unroll
+          for (int qt = 0; qt < 4; ++qt)
+#pragma unroll
+            for (int sb = 0; sb < 2; ++sb)
+              ql[qt][sb] = *reinterpret_cast<const f16x8 *>(
+                  lds + LL::qf + (((cn - KR) * 4 + wave) * 8 + qt * 2 + sb) * 1024 + lane * 16);
+        }
+        __builtin_amdgcn_sched_barrier(0);
       }
-      epilogue(t);
+      if (!(dbg & 128)) epilogue(t);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // clamped tail DMAs land before the LDS is released
   }
@@ -1391,7 +1439,8 @@ int dense_grow(cm_dense *h, int64_t need_rows) {
 }
 
 // CM_DENSE_DEBUG (ablation only) for the scan kernels: bit0 skip the top-k epilogue, bit4 filter
-// without inserting survivors, bit5 (K1c) no sample pre-pass.
+// without inserting survivors, bit5 (K1c) no sample pre-pass, bit6 (K1c) no MFMAs, bit7 (K1c) no
+// per-tile epilogue.
 int dense_debug_flags() {
   static const int f = [] {
     const char *e = getenv("CM_DENSE_DEBUG");
@@ -1519,8 +1568,8 @@ int launch_split(cm_dense *h, const float *q_dev, int nq, int k, bool coarse, co
     static hipError_t err = hipSuccess;
     std::call_once(once, [] {
       const std::pair<const void *, int> fs[] = {
-          {reinterpret_cast<const void *>(&dense_coarse_scan_kernel<12, 2, false>), K1rLds<2>::total},
-          {reinterpret_cast<const void *>(&dense_coarse_scan_kernel<12, 2, true>), K1rLds<2>::total},
+          {reinterpret_cast<const void *>(&dense_coarse_scan_kernel<12, 3, false>), K1rLds<3>::total},
+          {reinterpret_cast<const void *>(&dense_coarse_scan_kernel<12, 3, true>), K1rLds<3>::total},
           {reinterpret_cast<const void *>(&dense_coarse_scan_kernel<6, 0, false>), K1rLds<0>::total},
           {reinterpret_cast<const void *>(&dense_coarse_scan_kernel<6, 0, true>), K1rLds<0>::total},
           {reinterpret_cast<const void *>(&dense_rerank_kernel), kGatherCap * 12}};
@@ -1546,14 +1595,14 @@ int launch_split(cm_dense *h, const float *q_dev, int nq, int k, bool coarse, co
     const K1cSample sm = k1c_sample(h, c);
     const bool d768 = h->ld == 768;
     auto scan = [&](bool minonly) {
-      if (d768) return minonly ? &dense_coarse_scan_kernel<12, 2, true> : &dense_coarse_scan_kernel<12, 2, false>;
+      if (d768) return minonly ? &dense_coarse_scan_kernel<12, 3, true> : &dense_coarse_scan_kernel<12, 3, false>;
       return minonly ? &dense_coarse_scan_kernel<6, 0, true> : &dense_coarse_scan_kernel<6, 0, false>;
     };
-    const size_t slds = d768 ? K1rLds<2>::total : K1rLds<0>::total;
+    const size_t slds = d768 ? K1rLds<3>::total : K1rLds<0>::total;
     // 1. sample pre-pass (per-group minima) -> seed
     hipLaunchKernelGGL(scan(true), dim3(sm.n_wg * c.n_pass), dim3(256), slds, st, h->Xh, h->live, allow, n_words,
                        w.qh, nq, (const float *)nullptr, sm.rows_per_wg, sm.rows_end, sm.n_wg, (uint64_t *)nullptr,
-                       (uint32_t *)nullptr, w.mins);
+                       (uint32_t *)nullptr, w.mins, 0);
     CM_HIP(hipGetLastError());
     hipLaunchKernelGGL(dense_seed_kernel, dim3(nq), dim3(256), 0, st, w.mins, sm.n_wg, k, nq, w.qnorm, h->rnorm,
                        h->dim, w.seed);
@@ -1561,7 +1610,8 @@ int launch_split(cm_dense *h, const float *q_dev, int nq, int k, bool coarse, co
     // 2. coarse scan: rows under the seed -> candidate buffers
     h->timer.begin(st);
     hipLaunchKernelGGL(scan(false), grid, dim3(256), slds, st, h->Xh, h->live, allow, n_words, w.qh, nq,
-                       (const float *)w.seed, c.rows_per_wg, c.rows_end, c.n_wg, w.keys, w.cnt, (float *)nullptr);
+                       (const float *)w.seed, c.rows_per_wg, c.rows_end, c.n_wg, w.keys, w.cnt, (float *)nullptr,
+                       dense_debug_flags());
     h->timer.end(st);
     CM_HIP(hipGetLastError());
     // 3. certificate + exact re-rank (failures -> fb_mask)
