@@ -887,7 +887,7 @@ __global__ void __launch_bounds__(256, 1)
         __builtin_amdgcn_s_barrier();
         issue(gc + kRRing);
 #pragma unroll
-        for (int rt = 0; rt < 2; ++rt) {
+        for (int rt = 0; rt < ((dbg & 2048) ? 0 : 2); ++rt) {  // bit 11: ablation only (stale fragments)
           xf[rt][0] = frag(gc + 1, rt, 0);
           xf[rt][1] = frag(gc + 1, rt, 1);
         }
@@ -904,7 +904,7 @@ __global__ void __launch_bounds__(256, 1)
         }
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int rt = 2; rt < 4; ++rt) {
+        for (int rt = 2; rt < ((dbg & 2048) ? 2 : 4); ++rt) {  // bit 11: ablation only (stale fragments)
           xf[rt][0] = frag(gc + 1, rt, 0);
           xf[rt][1] = frag(gc + 1, rt, 1);
         }
@@ -1440,7 +1440,8 @@ int dense_grow(cm_dense *h, int64_t need_rows) {
 
 // CM_DENSE_DEBUG (ablation only) for the scan kernels: bit0 skip the top-k epilogue, bit4 filter
 // without inserting survivors, bit5 (K1c) no sample pre-pass, bit6 (K1c) no MFMAs, bit7 (K1c) no
-// per-tile epilogue.
+// per-tile epilogue, bit9 no chunk barrier, bit10 no DMA issue, bit11 no fragment reads (K1c
+// timing ablations only: results are garbage under bits 9-11).
 int dense_debug_flags() {
   static const int f = [] {
     const char *e = getenv("CM_DENSE_DEBUG");
