@@ -884,8 +884,8 @@ __global__ void __launch_bounds__(256, 1)
         // chunk gc+1 landed (this wave's pieces: the 2 (kRRing - 2) younger DMAs may stay in
         // flight); own LDS reads of slot gc done; the barrier makes both true for every wave
         asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(2 * (kRRing - 2)) : "memory");
-        __builtin_amdgcn_s_barrier();
-        issue(gc + kRRing);
+        if (!(dbg & 512)) __builtin_amdgcn_s_barrier();  // bit 9: ablation only (races)
+        if (!(dbg & 1024)) issue(gc + kRRing);             // bit 10: ablation only (stale data)
 #pragma unroll
         for (int rt = 0; rt < ((dbg & 2048) ? 0 : 2); ++rt) {  // bit 11: ablation only (stale fragments)
           xf[rt][0] = frag(gc + 1, rt, 0);
