@@ -181,7 +181,7 @@ def main():
         qbuf = torch.empty((B, D), dtype=torch.float32, device=dev)
         graph = None
         if not args.no_graph:   # one hipGraph replay per batch instead of ~200 launches
-            g_ids, g_mask, qbuf, graph = emb.capture_graph(B, args.q_tokens)
+            g_ids, g_mask, qbuf, graph = emb.capture_graph(B, args.q_tokens, unpadded=True)  # fixed-length queries
             g_ids.copy_(ids)
             g_mask.copy_(mask)
     else:

@@ -134,23 +134,72 @@ class E5MultilingualEmbedder:
             hidden = self.model(input_ids=input_ids, attention_mask=attention_mask).last_hidden_state
             return engine.meanpool_l2norm(hidden, attention_mask, self.normalize, out=out)
 
+    def _lean_forward(self):
+        """XLM-R encoder forward for unpadded batches from this model's own weights (same math as
+        the HF module: embeddings + LayerNorm, 12 x [self-attention, residual + LayerNorm, GELU
+        MLP, residual + LayerNorm]) with the Q/K/V projections fused into one GEMM and attention
+        through unmasked SDPA (the flash kernel).  Built once; returns fwd(ids) -> hidden."""
+        import torch
+        import torch.nn.functional as F
+        if getattr(self, "_lean", None) is not None:
+            return self._lean
+        m = self.model
+        cfg = m.config
+        H = cfg.num_attention_heads
+        D = cfg.hidden_size
+        eps = cfg.layer_norm_eps
+        pad = cfg.pad_token_id
+        emb = m.embeddings
+        layers = []
+        with torch.no_grad():
+            for L in m.encoder.layer:
+                a = L.attention
+                wqkv = torch.cat([a.self.query.weight, a.self.key.weight, a.self.value.weight], 0).contiguous()
+                bqkv = torch.cat([a.self.query.bias, a.self.key.bias, a.self.value.bias], 0).contiguous()
+                layers.append((wqkv, bqkv, a.output.dense.weight, a.output.dense.bias, a.output.LayerNorm.weight,
+                               a.output.LayerNorm.bias, L.intermediate.dense.weight, L.intermediate.dense.bias,
+                               L.output.dense.weight, L.output.dense.bias, L.output.LayerNorm.weight,
+                               L.output.LayerNorm.bias))
+
+        def fwd(ids):
+            B, S = ids.shape
+            # unpadded rows: XLM-R position ids are padding_idx + 1 .. padding_idx + S
+            pos = torch.arange(pad + 1, pad + 1 + S, device=ids.device)
+            x = emb.word_embeddings(ids) + emb.position_embeddings(pos)[None] + emb.token_type_embeddings.weight[0]
+            x = F.layer_norm(x, (D,), emb.LayerNorm.weight, emb.LayerNorm.bias, eps)
+            for (wqkv, bqkv, wo, bo, g1, b1, wi, bi, w2, b2, g2, bb2) in layers:
+                qkv = F.linear(x, wqkv, bqkv).view(B, S, 3, H, D // H).permute(2, 0, 3, 1, 4)
+                o = F.scaled_dot_product_attention(qkv[0], qkv[1], qkv[2])
+                o = o.transpose(1, 2).reshape(B, S, D)
+                x = F.layer_norm(x + F.linear(o, wo, bo), (D,), g1, b1, eps)
+                h = F.gelu(F.linear(x, wi, bi))
+                x = F.layer_norm(x + F.linear(h, w2, b2), (D,), g2, bb2, eps)
+            return x
+
+        self._lean = fwd
+        return fwd
+
     def capture_graph(self, batch: int, seq_len: int, unpadded: bool = False):
         """HIP-graph the device encode for a fixed (batch, seq_len) (hipGraph via torch.cuda.CUDAGraph:
         one replay instead of ~200 small launches per batch).  Returns (ids, mask, out, graph): fill
         ids/mask in place, graph.replay() writes out (B, 768) fp32.  The 2-D mask becomes the 4-D
         boolean attention mask inside the graph, so no host-side all-ones check runs.  unpadded=True
-        (the caller guarantees every mask entry is 1) passes no mask; on transformers 5.x that makes
-        SDPA fall back to its math kernel (slower on this image: tools/e5_probe.py), so the default
-        keeps the mask."""
+        (the caller guarantees every mask entry is 1, e.g. fixed-length query batches) captures the
+        lean forward instead (_lean_forward: fused QKV GEMM, unmasked flash SDPA)."""
         import torch
         dev = next(self.model.parameters()).device
         ids = torch.zeros((batch, seq_len), dtype=torch.long, device=dev)
         mask = torch.ones((batch, seq_len), dtype=torch.long, device=dev)
         out = torch.empty((batch, self.model.config.hidden_size), dtype=torch.float32, device=dev)
 
+        lean = self._lean_forward() if unpadded else None
+
         def fwd():
-            m4 = None if unpadded else mask.bool()[:, None, None, :].expand(batch, 1, seq_len, seq_len)
-            hidden = self.model(input_ids=ids, attention_mask=m4).last_hidden_state
+            if lean is not None:
+                hidden = lean(ids)
+            else:
+                m4 = mask.bool()[:, None, None, :].expand(batch, 1, seq_len, seq_len)
+                hidden = self.model(input_ids=ids, attention_mask=m4).last_hidden_state
             engine.meanpool_l2norm(hidden, mask, self.normalize, out=out)
 
         with torch.inference_mode():
