@@ -773,15 +773,17 @@ __global__ void __launch_bounds__(256, 1)
 #pragma unroll
     for (int qt = 0; qt < 4; ++qt) acc[rt][qt] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  uint32_t tile_words = 0;  // lanes 0, 1: live & allow words of the current tile
   auto epilogue = [&](int t) __attribute__((always_inline)) {
     const int64_t row0 = r_begin + (int64_t)t * kRRows;
     const int64_t w0 = row0 >> 5;  // wave-uniform: scalar loads, outside the DMA's vmcnt queue
-    // lane (g, j) holds rows rt*16 + 4g + r: bit (16 rt + 4 g + r) of the 64-bit tile mask.  The
-    // main scan needs it only when some row of the tile passes a seed (rare), so its two scalar
-    // loads (a full memory latency per tile) are issued on that path only
+    // lane (g, j) holds rows rt*16 + 4g + r: bit (16 rt + 4 g + r) of the 64-bit tile mask, whose
+    // two words lanes 0 and 1 loaded when the tile started (tile_words: a vector load that lands
+    // during the tile's chunks instead of a scalar load waited for here)
+    (void)w0;
     auto tile_mask = [&]() -> uint64_t {
-      const uint32_t b0 = w0 < n_words ? (live[w0] & (allow ? allow[w0] : 0xffffffffu)) : 0u;
-      const uint32_t b1 = w0 + 1 < n_words ? (live[w0 + 1] & (allow ? allow[w0 + 1] : 0xffffffffu)) : 0u;
+      const uint32_t b0 = (uint32_t)__builtin_amdgcn_readlane((int)tile_words, 0);
+      const uint32_t b1 = (uint32_t)__builtin_amdgcn_readlane((int)tile_words, 1);
       return ((uint64_t)b1 << 32) | b0;
     };
     const uint64_t tmask = MINONLY ? tile_mask() : 0ull;
@@ -866,6 +868,10 @@ __global__ void __launch_bounds__(256, 1)
                                                         lane * 16);
     }
     for (int t = 0; t < ntiles; ++t) {
+      {
+        const int64_t wi = ((r_begin + (int64_t)t * kRRows) >> 5) + (lane & 1);  // lane-split: VMEM, not SMEM
+        tile_words = wi < n_words ? (live[wi] & (allow ? allow[wi] : 0xffffffffu)) : 0u;
+      }
 #pragma unroll
       for (int c = 0; c < KC; ++c) {
         const int gc = t * KC + c;
