@@ -41,7 +41,7 @@ PEAK_F32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 matrix (dense)
 PEAK_F16_MFMA_TFLOPS = 2500.0  # MI355X_MICROARCH.md: BF16/F16 matrix, dense (no sparsity)
 PEAK_HBM_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E spec
 DENSE_KINDS = {1: "K1 fp32 MFMA (dense_topk_kernel)", 2: "K1b f16x3 split planes (dense_split_kernel<2>)",
-               3: "K1c coarse f16 scan (dense_split_kernel<1>) + certified fp64 re-rank"}
+               3: "K1c dense_coarse_scan_kernel (f16 hi plane, MFMA) + certified fp64 re-rank"}
 
 
 def parse_args():
