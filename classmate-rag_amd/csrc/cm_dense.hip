@@ -656,7 +656,13 @@ __global__ void __launch_bounds__(512, 1)
   }
 }
 
-constexpr int kCQWave = 64;  // queries per wave in the resident-query scan
+// Waves per K1c workgroup.  4 (one per SIMD) is the measured best: 8 (two per SIMD, 32 queries
+// each, 256 VGPRs with 16 spilled at tile boundaries) ran 5.63 vs 4.96 ms on the 10M x 768 scan --
+// the second wave did not hide barrier/epilogue time.  Kept selectable for experiments.
+#ifndef K1C_WAVES
+#define K1C_WAVES 4
+#endif
+constexpr int kK1cWaves = K1C_WAVES;
 
 // K1c's per-query error bound E (see dense_rerank_kernel).
 __device__ inline float coarse_err(const float *qnorm, int qi, const float *row_norms, int dim) {
@@ -667,7 +673,8 @@ __device__ inline float coarse_err(const float *qnorm, int qi, const float *row_
 
 // ---------------------------------------------------------------------------
 // K1c scan (coarse f16, Xh plane only), resident-query form for ld = 64 KC.
-// 256 threads, one wave per SIMD; wave w owns queries 64w..64w+63 of the 256-query pass and
+// 64 W threads (W = kK1cWaves: 4 -> one wave per SIMD, 8 -> two, so one wave's barrier wait, DMA
+// issue and epilogue hide under the other's MFMAs); wave w owns queries 256w/W.. of the 256-query pass and
 // keeps their Qh fragments resident -- chunks 0..KC-NQL-1 in registers (32 VGPRs each), the last
 // NQL chunks in LDS -- so the corpus is the only memory stream: 64-row x 64-f16 chunks (8 KB; one
 // glds wave-instruction = 8 rows x 128 B, full lines) LDS-DMA'd into a kRRing-slot ring, retired
@@ -690,13 +697,13 @@ constexpr int kCBufCap = 64;    // candidate slots per (range, query)
 template <int NQL>
 struct K1rLds {
   static constexpr int ring = 0;
-  static constexpr int qf = ring + kRRing * 8192;          // [NQL][4 waves][8 frags][64 lanes] x 16 B
+  static constexpr int qf = ring + kRRing * 8192;          // [NQL][W waves][32/W frags][64 lanes] x 16 B
   static constexpr int total = qf + NQL * 4 * 8 * 1024;
 };
 __device__ inline int ring_swz(int row) { return (row >> 1) & 7; }
 
-template <int KC, int NQL, bool MINONLY>
-__global__ void __launch_bounds__(256, 1)
+template <int KC, int NQL, bool MINONLY, int W>
+__global__ void __launch_bounds__(64 * W, 1)
     dense_coarse_scan_kernel(const _Float16 *__restrict__ Xh, const uint32_t *__restrict__ live,
                              const uint32_t *__restrict__ allow, int64_t n_words, const _Float16 *__restrict__ Qh,
                              int nq, const float *__restrict__ seed, int64_t rows_per_wg, int64_t rows_end, int n_wg,
@@ -705,6 +712,10 @@ __global__ void __launch_bounds__(256, 1)
   constexpr int ld = 64 * KC;
   constexpr int KR = KC - NQL;  // register-resident query chunks
   using LL = K1rLds<NQL>;
+  constexpr int QT = 16 / W;        // 16-query tiles per wave
+  constexpr int NF = 2 * QT;        // query fragments per wave and chunk
+  constexpr int PCS = 8 / W;        // 16-B DMA pieces per thread and chunk
+  static_assert(W == 4 || W == 8, "K1c: 4 or 8 waves");
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -717,40 +728,41 @@ __global__ void __launch_bounds__(256, 1)
   const int64_t r_end = min(r_begin + rows_per_wg, rows_end);
   const int ntiles = r_begin < r_end ? (int)((r_end - r_begin) / kRRows) : 0;
   const int total = ntiles * KC;
-  const int qc0 = wave * kCQWave;
+  const int qc0 = wave * 16 * QT;
   const int qg0 = qp * kBQPass + qc0;
 
   // resident query fragments (B operand): lane (g, j) of q-tile qt, chunk c, half sb holds
   // q[qt*16 + j][64c + 32sb + 8g .. +7]
-  f16x8 qres[KR][4][2];
+  f16x8 qres[KR][QT][2];
   auto qsrc = [&](int c, int qt, int sb) -> const f16x8 * {
     return reinterpret_cast<const f16x8 *>(Qh + (int64_t)(qg0 + qt * 16 + j) * ld + c * 64 + sb * 32 + g * 8);
   };
 #pragma unroll
   for (int c = 0; c < KR; ++c)
 #pragma unroll
-    for (int qt = 0; qt < 4; ++qt)
+    for (int qt = 0; qt < QT; ++qt)
 #pragma unroll
       for (int sb = 0; sb < 2; ++sb) qres[c][qt][sb] = *qsrc(c, qt, sb);
 #pragma unroll
   for (int c = 0; c < NQL; ++c)
 #pragma unroll
-    for (int f = 0; f < 8; ++f)
-      *reinterpret_cast<f16x8 *>(lds + LL::qf + ((c * 4 + wave) * 8 + f) * 1024 + lane * 16) =
+    for (int f = 0; f < NF; ++f)
+      *reinterpret_cast<f16x8 *>(lds + LL::qf + ((c * W + wave) * NF + f) * 1024 + lane * 16) =
           *qsrc(KR + c, f >> 1, f & 1);
-  // per-lane seeds of the lane's 4 queries (qt*16 + j)
-  float sd[4];
+  // per-lane seeds of the lane's QT queries (qt*16 + j)
+  float sd[QT], best[QT];
+  uint32_t qcnt[QT];  // lanes g == 0: candidates appended for query qt*16 + j
 #pragma unroll
-  for (int qt = 0; qt < 4; ++qt) {
+  for (int qt = 0; qt < QT; ++qt) {
+    best[qt] = __builtin_inff();
+    qcnt[qt] = 0u;
     const int qq = qg0 + qt * 16 + j;
     sd[qt] = MINONLY ? 0.f : (qq < nq ? seed[qq] : -__builtin_inff());  // padded queries accept nothing
   }
-  float best[4] = {__builtin_inff(), __builtin_inff(), __builtin_inff(), __builtin_inff()};
-  uint32_t qcnt[4] = {0u, 0u, 0u, 0u};  // lanes g == 0: candidates appended for query qt*16 + j
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();  // LDS query fragments ready; no DMA in flight yet
 
-  // glds source of wave-instruction i (0, 1) of chunk gc: ring cell o16 = 256 i + tid holds the
+  // glds source of wave-instruction i (< PCS) of chunk gc: ring cell o16 = 64 W i + tid holds the
   // 16-B piece (row o16 >> 3, logical chunk (o16 & 7) ^ ring_swz(row)) of the tile-major plane
   auto issue = [&](int gc) __attribute__((always_inline)) {
     const int gl = min(gc, total - 1);  // clamped: one control path past the end
@@ -758,20 +770,20 @@ __global__ void __launch_bounds__(256, 1)
     const int64_t R0 = r_begin + (int64_t)t * kRRows;
     unsigned char *slot = lds + LL::ring + (gc % kRRing) * 8192;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int o16 = 256 * i + tid;
+    for (int i = 0; i < PCS; ++i) {
+      const int o16 = 64 * W * i + tid;
       const int row = o16 >> 3, lg = (o16 & 7) ^ ring_swz(row);
       const _Float16 *src = Xh + ((((R0 >> 7) * KC + c) << 13) + (((R0 & 127) + row) << 6) + lg * 8);
       __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)src,
-                                       (__attribute__((address_space(3))) void *)(slot + i * 4096 + wave * 1024), 16,
+                                       (__attribute__((address_space(3))) void *)(slot + i * W * 1024 + wave * 1024), 16,
                                        0, 0);
     }
   };
-  f32x4 acc[4][4];
+  f32x4 acc[4][QT];
 #pragma unroll
   for (int rt = 0; rt < 4; ++rt)
 #pragma unroll
-    for (int qt = 0; qt < 4; ++qt) acc[rt][qt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int qt = 0; qt < QT; ++qt) acc[rt][qt] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   uint32_t tile_words = 0;  // lanes 0, 1: live & allow words of the current tile
   auto epilogue = [&](int t) __attribute__((always_inline)) {
@@ -788,7 +800,7 @@ __global__ void __launch_bounds__(256, 1)
     };
     const uint64_t tmask = MINONLY ? tile_mask() : 0ull;
 #pragma unroll
-    for (int qt = 0; qt < 4; ++qt) {
+    for (int qt = 0; qt < QT; ++qt) {
       if (MINONLY) {
         float m = __builtin_inff();
 #pragma unroll
@@ -832,7 +844,7 @@ __global__ void __launch_bounds__(256, 1)
 #pragma unroll
     for (int rt = 0; rt < 4; ++rt)
 #pragma unroll
-      for (int qt = 0; qt < 4; ++qt) acc[rt][qt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int qt = 0; qt < QT; ++qt) acc[rt][qt] = f32x4{0.f, 0.f, 0.f, 0.f};
   };
 
   if (total > 0) {
@@ -849,7 +861,7 @@ __global__ void __launch_bounds__(256, 1)
     };
 #pragma unroll
     for (int p = 0; p < kRRing - 1; ++p) issue(p);
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * (kRRing - 2)) : "memory");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PCS * (kRRing - 2)) : "memory");
     __builtin_amdgcn_s_barrier();
     issue(kRRing - 1);
     f16x8 xf[4][2];
@@ -858,13 +870,13 @@ __global__ void __launch_bounds__(256, 1)
       xf[rt][0] = frag(0, rt, 0);
       xf[rt][1] = frag(0, rt, 1);
     }
-    f16x8 ql[4][2];  // query fragments of an LDS-resident chunk (c >= KR)
+    f16x8 ql[QT][2];  // query fragments of an LDS-resident chunk (c >= KR)
     if (KR == 0) {
 #pragma unroll
-      for (int qt = 0; qt < 4; ++qt)
+      for (int qt = 0; qt < QT; ++qt)
 #pragma unroll
         for (int sb = 0; sb < 2; ++sb)
-          ql[qt][sb] = *reinterpret_cast<const f16x8 *>(lds + LL::qf + ((0 * 4 + wave) * 8 + qt * 2 + sb) * 1024 +
+          ql[qt][sb] = *reinterpret_cast<const f16x8 *>(lds + LL::qf + ((0 * W + wave) * NF + qt * 2 + sb) * 1024 +
                                                         lane * 16);
     }
     for (int t = 0; t < ntiles; ++t) {
@@ -880,16 +892,16 @@ __global__ void __launch_bounds__(256, 1)
 #pragma unroll
         for (int rt = 0; rt < 2; ++rt) {
 #pragma unroll
-          for (int qt = 0; qt < 4; ++qt)
+          for (int qt = 0; qt < QT; ++qt)
             acc[rt][qt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xf[rt][0], qv(qt, 0), acc[rt][qt], 0, 0, 0);
 #pragma unroll
-          for (int qt = 0; qt < 4; ++qt)
+          for (int qt = 0; qt < QT; ++qt)
             acc[rt][qt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xf[rt][1], qv(qt, 1), acc[rt][qt], 0, 0, 0);
         }
         __builtin_amdgcn_sched_barrier(0);
-        // chunk gc+1 landed (this wave's pieces: the 2 (kRRing - 2) younger DMAs may stay in
+        // chunk gc+1 landed (this wave's pieces: the PCS (kRRing - 2) younger DMAs may stay in
         // flight); own LDS reads of slot gc done; the barrier makes both true for every wave
-        asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(2 * (kRRing - 2)) : "memory");
+        asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(PCS * (kRRing - 2)) : "memory");
         if (!(dbg & 512)) __builtin_amdgcn_s_barrier();  // bit 9: ablation only (races)
         if (!(dbg & 1024)) issue(gc + kRRing);             // bit 10: ablation only (stale data)
 #pragma unroll
@@ -902,10 +914,10 @@ __global__ void __launch_bounds__(256, 1)
 #pragma unroll
         for (int rt = 2; rt < 4; ++rt) {
 #pragma unroll
-          for (int qt = 0; qt < 4; ++qt)
+          for (int qt = 0; qt < QT; ++qt)
             acc[rt][qt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xf[rt][0], qv(qt, 0), acc[rt][qt], 0, 0, 0);
 #pragma unroll
-          for (int qt = 0; qt < 4; ++qt)
+          for (int qt = 0; qt < QT; ++qt)
             acc[rt][qt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xf[rt][1], qv(qt, 1), acc[rt][qt], 0, 0, 0);
         }
         __builtin_amdgcn_sched_barrier(0);
@@ -917,11 +929,11 @@ __global__ void __launch_bounds__(256, 1)
         const int cn = (c + 1) % KC;  // next chunk's query fragments, when LDS-resident
         if (cn >= KR) {
 #pragma unroll
-          for (int qt = 0; qt < 4; ++qt)
+          for (int qt = 0; qt < QT; ++qt)
 #pragma unroll
             for (int sb = 0; sb < 2; ++sb)
               ql[qt][sb] = *reinterpret_cast<const f16x8 *>(
-                  lds + LL::qf + (((cn - KR) * 4 + wave) * 8 + qt * 2 + sb) * 1024 + lane * 16);
+                  lds + LL::qf + (((cn - KR) * W + wave) * NF + qt * 2 + sb) * 1024 + lane * 16);
         }
         __builtin_amdgcn_sched_barrier(0);
       }
@@ -931,7 +943,7 @@ __global__ void __launch_bounds__(256, 1)
   }
   if (MINONLY) {
 #pragma unroll
-    for (int qt = 0; qt < 4; ++qt) {
+    for (int qt = 0; qt < QT; ++qt) {
       float m = best[qt];
       m = fminf(m, __shfl_xor(m, 16));
       m = fminf(m, __shfl_xor(m, 32));
@@ -939,7 +951,7 @@ __global__ void __launch_bounds__(256, 1)
     }
   } else if (g == 0) {
 #pragma unroll
-    for (int qt = 0; qt < 4; ++qt) out_cnt[((int64_t)qp * n_wg + wg) * kBQPass + qc0 + qt * 16 + j] = qcnt[qt];
+    for (int qt = 0; qt < QT; ++qt) out_cnt[((int64_t)qp * n_wg + wg) * kBQPass + qc0 + qt * 16 + j] = qcnt[qt];
   }
 }
 
@@ -1575,10 +1587,10 @@ int launch_split(cm_dense *h, const float *q_dev, int nq, int k, bool coarse, co
     static hipError_t err = hipSuccess;
     std::call_once(once, [] {
       const std::pair<const void *, int> fs[] = {
-          {reinterpret_cast<const void *>(&dense_coarse_scan_kernel<12, 3, false>), K1rLds<3>::total},
-          {reinterpret_cast<const void *>(&dense_coarse_scan_kernel<12, 3, true>), K1rLds<3>::total},
-          {reinterpret_cast<const void *>(&dense_coarse_scan_kernel<6, 0, false>), K1rLds<0>::total},
-          {reinterpret_cast<const void *>(&dense_coarse_scan_kernel<6, 0, true>), K1rLds<0>::total},
+          {reinterpret_cast<const void *>(&dense_coarse_scan_kernel<12, 3, false, kK1cWaves>), K1rLds<3>::total},
+          {reinterpret_cast<const void *>(&dense_coarse_scan_kernel<12, 3, true, kK1cWaves>), K1rLds<3>::total},
+          {reinterpret_cast<const void *>(&dense_coarse_scan_kernel<6, 0, false, kK1cWaves>), K1rLds<0>::total},
+          {reinterpret_cast<const void *>(&dense_coarse_scan_kernel<6, 0, true, kK1cWaves>), K1rLds<0>::total},
           {reinterpret_cast<const void *>(&dense_rerank_kernel), kGatherCap * 12}};
       for (const auto &f : fs) {
         const hipError_t e = hipFuncSetAttribute(f.first, hipFuncAttributeMaxDynamicSharedMemorySize, f.second);
@@ -1602,12 +1614,12 @@ int launch_split(cm_dense *h, const float *q_dev, int nq, int k, bool coarse, co
     const K1cSample sm = k1c_sample(h, c);
     const bool d768 = h->ld == 768;
     auto scan = [&](bool minonly) {
-      if (d768) return minonly ? &dense_coarse_scan_kernel<12, 3, true> : &dense_coarse_scan_kernel<12, 3, false>;
-      return minonly ? &dense_coarse_scan_kernel<6, 0, true> : &dense_coarse_scan_kernel<6, 0, false>;
+      if (d768) return minonly ? &dense_coarse_scan_kernel<12, 3, true, kK1cWaves> : &dense_coarse_scan_kernel<12, 3, false, kK1cWaves>;
+      return minonly ? &dense_coarse_scan_kernel<6, 0, true, kK1cWaves> : &dense_coarse_scan_kernel<6, 0, false, kK1cWaves>;
     };
     const size_t slds = d768 ? K1rLds<3>::total : K1rLds<0>::total;
     // 1. sample pre-pass (per-group minima) -> seed
-    hipLaunchKernelGGL(scan(true), dim3(sm.n_wg * c.n_pass), dim3(256), slds, st, h->Xh, h->live, allow, n_words,
+    hipLaunchKernelGGL(scan(true), dim3(sm.n_wg * c.n_pass), dim3(64 * kK1cWaves), slds, st, h->Xh, h->live, allow, n_words,
                        w.qh, nq, (const float *)nullptr, sm.rows_per_wg, sm.rows_end, sm.n_wg, (uint64_t *)nullptr,
                        (uint32_t *)nullptr, w.mins, 0);
     CM_HIP(hipGetLastError());
@@ -1616,7 +1628,7 @@ int launch_split(cm_dense *h, const float *q_dev, int nq, int k, bool coarse, co
     CM_HIP(hipGetLastError());
     // 2. coarse scan: rows under the seed -> candidate buffers
     h->timer.begin(st);
-    hipLaunchKernelGGL(scan(false), grid, dim3(256), slds, st, h->Xh, h->live, allow, n_words, w.qh, nq,
+    hipLaunchKernelGGL(scan(false), grid, dim3(64 * kK1cWaves), slds, st, h->Xh, h->live, allow, n_words, w.qh, nq,
                        (const float *)w.seed, c.rows_per_wg, c.rows_end, c.n_wg, w.keys, w.cnt, (float *)nullptr,
                        dense_debug_flags());
     h->timer.end(st);
