@@ -10,10 +10,22 @@ order (Q1), ZeroDivisionError on an all-empty vocabulary (Q7).
 
 The reference rebuilds BM25Okapi on every mutation and again per search; here
 mutations mark the device index dirty and the next search rebuilds it once.
+
+Persistence: ``save`` writes the reference's JSONL catalog
+unchanged (bm25.py:220-231) plus a binary sidecar ``<index_file>.cm/`` -- the
+CSR term ids, document offsets, vocabulary and each record's byte offset in the
+JSONL.  ``load`` checks the sidecar against the JSONL's size and mtime and, when
+it matches, builds the device index straight from the memory-mapped CSR: no JSON
+parsing, re-tokenisation or vocabulary mapping at open.  Records are parsed one
+by one when a search returns them; metadata is parsed in full only when a
+``where`` filter first needs it, and a mutation or ``save`` materializes every
+record.  A missing or stale sidecar falls back to the reference's full parse.
 """
 from __future__ import annotations
 
 import json
+import os
+import shutil
 from dataclasses import dataclass, field
 from pathlib import Path
 from typing import Any, Dict, List, Mapping, Optional, Sequence
@@ -34,18 +46,105 @@ class _Entry:
     term_ids: Optional[np.ndarray] = None
 
 
+_SIDECAR_VERSION = 1
+
+
+def _entry_of(rec: Mapping[str, Any]) -> _Entry:
+    """bm25.py:240-245: one JSONL record -> _Entry."""
+    return _Entry(id=rec["id"], text=rec.get("text", ""), tokens=list(rec.get("tokens", [])),
+                  metadata=dict(rec.get("metadata", {})))
+
+
+class _Catalog(dict):
+    """id -> _Entry, in insertion order.  Opened from a sidecar, values start as JSONL line numbers
+    and a record is parsed on first read (search results); ``values``/``items``/``materialize``
+    parse every pending record in one sequential pass."""
+
+    def __init__(self):
+        super().__init__()
+        self._src = None  # (jsonl path, line byte offsets, CSR term ids, doc offsets)
+        self._fh = None
+
+    def attach(self, path: Path, ids: Sequence[str], line_off, term_ids, doc_off) -> None:
+        self._src = (path, line_off, term_ids, doc_off)
+        for r, i in enumerate(ids):
+            dict.__setitem__(self, i, r)
+
+    @property
+    def pending(self) -> bool:
+        return self._src is not None
+
+    def _finish(self, row: int, rec: Mapping[str, Any]) -> _Entry:
+        _, _, terms, doc_off = self._src
+        e = _entry_of(rec)
+        e.term_ids = np.array(terms[int(doc_off[row]): int(doc_off[row + 1])], np.int32)
+        return e
+
+    def _parse(self, row: int) -> _Entry:
+        path, line_off = self._src[0], self._src[1]
+        if self._fh is None:
+            self._fh = open(path, "rb")
+        self._fh.seek(int(line_off[row]))
+        return self._finish(row, json.loads(self._fh.read(int(line_off[row + 1] - line_off[row]))))
+
+    def __getitem__(self, key):
+        v = dict.__getitem__(self, key)
+        if type(v) is int:
+            v = self._parse(v)
+            dict.__setitem__(self, key, v)
+        return v
+
+    def get(self, key, default=None):
+        return self[key] if key in self else default
+
+    def pop(self, key, *default):
+        v = dict.pop(self, key, *default)
+        return self._parse(v) if type(v) is int and self._src is not None else v
+
+    def materialize(self) -> None:
+        if self._src is None:
+            return
+        pending = {v: k for k, v in dict.items(self) if type(v) is int}
+        if pending:
+            with open(self._src[0], "rb") as f:
+                for row, line in enumerate(f):
+                    key = pending.get(row)
+                    if key is not None:
+                        dict.__setitem__(self, key, self._finish(row, json.loads(line)))
+        self.detach()
+
+    def detach(self) -> None:
+        if self._fh is not None:
+            self._fh.close()
+        self._src = self._fh = None
+
+    def values(self):
+        self.materialize()
+        return dict.values(self)
+
+    def items(self):
+        self.materialize()
+        return dict.items(self)
+
+    def clear(self):
+        self.detach()
+        dict.clear(self)
+
+
 @dataclass
 class BM25Store:
     index_dir: Optional[Path] = Path("./indexes/bm25")
     index_file: str = "bm25_index.jsonl"
     device: Optional[int] = None
 
-    _entries: Dict[str, _Entry] = field(default_factory=dict)
+    _entries: Dict[str, _Entry] = field(default_factory=_Catalog)
     _id_list: List[str] = field(default_factory=list)
     _vocab: Dict[str, int] = field(default_factory=dict, repr=False)
     _index: Optional[engine.BM25Index] = field(default=None, repr=False)
     _meta: MetaIndex = field(default_factory=MetaIndex, repr=False)
     _dirty: bool = field(default=True, repr=False)
+    _meta_dirty: bool = field(default=True, repr=False)
+    _csr: Optional[tuple] = field(default=None, repr=False)  # persisted (term_ids, doc_off) to build from
 
     # ---------- core ops ----------
     def _term_ids(self, tokens: Sequence[str]) -> np.ndarray:
@@ -56,12 +155,21 @@ class BM25Store:
         """bm25.py:140-145: the reference rebuilds BM25Okapi here; it raises ZeroDivisionError when
         entries exist but every token list is empty.  We check that and defer the device build."""
         self._id_list = list(self._entries.keys())
+        self._csr = None
         if self._entries and all(len(e.tokens) == 0 for e in self._entries.values()):
             raise ZeroDivisionError("float division by zero")
-        self._dirty = True
+        self._dirty = self._meta_dirty = True
 
     def _ensure_index(self) -> None:
         if not self._dirty and self._index is not None:
+            return
+        if self._index is None:
+            self._index = engine.BM25Index(device=self.device)
+        if self._csr is not None:  # opened from a sidecar: the persisted CSR is the index
+            term_ids, doc_off = self._csr
+            self._index.build(np.ascontiguousarray(term_ids), np.ascontiguousarray(doc_off),
+                              max(len(self._vocab), 1))
+            self._dirty = False
             return
         entries = [self._entries[i] for i in self._id_list]
         for e in entries:
@@ -71,13 +179,17 @@ class BM25Store:
         if entries:
             off[1:] = np.cumsum([e.term_ids.shape[0] for e in entries])
         flat = np.concatenate([e.term_ids for e in entries]) if off[-1] else np.zeros(0, np.int32)
-        if self._index is None:
-            self._index = engine.BM25Index(device=self.device)
         self._index.build(flat, off, max(len(self._vocab), 1))
-        self._meta = MetaIndex()
-        for r, e in enumerate(entries):
-            self._meta.set(r, e.metadata)
         self._dirty = False
+
+    def _ensure_meta(self) -> None:
+        """Row-aligned metadata for where-filters (parses every record of a sidecar-opened store)."""
+        if not self._meta_dirty:
+            return
+        self._meta = MetaIndex()
+        for r, i in enumerate(self._id_list):
+            self._meta.set(r, self._entries[i].metadata)
+        self._meta_dirty = False
 
     def upsert_many(self, *, ids: Sequence[str], texts: Sequence[str], metadatas: Sequence[Mapping[str, Any]]) -> None:
         """bm25.py:147-166: language from metadata (or detected), tokenize, replace in place."""
@@ -116,7 +228,11 @@ class BM25Store:
         if not live or not self._entries:
             return out
         self._ensure_index()
-        mask = self._meta.bm25_mask(where)
+        if where:
+            self._ensure_meta()
+            mask = self._meta.bm25_mask(where)
+        else:
+            mask = np.ones(len(self._id_list), bool)
         n_cand = int(mask.sum())
         if n_cand == 0:
             return out
@@ -145,28 +261,102 @@ class BM25Store:
     def index_path(self) -> Path:
         return Path(self.index_dir) / self.index_file
 
+    @property
+    def sidecar_dir(self) -> Path:
+        return Path(self.index_dir) / (self.index_file + ".cm")
+
     def save(self) -> None:
+        """bm25.py:220-231 (same JSONL records) + the binary sidecar of the device index."""
         if self.index_dir is None:
             return
         Path(self.index_dir).mkdir(parents=True, exist_ok=True)
-        with self.index_path.open("w", encoding="utf-8") as f:
-            for e in self._entries.values():
+        side = self.sidecar_dir
+        if (side / "meta.json").exists():
+            os.remove(side / "meta.json")  # the sidecar is invalid until rewritten below
+        entries = list(self._entries.values())
+        line_off = np.zeros(len(entries) + 1, np.int64)
+        doc_off = np.zeros(len(entries) + 1, np.int64)
+        parts = []
+        with self.index_path.open("wb") as f:
+            for r, e in enumerate(entries):
                 rec = {"id": e.id, "text": e.text, "tokens": e.tokens, "metadata": e.metadata}
-                f.write(json.dumps(rec, ensure_ascii=False) + "\n")
+                line = (json.dumps(rec, ensure_ascii=False) + "\n").encode("utf-8")
+                f.write(line)
+                line_off[r + 1] = line_off[r] + len(line)
+                if e.term_ids is None:
+                    e.term_ids = self._term_ids(e.tokens)
+                parts.append(e.term_ids)
+                doc_off[r + 1] = doc_off[r] + e.term_ids.shape[0]
+        st = self.index_path.stat()
+        tmp = Path(str(side) + ".tmp")
+        shutil.rmtree(tmp, ignore_errors=True)
+        tmp.mkdir(parents=True)
+        np.save(tmp / "term_ids.npy", np.concatenate(parts) if doc_off[-1] else np.zeros(0, np.int32))
+        np.save(tmp / "doc_off.npy", doc_off)
+        np.save(tmp / "line_off.npy", line_off)
+        vocab = [None] * len(self._vocab)
+        for t, i in self._vocab.items():
+            vocab[i] = t
+        (tmp / "vocab.json").write_text(json.dumps(vocab, ensure_ascii=False), encoding="utf-8")
+        (tmp / "ids.json").write_text(json.dumps([e.id for e in entries], ensure_ascii=False), encoding="utf-8")
+        (tmp / "meta.json").write_text(json.dumps({
+            "version": _SIDECAR_VERSION, "docs": len(entries), "postings": int(doc_off[-1]),
+            "jsonl_size": st.st_size, "jsonl_mtime_ns": st.st_mtime_ns}), encoding="utf-8")
+        shutil.rmtree(side, ignore_errors=True)
+        os.replace(tmp, side)
+
+    def _sidecar_valid(self) -> Optional[dict]:
+        try:
+            meta = json.loads((self.sidecar_dir / "meta.json").read_text(encoding="utf-8"))
+            st = self.index_path.stat()
+        except (OSError, ValueError):
+            return None
+        if (meta.get("version") != _SIDECAR_VERSION or meta.get("jsonl_size") != st.st_size
+                or meta.get("jsonl_mtime_ns") != st.st_mtime_ns):
+            return None
+        return meta
+
+    def _load_sidecar(self, meta: dict) -> bool:
+        side = self.sidecar_dir
+        try:
+            ids = json.loads((side / "ids.json").read_text(encoding="utf-8"))
+            vocab = json.loads((side / "vocab.json").read_text(encoding="utf-8"))
+            term_ids = np.load(side / "term_ids.npy", mmap_mode="r")
+            doc_off = np.load(side / "doc_off.npy", mmap_mode="r")
+            line_off = np.load(side / "line_off.npy", mmap_mode="r")
+        except (OSError, ValueError):
+            return False
+        n = len(ids)
+        if (n != meta["docs"] or doc_off.shape[0] != n + 1 or line_off.shape[0] != n + 1
+                or term_ids.shape[0] != int(doc_off[-1]) or len(set(ids)) != n):
+            return False
+        if n and int(doc_off[-1]) == 0:
+            raise ZeroDivisionError("float division by zero")  # bm25.py:145 on an all-empty corpus
+        cat = _Catalog()
+        cat.attach(self.index_path, ids, line_off, term_ids, doc_off)
+        self._entries = cat
+        self._vocab = {t: i for i, t in enumerate(vocab)}
+        self._id_list = list(ids)
+        self._csr = (term_ids, doc_off)
+        self._dirty = self._meta_dirty = True
+        return True
 
     def load(self) -> None:
+        """bm25.py:233-248; through the sidecar when it matches the JSONL."""
         self._entries.clear()
+        self._vocab = {}
         if self.index_dir is None or not self.index_path.exists():
             self._rebuild()
+            return
+        meta = self._sidecar_valid()
+        if meta is not None and self._load_sidecar(meta):
             return
         with self.index_path.open("r", encoding="utf-8") as f:
             for line in f:
                 if not line.strip():
                     continue
                 rec = json.loads(line)
-                self._entries[rec["id"]] = _Entry(id=rec["id"], text=rec.get("text", ""),
-                                                  tokens=list(rec.get("tokens", [])),
-                                                  metadata=dict(rec.get("metadata", {})))
+                self._entries[rec["id"]] = _entry_of(rec)
         self._rebuild()
 
     @classmethod

@@ -70,6 +70,25 @@ def test_bm25store_misc(stores, corpus, golden):
         == m["tags_contains"]
 
 
+def test_bm25store_sidecar_reload_matches_goldens(stores, corpus, golden, tmp_path):
+    """§8f-1: a store reopened through the binary sidecar (device index from the persisted CSR,
+    records parsed on demand) returns the reference's results, before and after a mutation."""
+    from classmate_hip.retrieval import BM25Store
+    _, bm, _ = stores
+    bm.index_dir = tmp_path
+    bm.save()
+    again = BM25Store.load_or_create(tmp_path)
+    assert again._entries.pending and again._csr is not None
+    for fname in FILTERS:
+        for q, want in zip(corpus["qtexts"], golden["bm25"][fname]):
+            assert [[r["id"], r["score"]] for r in again.search(query=q, where=FILTERS[fname], top_k=10)] == want
+    i0 = corpus["ids"][0]
+    again.upsert_many(ids=[i0], texts=[corpus["texts"][0]], metadatas=[corpus["metas"][0]])   # same content
+    assert again._csr is None and not again._entries.pending
+    for q, want in zip(corpus["qtexts"], golden["bm25"]["course_cs101"]):
+        assert [[r["id"], r["score"]] for r in again.search(query=q, where=FILTERS["course_cs101"], top_k=10)] == want
+
+
 @pytest.mark.parametrize("fname", list(FILTERS))
 def test_vector_store_query(stores, corpus, golden, fname):
     from classmate_hip.retrieval import build_where_filter

@@ -110,6 +110,50 @@ def test_bm25store_host_semantics(tmp_path):
     assert BM25Store(index_dir=tmp_path / "none").search(query="alpha") == []
 
 
+def test_bm25store_sidecar_roundtrip_lazy_and_stale(tmp_path):
+    """save() writes the reference JSONL + a binary sidecar; load() opens through it
+    without parsing records, falls back to the full parse when the JSONL changed."""
+    from classmate_hip.retrieval import BM25Store
+    s = BM25Store(index_dir=tmp_path)
+    texts = ["alpha beta gamma", "gamma delta", "epsilon alpha alpha", "zeta eta theta"]
+    metas = [{"language": "en", "course": c, "tags": ["x"]} for c in ("c1", "c2", "c1", None)]
+    s.upsert_many(ids=[f"d{i}" for i in range(4)], texts=texts, metadatas=metas)
+    s.delete_many(["d1"])
+    s.save()
+    side = tmp_path / "bm25_index.jsonl.cm"
+    assert sorted(p.name for p in side.iterdir()) == ["doc_off.npy", "ids.json", "line_off.npy", "meta.json",
+                                                       "term_ids.npy", "vocab.json"]
+    s2 = BM25Store.load_or_create(tmp_path)
+    assert s2._entries.pending and s2._csr is not None and s2._id_list == ["d0", "d2", "d3"]
+    assert s2._csr[1].tolist() == [0, 3, 6, 9]
+    e = s2._entries["d2"]                                    # parsed on demand from its byte range
+    assert (e.id, e.text, e.tokens, e.metadata) == ("d2", texts[2], ["epsilon", "alpha", "alpha"], metas[2])
+    assert [s2._vocab.get(t) for t in e.tokens] == e.term_ids.tolist()
+    assert dict.__getitem__(s2._entries, "d3") == 2           # still a line number: nothing else parsed
+    ref = {i: (x.text, x.tokens, x.metadata) for i, x in s._entries.items()}
+    assert {i: (x.text, x.tokens, x.metadata) for i, x in s2._entries.items()} == ref   # materializes
+    assert not s2._entries.pending
+    # mutation after a sidecar open: ids keep their order, vocab ids stay consistent
+    s3 = BM25Store.load_or_create(tmp_path)
+    s3.upsert_many(ids=["d4"], texts=["alpha omega"], metadatas=[{"language": "en"}])
+    assert s3._id_list == ["d0", "d2", "d3", "d4"] and s3._csr is None
+    for x in s3._entries.values():
+        ids = x.term_ids if x.term_ids is not None else s3._term_ids(x.tokens)
+        assert [s3._vocab[t] for t in x.tokens] == list(ids)
+    s3.save()
+    assert BM25Store.load_or_create(tmp_path)._id_list == ["d0", "d2", "d3", "d4"]
+    # a JSONL edited behind the sidecar's back: stale -> reference full parse
+    with (tmp_path / "bm25_index.jsonl").open("a", encoding="utf-8") as f:
+        f.write(json.dumps({"id": "d9", "text": "late", "tokens": ["late"], "metadata": {}}) + "\n")
+    s4 = BM25Store.load_or_create(tmp_path)
+    assert not s4._entries.pending and s4._csr is None and s4._id_list[-1] == "d9"
+    # a corrupt sidecar is ignored too
+    s3.save()
+    (side / "ids.json").write_text("[1, 2", encoding="utf-8")
+    s5 = BM25Store.load_or_create(tmp_path)
+    assert not s5._entries.pending and len(s5._id_list) == 4
+
+
 def test_rrf_weights_error_before_device():
     from classmate_hip.retrieval import rrf_fuse
     with pytest.raises(ValueError):
