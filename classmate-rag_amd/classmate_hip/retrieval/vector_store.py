@@ -5,7 +5,19 @@ Same constructor, methods and return shapes as rag/retrieval/vector_chroma.py:81
 the Chroma client + HNSW server is replaced by ``engine.DenseIndex`` (exact
 brute-force cosine on the GPU, kernel K1).  Extra, build-side: ``query_batch``
 (many query rows at once — the reference returns row 0 only, quirk Q6),
-``save``/``load`` persistence under ``persist_dir/collection_name``.
+persistence under ``persist_dir/collection_name`` (replacing the
+Chroma persistent dir):
+
+* ``vectors.f32`` -- row-aligned fp32 rows (row r at byte r * dim * 4), written in
+  place through a memory map; the load streams it to HBM in 64k-row slabs;
+* ``rows.log.jsonl`` -- an append-only log of ``{"row", "id", "document",
+  "metadata"}`` records (``"id": null`` = tombstone), replayed on load, last
+  record per row wins;
+* ``meta.json`` -- ``{"format", "dim", "rows"}``, rewritten after every append.
+
+With ``autosave`` (the reference persists every ``upsert``/``delete``) a call
+writes only its own rows and log records: O(batch), not O(collection).
+``save()`` writes everything from the device copy and compacts the log.
 
 String ids, documents and metadata stay on the host; rows are assigned in
 insertion order and re-upserting an id overwrites its row in place.
@@ -23,6 +35,9 @@ import numpy as np
 
 from .. import engine
 from .filters import MetaIndex, pack_bits
+
+
+_FORMAT = 2
 
 
 @dataclass
@@ -56,46 +71,90 @@ class GpuVectorStore:
             return
         self._loaded = True
         d = self._dir
-        if d is not None and (d / "rows.jsonl").exists() and (d / "vectors.npy").exists():
+        if d is not None and (d / "meta.json").exists():
             self._load_from(d)
 
     def _load_from(self, d: Path):
-        vecs = np.load(d / "vectors.npy", mmap_mode="r")
-        rows = []
-        with (d / "rows.jsonl").open("r", encoding="utf-8") as f:
+        meta = json.loads((d / "meta.json").read_text(encoding="utf-8"))
+        if meta.get("format") != _FORMAT:
+            raise ValueError(f"{d}: unsupported vector store format {meta.get('format')!r}")
+        dim, n = int(meta["dim"]), int(meta["rows"])
+        recs: Dict[int, Mapping[str, Any]] = {}
+        with (d / "rows.log.jsonl").open("r", encoding="utf-8") as f:
             for line in f:
                 if line.strip():
-                    rows.append(json.loads(line))
-        live = [i for i, r in enumerate(rows) if r.get("id") is not None]
-        self._index = engine.DenseIndex(int(vecs.shape[1]), device=self.device, capacity=len(rows))
-        for i, r in enumerate(rows):
-            self._ids.append(r.get("id"))
-            self._docs.append(r.get("document"))
-            if r.get("id") is not None:
-                self._row[r["id"]] = i
-                self._meta.set(i, r.get("metadata"))
+                    rec = json.loads(line)
+                    if rec["row"] < n:   # records past meta.rows belong to an interrupted append
+                        recs[rec["row"]] = rec
+        vecs = np.memmap(d / "vectors.f32", dtype=np.float32, mode="r", shape=(n, dim)) if n else None
+        self._index = engine.DenseIndex(dim, device=self.device, capacity=max(n, 1))
+        live = []
+        for r in range(n):
+            rec = recs.get(r)
+            _id = rec.get("id") if rec else None
+            self._ids.append(_id)
+            self._docs.append(rec.get("document") if _id is not None else None)
+            if _id is not None:
+                self._row[_id] = r
+                self._meta.set(r, rec.get("metadata"))
+                live.append(r)
         if live:
             idx = np.asarray(live, np.int64)
             for s in range(0, idx.shape[0], 1 << 16):
                 part = idx[s: s + (1 << 16)]
                 self._index.upsert(np.asarray(vecs[part], np.float32), part)
+        del vecs
+
+    def _record(self, r: int) -> str:
+        _id = self._ids[r]
+        rec = {"row": r, "id": _id, "document": self._docs[r] if _id is not None else None,
+               "metadata": (self._meta.metas[r] if r < len(self._meta.metas) else None) if _id is not None else None}
+        return json.dumps(rec, ensure_ascii=False) + "\n"
+
+    def _write_meta(self, d: Path):
+        tmp = d / "meta.tmp.json"
+        tmp.write_text(json.dumps({"format": _FORMAT, "dim": self._index.dim, "rows": len(self._ids)}),
+                       encoding="utf-8")
+        os.replace(tmp, d / "meta.json")
+
+    def _append(self, rows: np.ndarray, emb: Optional[np.ndarray]):
+        """Autosave of one upsert (emb given) or delete: its rows' vectors and log records only."""
+        d = self._dir
+        if d is None or self._index is None:
+            return
+        if not (d / "meta.json").exists():   # first write of this collection: the full layout
+            self.save()
+            return
+        if emb is not None:
+            n, dim = len(self._ids), self._index.dim
+            with open(d / "vectors.f32", "r+b") as f:
+                if f.seek(0, 2) < n * dim * 4:
+                    f.truncate(n * dim * 4)
+            mm = np.memmap(d / "vectors.f32", dtype=np.float32, mode="r+", shape=(n, dim))
+            mm[rows] = emb
+            mm.flush()
+            del mm
+        with (d / "rows.log.jsonl").open("a", encoding="utf-8") as f:
+            f.write("".join(self._record(int(r)) for r in rows))
+        self._write_meta(d)
 
     def save(self):
-        """Write vectors.npy (row-aligned fp32) + rows.jsonl ({id, document, metadata} or nulls)."""
+        """Full write from the device copy + a compacted log (one record per row)."""
         d = self._dir
         if d is None or self._index is None:
             return
         d.mkdir(parents=True, exist_ok=True)
-        vecs = self._index.export()
-        tmp = d / "vectors.tmp.npy"
-        np.save(tmp, vecs)
-        os.replace(tmp, d / "vectors.npy")
+        if (d / "meta.json").exists():
+            os.remove(d / "meta.json")    # invalid until the rewrite below completes
+        vecs = np.ascontiguousarray(self._index.export(), np.float32)
+        with open(d / "vectors.tmp.f32", "wb") as f:
+            f.write(vecs[: len(self._ids)].tobytes())
+        os.replace(d / "vectors.tmp.f32", d / "vectors.f32")
         with (d / "rows.tmp.jsonl").open("w", encoding="utf-8") as f:
-            for i, _id in enumerate(self._ids):
-                rec = {"id": _id, "document": self._docs[i] if _id is not None else None,
-                       "metadata": (self._meta.metas[i] if i < len(self._meta.metas) else None) if _id else None}
-                f.write(json.dumps(rec, ensure_ascii=False) + "\n")
-        os.replace(d / "rows.tmp.jsonl", d / "rows.jsonl")
+            for r in range(len(self._ids)):
+                f.write(self._record(r))
+        os.replace(d / "rows.tmp.jsonl", d / "rows.log.jsonl")
+        self._write_meta(d)
 
     # ---- upsert (vector_chroma.py:168-200) ---------------------------------
     def upsert(self, *, ids: Sequence[str], documents: Sequence[str], metadatas: Sequence[Mapping[str, Any]],
@@ -128,7 +187,7 @@ class GpuVectorStore:
             self._meta.set(r, metadatas[i])
         self._index.upsert(emb, rows)
         if self.autosave:
-            self.save()
+            self._append(rows, emb)
 
     def delete(self, ids: Sequence[str]) -> None:
         """col.delete(ids=...) (vector_chroma.py:181-187); unknown ids are ignored."""
@@ -142,7 +201,7 @@ class GpuVectorStore:
             self._meta.remove(r)
         self._index.delete(np.asarray(rows, np.int64))
         if self.autosave:
-            self.save()
+            self._append(np.asarray(rows, np.int64), None)
 
     # ---- query (vector_chroma.py:204-253) ------------------------------------
     def _search(self, q: np.ndarray, where, top_k: int, include_embeddings: bool):

@@ -119,6 +119,34 @@ def test_vector_store_persistence_and_delete(stores, corpus):
     assert again.count() == 0
 
 
+def test_vector_store_incremental_log(corpus, tmp_path):
+    """§8f-1: autosave appends only the call's rows (vectors in place + log records, tombstones for
+    deletes); a reload replays the log; save() compacts it to one record per row."""
+    import json
+    from classmate_hip.retrieval import GpuVectorStore
+    ids, emb = corpus["ids"][:300], corpus["emb"][:300]
+    vs = GpuVectorStore(persist_dir=tmp_path)
+    vs.upsert(ids=ids[:200], documents=corpus["texts"][:200], metadatas=corpus["metas"][:200], embeddings=emb[:200])
+    vs.upsert(ids=ids[150:300], documents=["new"] * 150, metadatas=corpus["metas"][150:300], embeddings=emb[150:300])
+    vs.delete(ids[:10])
+    d = tmp_path / "classmate_rag"
+    log = (d / "rows.log.jsonl").read_text().splitlines()
+    assert len(log) == 200 + 150 + 10 and json.loads(log[-1])["id"] is None
+    assert (d / "vectors.f32").stat().st_size == 300 * emb.shape[1] * 4
+    again = GpuVectorStore(persist_dir=tmp_path)
+    assert again.count() == 290
+    q = corpus["qvecs"][0]
+    a = vs.query(query_embeddings=q, top_k=20, include_embeddings=True)
+    b = again.query(query_embeddings=q, top_k=20, include_embeddings=True)
+    assert [(r["id"], r["document"], r["metadata"]) for r in a] == [(r["id"], r["document"], r["metadata"]) for r in b]
+    assert all(np.array_equal(x["embedding"], y["embedding"]) for x, y in zip(a, b))
+    assert {r["document"] for r in b if r["id"] in ids[200:]} <= {"new"}
+    again.save()
+    assert len((d / "rows.log.jsonl").read_text().splitlines()) == 300
+    third = GpuVectorStore(persist_dir=tmp_path)
+    assert [r["id"] for r in third.query(query_embeddings=q, top_k=20)] == [r["id"] for r in a]
+
+
 def _rows(res):
     return [[r["id"], r["scores"]["fused"], r["scores"]["vector_distance"], r["scores"]["bm25_score"]] for r in res]
 
