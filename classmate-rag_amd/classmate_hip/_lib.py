@@ -23,6 +23,8 @@ LIB_NAME = "libclassmate_hip.so"
 LIB_PATH = Path(os.environ.get("CLASSMATE_HIP_LIB", Path(__file__).with_name(LIB_NAME)))
 
 CM_OK, CM_EINVAL, CM_ENOMEM, CM_EDEVICE, CM_EZERODIV, CM_EUNSUPPORTED = 0, -1, -2, -3, -4, -5
+CM_FOP_EQ, CM_FOP_NE, CM_FOP_BITS, CM_FOP_TRUE, CM_FOP_FALSE, CM_FOP_AND, CM_FOP_OR, CM_FOP_NOT = range(1, 9)
+CM_FILTER_MAX_OPS, CM_FILTER_MAX_SOURCES = 64, 16
 CM_DTYPE_F32, CM_DTYPE_BF16, CM_DTYPE_F16, CM_DTYPE_I32, CM_DTYPE_I64 = 0, 1, 2, 3, 4
 
 if not LIB_PATH.exists():
@@ -99,6 +101,7 @@ SIGNATURES = {
                      c_vp, c_vp, c_vp, c_vp, c_vp, c_vp),
     "cm_rrf_merge_dev": (c_int, c_vp, c_vp, c_vp, c_i32, c_vp, c_vp, c_vp, c_i32, c_i32, c_f64, c_f64, c_i32, c_i32,
                          c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp),
+    "cm_filter_eval": (c_int, c_vp, c_i32, c_vp, c_i32, c_vp, c_i32, c_i64, c_vp, c_vp, c_vp),
     "cm_meanpool_l2norm": (c_int, c_vp, c_i32, c_vp, c_i32, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp),
 }
 

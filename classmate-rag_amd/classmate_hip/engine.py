@@ -113,8 +113,8 @@ class DenseIndex:
         rows = np.empty((nq, k), np.int64)
         vecs = np.empty((nq, k, self.dim), np.float32) if return_vectors else None
         ab = None
-        if allow_bits is not None:
-            ab = _c(allow_bits, np.uint32)
+        if allow_bits is not None:  # host words, or a device tensor from filter_bits
+            ab = allow_bits if hasattr(allow_bits, "data_ptr") else _c(allow_bits, np.uint32)
             need = (self.size + 31) // 32
             if ab.shape[0] < need:
                 raise ValueError(f"allow bitmap has {ab.shape[0]} words, need {need}")
@@ -318,7 +318,11 @@ class BM25Index:
         scores = np.empty((nq, k), np.float64)
         rows = np.empty((nq, k), np.int64)
         nvalid = np.empty(nq, np.int32)
-        ab = None if allow_bits is None else _c(allow_bits, np.uint32)
+        ab = None  # host words, or a device tensor from filter_bits
+        if allow_bits is not None:
+            ab = allow_bits if hasattr(allow_bits, "data_ptr") else _c(allow_bits, np.uint32)
+            if ab.shape[0] < (self.num_docs + 31) // 32:
+                raise ValueError(f"allow bitmap has {ab.shape[0]} words, need {(self.num_docs + 31) // 32}")
         L.check(L.fn["cm_bm25_search"](self._h, L.ptr(flat), L.ptr(off), nq, int(k), L.ptr(ab), L.ptr(scores),
                                        L.ptr(rows), L.ptr(nvalid)), "cm_bm25_search")
         return scores, rows, nvalid
@@ -441,3 +445,55 @@ def meanpool_l2norm(hidden, mask, normalize: bool = True, out=None):
     L.check(L.fn["cm_meanpool_l2norm"](L.ptr(hidden), hd, L.ptr(mask), md, B, S, D, int(bool(normalize)),
                                        L.ptr(out), _stream(hidden.device.index)), "cm_meanpool_l2norm")
     return out
+
+
+# ---------------------------------------------------------------------------
+# Where-filters on the device: retrieval.filters compiles, cm_filter_eval runs.
+def filter_bits(prog, device: Optional[int] = None):
+    """Run a compiled ``FilterProgram`` in HBM -> (allow words as a device int32 tensor, set bits).
+
+    The MetaIndex's code columns and live bits are copied to the device once per metadata
+    version and reused by every later filter; host-evaluated leaves are uploaded per call.
+    """
+    from .retrieval.filters import pack_bits
+    device = default_device() if device is None else int(device)
+    meta, n = prog.meta, prog.n
+    dev = torch.device("cuda", device)
+    cache = meta._dev_cache
+    if cache is None or (cache["version"], cache["n"], cache["device"]) != (meta.version, n, device):
+        cache = meta._dev_cache = {"version": meta.version, "n": n, "device": device, "cols": {}, "live": None}
+    cols = []
+    for slot, ck in enumerate(prog.cols):
+        t = cache["cols"].get(ck)
+        if t is None:
+            t = cache["cols"][ck] = torch.from_numpy(np.ascontiguousarray(prog.column(slot))).to(dev)
+        cols.append(t)
+    bits = []
+    for b in prog.bits:
+        if isinstance(b, str):  # "live"
+            if cache["live"] is None:
+                cache["live"] = torch.from_numpy(pack_bits(meta.live[:n]).view(np.int32)).to(dev)
+            bits.append(cache["live"])
+        else:
+            bits.append(torch.from_numpy(pack_bits(b).view(np.int32)).to(dev))
+    nw = max((n + 31) // 32, 1)
+    out = torch.zeros(nw, dtype=torch.int32, device=dev) if n == 0 else torch.empty(nw, dtype=torch.int32, device=dev)
+    cnt = torch.empty(1, dtype=torch.int64, device=dev)
+    ops = np.ascontiguousarray(np.asarray(prog.ops, np.int32).reshape(-1))
+    col_p = (C.c_void_p * max(len(cols), 1))(*[t.data_ptr() for t in cols])
+    bit_p = (C.c_void_p * max(len(bits), 1))(*[t.data_ptr() for t in bits])
+    L.check(L.fn["cm_filter_eval"](L.ptr(ops), len(prog.ops), col_p, len(cols), bit_p, len(bits), int(n),
+                                   out.data_ptr(), cnt.data_ptr(), _stream(device)), "cm_filter_eval")
+    return out, int(cnt.item())  # .item() orders the handle-stream searches after the kernel
+
+
+def where_bits(meta, where, semantics: str, device: Optional[int] = None):
+    """Allow bitmap + candidate count of ``where`` under "bm25" (rag/retrieval/bm25.py:79-107) or
+    "chroma" semantics: the compiled program on the device; a program over the kernel's limits
+    (e.g. a 40-value $in) is evaluated by the MetaIndex in numpy and uploaded as host words."""
+    from .retrieval.filters import pack_bits
+    prog = meta.bm25_program(where) if semantics == "bm25" else meta.chroma_program(where)
+    if prog.fits_device:
+        return filter_bits(prog, device)
+    mask = meta.bm25_mask(where) if semantics == "bm25" else meta.chroma_mask(where)
+    return pack_bits(mask), int(mask.sum())

@@ -33,7 +33,7 @@ from typing import Any, Dict, List, Mapping, Optional, Sequence
 import numpy as np
 
 from .. import engine
-from .filters import MetaIndex, pack_bits
+from .filters import MetaIndex
 from .tokenize import _tokenize, detect_lang_tag
 
 
@@ -228,12 +228,12 @@ class BM25Store:
         if not live or not self._entries:
             return out
         self._ensure_index()
-        if where:
+        allow = None
+        if where:  # device-evaluated filter; statistics follow it (Q2)
             self._ensure_meta()
-            mask = self._meta.bm25_mask(where)
+            allow, n_cand = engine.where_bits(self._meta, where, "bm25", self._index.device)
         else:
-            mask = np.ones(len(self._id_list), bool)
-        n_cand = int(mask.sum())
+            n_cand = len(self._id_list)
         if n_cand == 0:
             return out
         k = top_k if top_k >= 0 else n_cand + top_k      # python slice semantics of [:top_k]
@@ -242,7 +242,6 @@ class BM25Store:
             return out
         if k > engine.L.max_topk():
             raise ValueError(f"top_k={top_k} exceeds the GPU top-k limit {engine.L.max_topk()}")
-        allow = pack_bits(mask) if where else None
         qids = [self._query_ids(queries[i]) for i in live]
         scores, rows, nvalid = self._index.search(qids, k, allow)
         for j, i in enumerate(live):

@@ -11,9 +11,14 @@ Two semantics, both from the reference:
   over a ``tags`` list (returning before the simple fields are looked at), and
   ``$and`` recursion (ignoring sibling keys).
 
-Metadata is kept column-wise (per key an int32 code array + value->code dicts)
-so a filter over N rows is a few vectorised numpy compares, and the resulting
-boolean mask is packed into the uint32 bitmap the kernels read.
+Metadata is kept column-wise (per key an int32 code array + value->code dicts).
+``bm25_program`` / ``chroma_program`` compile a where clause into a postfix
+``FilterProgram`` over those code columns that ``cm_filter_eval`` runs in HBM
+(``engine.filter_bits``), one lane per row, straight into the
+uint32 allow bitmap the scan kernels read.  Leaves the columns cannot express
+-- BM25 ``tags.$contains`` row sets, ``$gt``-style comparisons, unhashable
+values -- are evaluated here and enter the program as bitmaps.
+``bm25_mask`` / ``chroma_mask`` are the same semantics in numpy (bool[n]).
 """
 from __future__ import annotations
 
@@ -81,9 +86,10 @@ def _typed(v):
 
 
 class _Column:
-    __slots__ = ("py", "ty", "py_map", "ty_map")
+    __slots__ = ("py", "ty", "py_map", "ty_map", "n_odd")
 
     def __init__(self, cap: int):
+        self.n_odd = 0  # rows holding an unhashable value (evaluated row by row)
         self.py = np.full(cap, _MISSING, np.int32)
         self.ty = np.full(cap, _MISSING, np.int32)
         self.py_map: Dict[Any, int] = {}
@@ -107,6 +113,8 @@ class MetaIndex:
         self.cols: Dict[str, _Column] = {}
         self.tags: Dict[Any, set] = {}
         self._cap = 0
+        self.version = 0          # bumped by every set/remove: device copies compare against it
+        self._dev_cache = None    # engine.filter_bits' device copies of columns / live bits
 
     def __len__(self):
         return len(self.metas)
@@ -127,6 +135,7 @@ class MetaIndex:
         self._ensure(row + 1)
         if self.live[row]:
             self.remove(row)
+        self.version += 1
         self.metas[row] = meta
         self.live[row] = True
         for key, v in (meta or {}).items():
@@ -138,6 +147,7 @@ class MetaIndex:
                 col.ty[row] = col.ty_map.setdefault(_typed(v), len(col.ty_map))
             except TypeError:  # unhashable value: evaluated row by row
                 col.py[row] = col.ty[row] = _UNHASHABLE
+                col.n_odd += 1
         tags = (meta or {}).get("tags")
         if isinstance(tags, (list, tuple, set)):
             for t in tags:
@@ -149,10 +159,13 @@ class MetaIndex:
     def remove(self, row: int):
         if row >= len(self.metas) or not self.live[row]:
             return
+        self.version += 1
         meta = self.metas[row] or {}
         for key in meta:
             col = self.cols.get(key)
             if col is not None:
+                if col.py[row] == _UNHASHABLE:
+                    col.n_odd -= 1
                 col.py[row] = col.ty[row] = _MISSING
         tags = meta.get("tags")
         if isinstance(tags, (list, tuple, set)):
@@ -186,7 +199,7 @@ class MetaIndex:
         m = (codes == c) if c is not None else np.zeros(n, bool)
         if value is None:
             m = m | (codes == _MISSING)
-        if (codes == _UNHASHABLE).any():
+        if col.n_odd:
             odd = np.nonzero(codes == _UNHASHABLE)[0]
             for r in odd:
                 m[r] = (self.metas[r] or {}).get(key) == value
@@ -280,6 +293,200 @@ class MetaIndex:
             else:
                 m &= self._eq_typed(key, cond)
         return m
+
+
+    # ---- compiled programs (same semantics, evaluated by cm_filter_eval) ----
+    def _eq_py_prog(self, P: "FilterProgram", key: str, value) -> None:
+        col = self.cols.get(key)
+        if col is None:
+            P.const(value is None)
+            return
+        try:
+            c = col.py_map.get(value, None)
+        except TypeError:
+            P.mask(self._eq_py(key, value))
+            return
+        if col.n_odd:
+            P.mask(self._eq_py(key, value))
+            return
+        if c is None and value is not None:
+            P.const(False)
+            return
+        if c is not None:
+            P.eq(key, "py", c)
+        if value is None:
+            P.eq(key, "py", _MISSING)
+            if c is not None:
+                P.op(FOP_OR)
+
+    def _eq_typed_prog(self, P: "FilterProgram", key: str, value) -> None:
+        col = self.cols.get(key)
+        try:
+            c = None if col is None else col.ty_map.get(_typed(value), None)
+        except TypeError:
+            c = None
+        if c is None:
+            P.const(False)
+        else:
+            P.eq(key, "ty", c)
+
+    def _has_prog(self, P: "FilterProgram", key: str) -> None:
+        if key not in self.cols:
+            P.const(False)
+        else:
+            P.ne(key, "ty", _MISSING)
+
+    def _bm25_prog(self, P: "FilterProgram", where) -> None:
+        if not where:
+            P.const(True)
+            return
+        if "$and" in where:
+            P.const(True)
+            for clause in where["$and"]:
+                self._bm25_prog(P, clause)
+                P.op(FOP_AND)
+            return
+        if "tags" in where and isinstance(where["tags"], dict) and "$contains" in where["tags"]:
+            t = where["tags"]["$contains"]
+            P.const(True)
+            if t:
+                n = self._n()
+                for tag in ({t} if isinstance(t, str) else set(t)):
+                    hit = np.zeros(n, bool)
+                    hit[np.fromiter(self.tags.get(tag, ()), np.int64)] = True
+                    P.mask(hit)
+                    P.op(FOP_AND)
+            return
+        P.const(True)
+        for f in SIMPLE_FIELDS:
+            if f in where:
+                self._eq_py_prog(P, f, where[f])
+                P.op(FOP_AND)
+
+    def _chroma_prog(self, P: "FilterProgram", where) -> None:
+        P.const(True)
+        if not where:
+            return
+        for key, cond in where.items():
+            if key == "$and":
+                P.const(True)
+                for c in cond:
+                    self._chroma_prog(P, c)
+                    P.op(FOP_AND)
+            elif key == "$or":
+                P.const(False)
+                for c in cond:
+                    self._chroma_prog(P, c)
+                    P.op(FOP_OR)
+            elif isinstance(cond, dict):
+                if len(cond) != 1:
+                    raise ValueError(f"Expected operator expression with one operator, got {cond}")
+                (op, arg), = cond.items()
+                if op == "$eq":
+                    self._eq_typed_prog(P, key, arg)
+                elif op == "$ne":
+                    self._has_prog(P, key)
+                    self._eq_typed_prog(P, key, arg)
+                    P.op(FOP_NOT)
+                    P.op(FOP_AND)
+                elif op == "$in":
+                    P.const(False)
+                    for a in arg:
+                        self._eq_typed_prog(P, key, a)
+                        P.op(FOP_OR)
+                elif op == "$nin":
+                    self._has_prog(P, key)
+                    for a in arg:
+                        self._eq_typed_prog(P, key, a)
+                        P.op(FOP_NOT)
+                        P.op(FOP_AND)
+                elif op in ("$gt", "$gte", "$lt", "$lte"):
+                    P.mask(self._slow(lambda meta, k=key, o=op, a=arg: _cmp(meta, k, o, a)))
+                else:
+                    raise ValueError(f"Unsupported where operator {op}")
+            else:
+                self._eq_typed_prog(P, key, cond)
+            P.op(FOP_AND)
+
+    def bm25_program(self, where: Optional[Mapping[str, Any]]) -> "FilterProgram":
+        """bm25_mask as a device program: live AND the clause."""
+        P = FilterProgram(self)
+        P.live()
+        self._bm25_prog(P, where)
+        P.op(FOP_AND)
+        return P
+
+    def chroma_program(self, where: Optional[Mapping[str, Any]]) -> "FilterProgram":
+        """chroma_mask as a device program: live AND the clause."""
+        P = FilterProgram(self)
+        P.live()
+        self._chroma_prog(P, where)
+        P.op(FOP_AND)
+        return P
+
+
+# cm_filter_eval opcodes (include/classmate_hip.h)
+FOP_EQ, FOP_NE, FOP_BITS, FOP_TRUE, FOP_FALSE, FOP_AND, FOP_OR, FOP_NOT = range(1, 9)
+MAX_OPS, MAX_SOURCES = 64, 16
+
+
+class FilterProgram:
+    """Postfix program for cm_filter_eval: ops (opcode, a, b); column slots name (key, "py"|"ty")
+    code arrays of the MetaIndex, bitmap slots are the live bits ("live") or host-evaluated masks."""
+
+    def __init__(self, meta: MetaIndex):
+        self.meta = meta
+        self.n = meta._n()
+        self.ops: List[tuple] = []
+        self.cols: List[tuple] = []
+        self.bits: List[Any] = []
+        self._depth = self.max_depth = 0
+
+    def _push(self, op, a=0, b=0):
+        self.ops.append((op, a, b))
+        self._depth += 1
+        self.max_depth = max(self.max_depth, self._depth)
+
+    def op(self, op):
+        self.ops.append((op, 0, 0))
+        if op in (FOP_AND, FOP_OR):
+            self._depth -= 1
+
+    def _col(self, key, kind) -> int:
+        if (key, kind) not in self.cols:
+            self.cols.append((key, kind))
+        return self.cols.index((key, kind))
+
+    def eq(self, key, kind, code):
+        self._push(FOP_EQ, self._col(key, kind), int(code))
+
+    def ne(self, key, kind, code):
+        self._push(FOP_NE, self._col(key, kind), int(code))
+
+    def const(self, v: bool):
+        self._push(FOP_TRUE if v else FOP_FALSE)
+
+    def live(self):
+        if "live" not in self.bits:
+            self.bits.append("live")
+        self._push(FOP_BITS, self.bits.index("live"))
+
+    def mask(self, m: np.ndarray):
+        self.bits.append(np.asarray(m, bool)[: self.n])
+        self._push(FOP_BITS, len(self.bits) - 1)
+
+    @property
+    def fits_device(self) -> bool:
+        return (len(self.ops) <= MAX_OPS and len(self.cols) <= MAX_SOURCES and len(self.bits) <= MAX_SOURCES
+                and self.max_depth <= 32)
+
+    def column(self, slot: int) -> np.ndarray:
+        key, kind = self.cols[slot]
+        return getattr(self.meta.cols[key], kind)[: self.n]
+
+    def bitmap(self, slot: int) -> np.ndarray:
+        b = self.bits[slot]
+        return self.meta.live[: self.n] if isinstance(b, str) else b
 
 
 def _cmp(meta, key, op, arg) -> bool:

@@ -34,7 +34,7 @@ from typing import Any, Dict, List, Mapping, Optional, Sequence
 import numpy as np
 
 from .. import engine
-from .filters import MetaIndex, pack_bits
+from .filters import MetaIndex
 
 
 _FORMAT = 2
@@ -210,9 +210,8 @@ class GpuVectorStore:
         self._ensure_loaded()
         if self._index is None:
             return None
-        if where:
-            mask = self._meta.chroma_mask(where)
-            allow, n_ok = pack_bits(mask), int(mask.sum())
+        if where:  # device-evaluated filter
+            allow, n_ok = engine.where_bits(self._meta, where, "chroma", self._index.device)
         else:
             allow, n_ok = None, self._index.live_count()
         k = min(int(top_k), n_ok)

@@ -1581,7 +1581,7 @@ int cm_bm25_search(cm_bm25 *h, const int32_t *q_terms, const int32_t *q_off, int
   std::vector<double> q_idf((size_t)std::max(total, 1), 0.0);
   if (allow_bits) {
     if ((rc = h->allow_buf.ensure((size_t)nw * 4)) || (rc = h->tmp.ensure(16))) return rc;
-    CM_HIP(hipMemcpyAsync(h->allow_buf.ptr, allow_bits, (size_t)nw * 4, hipMemcpyHostToDevice, h->stream));
+    CM_HIP(hipMemcpyAsync(h->allow_buf.ptr, allow_bits, (size_t)nw * 4, hipMemcpyDefault, h->stream));  // host or device
     allow_dev = h->allow_buf.as<uint32_t>();
     CM_HIP(hipMemsetAsync(h->tmp.ptr, 0, 16, h->stream));
     hipLaunchKernelGGL(bm25_filtered_stats_kernel, dim3((unsigned)std::min<int64_t>(1024, ceil_div(nw, 256))),

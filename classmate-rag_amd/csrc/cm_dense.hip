@@ -1943,7 +1943,7 @@ int cm_dense_search(cm_dense *h, const float *q, int32_t nq, int32_t k, const ui
   if (allow_bits) {
     const int64_t nw = ceil_div(h->size, 32);
     if ((rc = h->allow_buf.ensure((size_t)std::max<int64_t>(nw, 1) * 4))) return rc;
-    CM_HIP(hipMemcpyAsync(h->allow_buf.ptr, allow_bits, (size_t)nw * 4, hipMemcpyHostToDevice, h->stream));
+    CM_HIP(hipMemcpyAsync(h->allow_buf.ptr, allow_bits, (size_t)nw * 4, hipMemcpyDefault, h->stream));  // host or device
     allow_dev = h->allow_buf.as<uint32_t>();
   }
   CM_HIP(hipMemcpyAsync(h->staging.ptr, q, qbytes, hipMemcpyHostToDevice, h->stream));

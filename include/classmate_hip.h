@@ -81,7 +81,8 @@ int32_t cm_dense_dim(cm_dense *h);
  * nq queries (host, nq x dim) return the k nearest live+allowed rows in
  * ascending (distance, row) order.  out_dist/out_row: nq x k.  out_vec
  * (nullable): nq x k x dim, the stored embeddings (include_embeddings).
- * allow_bits (nullable, host): ceil(size/32) words.                      */
+ * allow_bits (nullable, host or device memory -- e.g. cm_filter_eval's
+ * output, complete before the call): ceil(size/32) words.               */
 int cm_dense_search(cm_dense *h, const float *q, int32_t nq, int32_t k, const uint32_t *allow_bits,
                     float *out_dist, int64_t *out_row, float *out_vec);
 /* workspace bytes cm_dense_search_dev needs for (nq, k). */
@@ -195,6 +196,34 @@ int64_t cm_bm25_search_workspace(cm_bm25 *h, int32_t nq, int32_t total_terms, in
 int cm_bm25_search_dev(cm_bm25 *h, const int32_t *q_terms_dev, const int32_t *q_off_dev, int32_t nq,
                        int32_t total_terms, int32_t k, double *score_dev, int64_t *row_dev,
                        void *workspace_dev, int64_t workspace_bytes, void *stream);
+
+/* Where-filters on the device ---------------------------
+ * A where clause compiled on the host (classmate_hip/retrieval/filters.py,
+ * replacing the per-row _matches_filter of rag/retrieval/bm25.py:79-107
+ * and Chroma's where evaluation behind vector_chroma.py:45-78,204-253)
+ * into a postfix program: n_ops triples (opcode, a, b) in prog (host).
+ *   CM_FOP_EQ / CM_FOP_NE  push cols_dev[a][row] == b  /  != b
+ *   CM_FOP_BITS            push bit row of bitmap bits_dev[a]
+ *   CM_FOP_TRUE / FALSE    push a constant
+ *   CM_FOP_AND / OR        pop two, push the result;  CM_FOP_NOT  negate top
+ * cols_dev / bits_dev: host arrays of device pointers (int32 value codes,
+ * n_rows each; uint32 bitmaps, ceil(n_rows/32) words).  out_dev receives
+ * ceil(n_rows/32) words (bit r & 31 of word r >> 5); count_dev (nullable,
+ * device) the number of set bits.  Stack depth <= 32; <= CM_FILTER_MAX_OPS
+ * ops and <= CM_FILTER_MAX_SOURCES columns and bitmaps.  Async on stream. */
+#define CM_FILTER_MAX_OPS 64
+#define CM_FILTER_MAX_SOURCES 16
+#define CM_FOP_EQ 1
+#define CM_FOP_NE 2
+#define CM_FOP_BITS 3
+#define CM_FOP_TRUE 4
+#define CM_FOP_FALSE 5
+#define CM_FOP_AND 6
+#define CM_FOP_OR 7
+#define CM_FOP_NOT 8
+int cm_filter_eval(const int32_t *prog, int32_t n_ops, const int32_t *const *cols_dev, int32_t n_cols,
+                   const uint32_t *const *bits_dev, int32_t n_bits, int64_t n_rows, uint32_t *out_dev,
+                   unsigned long long *count_dev, void *stream);
 
 /* Fusion -------------------------------------------------------------- */
 /* _mmr_order (rag/retrieval/fusion.py:39-61) for nq queries at once:
