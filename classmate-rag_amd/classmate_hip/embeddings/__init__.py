@@ -236,4 +236,6 @@ class E5MultilingualEmbedder:
         return self._encode(self._fmt_passages(texts)).astype("float32", copy=False)
 
 
-__all__ = ["E5MultilingualEmbedder", "HashTokenizer", "E5_BASE_CONFIG"]
+from .cache import CachingEmbedder  # noqa: E402  (rag/embeddings/cache.py drop-in)
+
+__all__ = ["E5MultilingualEmbedder", "CachingEmbedder", "HashTokenizer", "E5_BASE_CONFIG"]
