@@ -138,7 +138,10 @@ class E5MultilingualEmbedder:
         """XLM-R encoder forward for unpadded batches from this model's own weights (same math as
         the HF module: embeddings + LayerNorm, 12 x [self-attention, residual + LayerNorm, GELU
         MLP, residual + LayerNorm]) with the Q/K/V projections fused into one GEMM and attention
-        through unmasked SDPA (the flash kernel).  Built once; returns fwd(ids) -> hidden."""
+        through unmasked SDPA (the flash kernel).  Every "residual add + LayerNorm" (and the
+        embeddings' sum + LayerNorm) is one pass of the HIP kernel cm_add_layernorm instead of
+        torch's add kernel + LayerNorm kernel (CM_E5_FUSED_LN=0 restores the torch pair).
+        Built once; returns fwd(ids) -> hidden."""
         import torch
         import torch.nn.functional as F
         if getattr(self, "_lean", None) is not None:
@@ -161,19 +164,27 @@ class E5MultilingualEmbedder:
                                L.output.dense.weight, L.output.dense.bias, L.output.LayerNorm.weight,
                                L.output.LayerNorm.bias))
 
+        fused = os.environ.get("CM_E5_FUSED_LN", "1") != "0" and self.dtype in (torch.bfloat16, torch.float32)
+        if fused:
+            def add_ln(x, r, g, b):
+                return engine.add_layernorm(x, r, g, b, eps)
+        else:
+            def add_ln(x, r, g, b):
+                return F.layer_norm(x + r, (D,), g, b, eps)
+
         def fwd(ids):
             B, S = ids.shape
             # unpadded rows: XLM-R position ids are padding_idx + 1 .. padding_idx + S
             pos = torch.arange(pad + 1, pad + 1 + S, device=ids.device)
-            x = emb.word_embeddings(ids) + emb.position_embeddings(pos)[None] + emb.token_type_embeddings.weight[0]
-            x = F.layer_norm(x, (D,), emb.LayerNorm.weight, emb.LayerNorm.bias, eps)
+            pt = emb.position_embeddings(pos) + emb.token_type_embeddings.weight[0]  # (S, D), tiled over the batch
+            x = add_ln(emb.word_embeddings(ids), pt if fused else pt[None], emb.LayerNorm.weight, emb.LayerNorm.bias)
             for (wqkv, bqkv, wo, bo, g1, b1, wi, bi, w2, b2, g2, bb2) in layers:
                 qkv = F.linear(x, wqkv, bqkv).view(B, S, 3, H, D // H).permute(2, 0, 3, 1, 4)
                 o = F.scaled_dot_product_attention(qkv[0], qkv[1], qkv[2])
                 o = o.transpose(1, 2).reshape(B, S, D)
-                x = F.layer_norm(x + F.linear(o, wo, bo), (D,), g1, b1, eps)
+                x = add_ln(x, F.linear(o, wo, bo), g1, b1)
                 h = F.gelu(F.linear(x, wi, bi))
-                x = F.layer_norm(x + F.linear(h, w2, b2), (D,), g2, bb2, eps)
+                x = add_ln(x, F.linear(h, w2, b2), g2, bb2)
             return x
 
         self._lean = fwd

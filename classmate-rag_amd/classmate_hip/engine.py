@@ -447,6 +447,31 @@ def meanpool_l2norm(hidden, mask, normalize: bool = True, out=None):
     return out
 
 
+
+def add_layernorm(x, r, weight, bias, eps: float, out=None):
+    """LayerNorm(x + r) over the last dim in one pass (cm_add_layernorm; the XLM-R block epilogue).
+
+    x: (..., D) f32/bf16 device; r: same shape as x, or (R, D) broadcast over rows (row i uses
+    r[i % R]), or None; weight/bias: (D,) of x's dtype.  The sum is rounded to x's dtype before the
+    statistics, as ``F.layer_norm(x + r, ...)`` does."""
+    D = x.shape[-1]
+    dt = {torch.float32: L.CM_DTYPE_F32, torch.bfloat16: L.CM_DTYPE_BF16}[x.dtype]
+    x = x.contiguous()
+    rows = x.numel() // D
+    if r is not None:
+        r = r.contiguous()
+        if r.dtype != x.dtype or r.shape[-1] != D or rows % (r.numel() // D):
+            raise ValueError("residual must match x's dtype and feature dim and tile its rows")
+    for t in (weight, bias):
+        if t.dtype != x.dtype or t.numel() != D or not t.is_contiguous():
+            raise ValueError("weight/bias must be contiguous (D,) of x's dtype")
+    if out is None:
+        out = torch.empty_like(x)
+    L.check(L.fn["cm_add_layernorm"](L.ptr(x), L.ptr(r) if r is not None else None,
+                                     (r.numel() // D) if r is not None else 0, L.ptr(weight), L.ptr(bias), rows, D,
+                                     float(eps), dt, L.ptr(out), _stream(x.device.index)), "cm_add_layernorm")
+    return out
+
 # ---------------------------------------------------------------------------
 # Where-filters on the device (SURVEY §8f-2): retrieval.filters compiles, cm_filter_eval runs.
 def filter_bits(prog, device: Optional[int] = None):

@@ -264,6 +264,17 @@ int cm_rrf_merge(const int64_t *vkeys, const float *vdist, const int32_t *vn, in
 int cm_meanpool_l2norm(const void *hidden_dev, int32_t hidden_dtype, const void *mask_dev, int32_t mask_dtype,
                        int32_t B, int32_t S, int32_t D, int32_t normalize, float *out_dev, void *stream);
 
+/* E5 encoder block epilogue ----------------------------------------------
+ * XLM-R "residual add + LayerNorm" (HF XLMRobertaSelfOutput / XLMRobertaOutput /
+ * XLMRobertaEmbeddings, run by E5MultilingualEmbedder.encode_*,
+ * rag/embeddings/__init__.py:85-105) fused into one pass:
+ * out[i] = LN(round(x[i] + r[i % r_rows])) * gamma + beta over D features,
+ * fp32 statistics.  r may be NULL (plain LayerNorm); out may alias x.
+ * dtype F32 or BF16 for x, r, gamma, beta and out; rows x D row-major.  */
+int cm_add_layernorm(const void *x_dev, const void *r_dev, int64_t r_rows, const void *gamma_dev,
+                     const void *beta_dev, int64_t rows, int32_t D, float eps, int32_t dtype, void *out_dev,
+                     void *stream);
+
 #ifdef __cplusplus
 }
 #endif

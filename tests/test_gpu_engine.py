@@ -474,3 +474,47 @@ def test_bm25_pruned_skips_ranges_and_matches_full_scan(eng):
     f2 = b.search(queries, k, allow)
     assert np.array_equal(f1[1], f2[1]) and np.array_equal(f1[0], f2[0])
     assert all(int(r) % 3 == 0 for r in f2[1].ravel() if r >= 0)
+
+
+@pytest.mark.parametrize("D", [768, 1024, 20, 2048])
+def test_add_layernorm_matches_torch(eng, D):
+    """cm_add_layernorm == F.layer_norm(x + r) (torch fp32 reference of the same op)."""
+    import torch
+    import torch.nn.functional as F
+    torch.manual_seed(D)
+    rows = 6144 + 3
+    for dt, tol in ((torch.float32, 2e-5), (torch.bfloat16, 1.6e-2)):
+        x = torch.randn(rows, D, device="cuda").to(dt)
+        r = (3 * torch.randn(rows, D, device="cuda") + 1).to(dt)
+        w = torch.randn(D, device="cuda").to(dt)
+        b = torch.randn(D, device="cuda").to(dt)
+        ref = F.layer_norm((x + r).float(), (D,), w.float(), b.float(), 1e-5)   # sum rounded to dt as torch does
+        out = eng.add_layernorm(x, r, w, b, 1e-5)
+        assert out.dtype == dt and out.shape == x.shape
+        torch.testing.assert_close(out.float(), ref, atol=tol, rtol=tol)
+        # broadcast residual (positional table tiled over the batch) and no residual
+        pt = torch.randn(24, D, device="cuda").to(dt)
+        xb = x[: 24 * 256]
+        ref = F.layer_norm((xb.view(256, 24, D) + pt).float(), (D,), w.float(), b.float(), 1e-5).view(-1, D)
+        torch.testing.assert_close(eng.add_layernorm(xb, pt, w, b, 1e-5).float(), ref, atol=tol, rtol=tol)
+        ref = F.layer_norm(x.float(), (D,), w.float(), b.float(), 1e-5)
+        torch.testing.assert_close(eng.add_layernorm(x, None, w, b, 1e-5).float(), ref, atol=tol, rtol=tol)
+    with pytest.raises(ValueError):
+        eng.add_layernorm(x, r[:5], w, b, 1e-5)
+
+
+def test_e5_lean_forward_fp32_matches_hf():
+    """The graph-captured lean E5 forward (fused QKV GEMM, flash SDPA, HIP add+LayerNorm) equals the
+    Hugging Face XLM-R module in fp32."""
+    import torch
+    from classmate_hip.embeddings import E5MultilingualEmbedder
+    emb = E5MultilingualEmbedder.random_init(seed=3, device="cuda", num_layers=2, dtype="float32")
+    B, S = 8, 24
+    g = torch.Generator(device="cuda").manual_seed(9)
+    ids = torch.randint(5, 250002, (B, S), device="cuda", generator=g)
+    mask = torch.ones_like(ids)
+    u_ids, u_mask, u_out, graph = emb.capture_graph(B, S, unpadded=True)
+    u_ids.copy_(ids)
+    graph.replay()
+    torch.cuda.synchronize()
+    torch.testing.assert_close(u_out, emb.encode_token_ids(ids, mask), atol=2e-5, rtol=0)
