@@ -103,6 +103,7 @@ SIGNATURES = {
                          c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp),
     "cm_filter_eval": (c_int, c_vp, c_i32, c_vp, c_i32, c_vp, c_i32, c_i64, c_vp, c_vp, c_vp),
     "cm_meanpool_l2norm": (c_int, c_vp, c_i32, c_vp, c_i32, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp),
+    "cm_short_attention": (c_int, c_vp, c_i32, c_i32, c_i32, c_i32, c_f32, c_i32, c_vp, c_vp),
     "cm_add_layernorm": (c_int, c_vp, c_vp, c_i64, c_vp, c_vp, c_i64, c_i32, c_f32, c_i32, c_vp, c_vp),
 }
 

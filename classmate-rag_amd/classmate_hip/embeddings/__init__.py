@@ -20,6 +20,7 @@ torch fp32 reference).
 from __future__ import annotations
 
 import hashlib
+import math
 import os
 import re
 from typing import Iterable, List, Optional
@@ -140,7 +141,9 @@ class E5MultilingualEmbedder:
         MLP, residual + LayerNorm]) with the Q/K/V projections fused into one GEMM and attention
         through unmasked SDPA (the flash kernel).  Every "residual add + LayerNorm" (and the
         embeddings' sum + LayerNorm) is one pass of the HIP kernel cm_add_layernorm instead of
-        torch's add kernel + LayerNorm kernel (CM_E5_FUSED_LN=0 restores the torch pair).
+        torch's add kernel + LayerNorm kernel (CM_E5_FUSED_LN=0 restores the torch pair), and for
+        S <= 64 attention is cm_short_attention reading the QKV GEMM output in place
+        (CM_E5_FUSED_ATTN=0 restores permute + SDPA + transpose).
         Built once; returns fwd(ids) -> hidden."""
         import torch
         import torch.nn.functional as F
@@ -165,6 +168,9 @@ class E5MultilingualEmbedder:
                                L.output.LayerNorm.bias))
 
         fused = os.environ.get("CM_E5_FUSED_LN", "1") != "0" and self.dtype in (torch.bfloat16, torch.float32)
+        fused_attn = (os.environ.get("CM_E5_FUSED_ATTN", "1") != "0" and D // H == 64
+                      and self.dtype in (torch.bfloat16, torch.float32))
+        scale = 1.0 / math.sqrt(D // H)
         if fused:
             def add_ln(x, r, g, b):
                 return engine.add_layernorm(x, r, g, b, eps)
@@ -178,10 +184,14 @@ class E5MultilingualEmbedder:
             pos = torch.arange(pad + 1, pad + 1 + S, device=ids.device)
             pt = emb.position_embeddings(pos) + emb.token_type_embeddings.weight[0]  # (S, D), tiled over the batch
             x = add_ln(emb.word_embeddings(ids), pt if fused else pt[None], emb.LayerNorm.weight, emb.LayerNorm.bias)
+            short = fused_attn and S <= 64
             for (wqkv, bqkv, wo, bo, g1, b1, wi, bi, w2, b2, g2, bb2) in layers:
-                qkv = F.linear(x, wqkv, bqkv).view(B, S, 3, H, D // H).permute(2, 0, 3, 1, 4)
-                o = F.scaled_dot_product_attention(qkv[0], qkv[1], qkv[2])
-                o = o.transpose(1, 2).reshape(B, S, D)
+                if short:   # HIP kernel reads the QKV GEMM output in place, writes (B, S, D)
+                    o = engine.short_attention(F.linear(x, wqkv, bqkv), H, scale)
+                else:
+                    qkv = F.linear(x, wqkv, bqkv).view(B, S, 3, H, D // H).permute(2, 0, 3, 1, 4)
+                    o = F.scaled_dot_product_attention(qkv[0], qkv[1], qkv[2])
+                    o = o.transpose(1, 2).reshape(B, S, D)
                 x = add_ln(x, F.linear(o, wo, bo), g1, b1)
                 h = F.gelu(F.linear(x, wi, bi))
                 x = add_ln(x, F.linear(h, w2, b2), g2, bb2)

@@ -472,6 +472,23 @@ def add_layernorm(x, r, weight, bias, eps: float, out=None):
                                      float(eps), dt, L.ptr(out), _stream(x.device.index)), "cm_add_layernorm")
     return out
 
+
+def short_attention(qkv, heads: int, scale: float, out=None):
+    """Unmasked self-attention straight from a fused QKV projection (cm_short_attention).
+
+    qkv: (B, S, 3*heads*64) f32/bf16 device, S <= 64 -> (B, S, heads*64): per head
+    softmax(q k^T * scale) v, fp32 softmax."""
+    B, S, F3 = qkv.shape
+    if F3 != 3 * heads * 64 or not 0 < S <= 64:
+        raise ValueError("qkv must be (B, S<=64, 3*heads*64)")
+    dt = {torch.float32: L.CM_DTYPE_F32, torch.bfloat16: L.CM_DTYPE_BF16}[qkv.dtype]
+    qkv = qkv.contiguous()
+    if out is None:
+        out = torch.empty((B, S, heads * 64), dtype=qkv.dtype, device=qkv.device)
+    L.check(L.fn["cm_short_attention"](L.ptr(qkv), B, S, heads, 64, float(scale), dt, L.ptr(out),
+                                       _stream(qkv.device.index)), "cm_short_attention")
+    return out
+
 # ---------------------------------------------------------------------------
 # Where-filters on the device (SURVEY §8f-2): retrieval.filters compiles, cm_filter_eval runs.
 def filter_bits(prog, device: Optional[int] = None):

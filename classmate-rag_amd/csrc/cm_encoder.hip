@@ -133,6 +133,199 @@ int launch_add_ln(const void *x, const void *r, int64_t r_rows, const void *g, c
   return CM_OK;
 }
 
+// Short-sequence self-attention for the unpadded query encode (XLM-R, S <= 64, head dim 64):
+// reads Q/K/V straight from the fused QKV GEMM output (B, S, 3, H, 64) and writes the
+// context in (B, S, H*64) — the layout the output projection consumes — so the permute /
+// transpose copies around torch's SDPA disappear.  One wave per (sequence, head); lane i
+// owns query row i: its q row in registers, K and V rows of the head staged in LDS (read as
+// broadcasts), fp32 online softmax.  bytes per (b, h) = 4*S*64*sizeof(T) (q, k, v in, o out).
+constexpr int kAttnDh = 64;
+constexpr int kAttnMaxS = 64;
+
+__device__ inline void ld8(const float *p, float (&v)[8]) {
+  ln_load4(p, *reinterpret_cast<float(*)[4]>(&v[0]));
+  ln_load4(p + 4, *reinterpret_cast<float(*)[4]>(&v[4]));
+}
+__device__ inline void ld8(const __hip_bfloat16 *p, float (&v)[8]) {
+  const uint4 x = *reinterpret_cast<const uint4 *>(p);
+  const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    v[2 * e] = __uint_as_float(w[e] << 16);
+    v[2 * e + 1] = __uint_as_float(w[e] & 0xffff0000u);
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(64) short_attention_kernel(const T *__restrict__ qkv, int S, int H, float scale,
+                                                             T *__restrict__ out) {
+  constexpr int VPR = kAttnDh * sizeof(T) / 16;  // 16-byte vectors per head row
+  __shared__ __attribute__((aligned(16))) T ks[kAttnMaxS * kAttnDh];
+  __shared__ __attribute__((aligned(16))) T vs[kAttnMaxS * kAttnDh];
+  const int lane = threadIdx.x;
+  const int h = blockIdx.x % H;
+  const int64_t b = blockIdx.x / H;
+  const int64_t tok_stride = 3LL * H * kAttnDh;
+  const T *base = qkv + b * S * tok_stride + (int64_t)h * kAttnDh;
+  // stage K and V rows of this head: S * VPR 16-byte vectors each
+  for (int t = lane; t < S * VPR; t += 64) {
+    const int s = t / VPR, v = t % VPR;
+    const uint4 *ksrc = reinterpret_cast<const uint4 *>(base + s * tok_stride + (int64_t)H * kAttnDh) + v;
+    const uint4 *vsrc = reinterpret_cast<const uint4 *>(base + s * tok_stride + 2LL * H * kAttnDh) + v;
+    reinterpret_cast<uint4 *>(ks)[t] = *ksrc;
+    reinterpret_cast<uint4 *>(vs)[t] = *vsrc;
+  }
+  __syncthreads();
+  if (lane >= S) return;
+  float q[kAttnDh], acc[kAttnDh];
+  const T *qrow = base + lane * tok_stride;
+#pragma unroll
+  for (int c = 0; c < kAttnDh / 8; ++c) {
+    float t8[8];
+    ld8(qrow + 8 * c, t8);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      q[8 * c + e] = t8[e] * scale;
+      acc[8 * c + e] = 0.f;
+    }
+  }
+  float m = -INFINITY, l = 0.f;
+  for (int j = 0; j < S; ++j) {
+    float sc = 0.f;
+#pragma unroll
+    for (int c = 0; c < kAttnDh / 8; ++c) {
+      float k8[8];
+      ld8(ks + j * kAttnDh + 8 * c, k8);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) sc += q[8 * c + e] * k8[e];
+    }
+    const float mn = fmaxf(m, sc);
+    const float corr = __expf(m - mn);
+    const float p = __expf(sc - mn);
+    l = l * corr + p;
+    m = mn;
+#pragma unroll
+    for (int c = 0; c < kAttnDh / 8; ++c) {
+      float v8[8];
+      ld8(vs + j * kAttnDh + 8 * c, v8);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[8 * c + e] = acc[8 * c + e] * corr + p * v8[e];
+    }
+  }
+  const float inv = 1.f / l;
+  T *orow = out + (b * S + lane) * (int64_t)H * kAttnDh + (int64_t)h * kAttnDh;
+#pragma unroll
+  for (int c = 0; c < kAttnDh / 4; ++c) {
+    float y[4] = {acc[4 * c] * inv, acc[4 * c + 1] * inv, acc[4 * c + 2] * inv, acc[4 * c + 3] * inv};
+    ln_store4(orow + 4 * c, y);
+  }
+}
+
+// bf16, S <= 32: the same attention on the matrix cores.  Per (sequence, head) one wave runs
+// S^T = K Q^T as 2x2 tiles of v_mfma_f32_16x16x32_bf16 (K = head dim 64 in two steps), the
+// softmax over keys on the accumulators (a query is one lane column: 8 registers x 4 lane
+// groups, two xor-shuffles), and O = P V as one K=32 MFMA per output tile: the S^T
+// accumulator layout (col = query on the lane, rows = keys in registers) IS the A-operand
+// layout of P once the key order inside the K=32 reduction is permuted — key slot (g, j)
+// of lane group g holds key 4g + j (j < 4) or 16 + 4g + j - 4 — and V^T is staged in LDS
+// in that order.  Padded keys (>= S) get probability 0 and zero V rows; padded queries
+// are computed and not stored.
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+
+__global__ void __launch_bounds__(64) short_attention_mfma_kernel(const __hip_bfloat16 *__restrict__ qkv, int S, int H,
+                                                                  float scale, __hip_bfloat16 *__restrict__ out) {
+  constexpr int VT = 36;  // V^T row stride (keys): 72 B keeps 8-byte reads aligned
+  __shared__ __attribute__((aligned(16))) __bf16 vt[kAttnDh * VT];
+  const int lane = threadIdx.x;
+  const int g = lane >> 4, c = lane & 15;
+  const int h = blockIdx.x % H;
+  const int64_t b = blockIdx.x / H;
+  const int64_t tok = 3LL * H * kAttnDh;
+  const __bf16 *base = reinterpret_cast<const __bf16 *>(qkv) + b * S * tok + (int64_t)h * kAttnDh;
+  const __bf16 *kb = base + (int64_t)H * kAttnDh;
+  const __bf16 *vb = base + 2LL * H * kAttnDh;
+  // V rows as 16-byte vectors, all four loads of a lane in flight together, then transposed into LDS
+  bf16x8_t vv[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int t = lane + 64 * u, kk = t >> 3;
+    vv[u] = kk < S ? *reinterpret_cast<const bf16x8_t *>(vb + kk * tok + 8 * (t & 7)) : bf16x8_t{};
+  }
+  bf16x8_t qf[2][2], kf[2][2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+      const int r = 16 * t + c;
+      const int d0 = 32 * st + 8 * g;
+      qf[t][st] = r < S ? *reinterpret_cast<const bf16x8_t *>(base + r * tok + d0) : bf16x8_t{};
+      kf[t][st] = r < S ? *reinterpret_cast<const bf16x8_t *>(kb + r * tok + d0) : bf16x8_t{};
+    }
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int t = lane + 64 * u, kk = t >> 3, d0 = 8 * (t & 7);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) vt[(d0 + e) * VT + kk] = vv[u][e];
+  }
+  f32x4_t sc[2][2];  // [key tile][query tile]
+#pragma unroll
+  for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+      f32x4_t a = {0.f, 0.f, 0.f, 0.f};
+      a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[kt][0], qf[it][0], a, 0, 0, 0);
+      a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[kt][1], qf[it][1], a, 0, 0, 0);
+      sc[kt][it] = a;
+    }
+  bf16x8_t pa[2];
+#pragma unroll
+  for (int it = 0; it < 2; ++it) {
+    float v[8];
+    float m = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int kt = j >> 2, r = j & 3;
+      const int kk = 16 * kt + 4 * g + r;
+      v[j] = kk < S ? sc[kt][it][r] * scale : -INFINITY;
+      m = fmaxf(m, v[j]);
+    }
+    m = fmaxf(m, __shfl_xor(m, 16));
+    m = fmaxf(m, __shfl_xor(m, 32));
+    float sum = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      v[j] = v[j] == -INFINITY ? 0.f : __expf(v[j] - m);
+      sum += v[j];
+    }
+    sum += __shfl_xor(sum, 16);
+    sum += __shfl_xor(sum, 32);
+    const float inv = 1.f / sum;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) pa[it][j] = (__bf16)(v[j] * inv);
+  }
+  __syncthreads();  // V^T staged
+#pragma unroll
+  for (int dt = 0; dt < kAttnDh / 16; ++dt) {
+    const int d = 16 * dt + c;
+    bf16x8_t vf;
+    const uint2 lo = *reinterpret_cast<const uint2 *>(&vt[d * VT + 4 * g]);
+    const uint2 hi = *reinterpret_cast<const uint2 *>(&vt[d * VT + 16 + 4 * g]);
+    const uint4 w = make_uint4(lo.x, lo.y, hi.x, hi.y);
+    vf = *reinterpret_cast<const bf16x8_t *>(&w);
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+      f32x4_t o = {0.f, 0.f, 0.f, 0.f};
+      o = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa[it], vf, o, 0, 0, 0);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int i = 16 * it + 4 * g + r;
+        if (i < S) out[(b * S + i) * (int64_t)H * kAttnDh + (int64_t)h * kAttnDh + d] = __float2bfloat16(o[r]);
+      }
+    }
+  }
+}
+
 }  // namespace cm
 
 using namespace cm;
@@ -151,4 +344,31 @@ extern "C" int cm_add_layernorm(const void *x_dev, const void *r_dev, int64_t r_
       return launch_add_ln<__hip_bfloat16>(x_dev, r_dev, r_rows, gamma_dev, beta_dev, rows, D, eps, out_dev, st);
     default: CM_FAIL(CM_EINVAL, "dtype must be f32/bf16");
   }
+}
+
+extern "C" int cm_short_attention(const void *qkv_dev, int32_t B, int32_t S, int32_t H, int32_t head_dim, float scale,
+                                  int32_t dtype, void *out_dev, void *stream) {
+  if (B <= 0) return CM_OK;
+  if (!qkv_dev || !out_dev) CM_FAIL(CM_EINVAL, "NULL argument");
+  if (head_dim != kAttnDh) CM_FAIL(CM_EINVAL, "head_dim must be 64");
+  if (S <= 0 || S > kAttnMaxS || H <= 0) CM_FAIL(CM_EINVAL, "need 0 < S <= 64 and H > 0");
+  hipStream_t st = (hipStream_t)stream;
+  const dim3 grid((unsigned)((int64_t)B * H)), block(64);
+  switch (dtype) {
+    case CM_DTYPE_F32:
+      hipLaunchKernelGGL(short_attention_kernel<float>, grid, block, 0, st, (const float *)qkv_dev, S, H, scale,
+                         (float *)out_dev);
+      break;
+    case CM_DTYPE_BF16:
+      if (S <= 32)
+        hipLaunchKernelGGL(short_attention_mfma_kernel, grid, block, 0, st, (const __hip_bfloat16 *)qkv_dev, S, H,
+                           scale, (__hip_bfloat16 *)out_dev);
+      else
+        hipLaunchKernelGGL(short_attention_kernel<__hip_bfloat16>, grid, block, 0, st, (const __hip_bfloat16 *)qkv_dev,
+                           S, H, scale, (__hip_bfloat16 *)out_dev);
+      break;
+    default: CM_FAIL(CM_EINVAL, "dtype must be f32/bf16");
+  }
+  CM_HIP(hipGetLastError());
+  return CM_OK;
 }

@@ -275,6 +275,13 @@ int cm_add_layernorm(const void *x_dev, const void *r_dev, int64_t r_rows, const
                      const void *beta_dev, int64_t rows, int32_t D, float eps, int32_t dtype, void *out_dev,
                      void *stream);
 
+/* Self-attention of an unpadded short batch (HF XLMRobertaSelfAttention with an all-ones
+ * mask, as run by E5MultilingualEmbedder.encode_queries): qkv_dev is the fused Q/K/V
+ * projection output B x S x 3 x H x head_dim, out_dev receives softmax(q k^T * scale) v as
+ * B x S x (H * head_dim).  head_dim must be 64, 0 < S <= 64; dtype F32 or BF16.   */
+int cm_short_attention(const void *qkv_dev, int32_t B, int32_t S, int32_t H, int32_t head_dim, float scale,
+                       int32_t dtype, void *out_dev, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -518,3 +518,22 @@ def test_e5_lean_forward_fp32_matches_hf():
     graph.replay()
     torch.cuda.synchronize()
     torch.testing.assert_close(u_out, emb.encode_token_ids(ids, mask), atol=2e-5, rtol=0)
+
+
+@pytest.mark.parametrize("S", [1, 7, 16, 24, 32, 33, 64])
+def test_short_attention_matches_torch(eng, S):
+    """cm_short_attention == per-head softmax(q k^T / 8) v on the (B, S, 3, H, 64) QKV layout
+    (torch fp32 reference)."""
+    import torch
+    torch.manual_seed(S)
+    B, H = 37, 12
+    for dt, tol in ((torch.float32, 2e-5), (torch.bfloat16, 1e-2)):
+        qkv = (2 * torch.randn(B, S, 3 * H * 64, device="cuda")).to(dt)
+        q, k, v = qkv.float().view(B, S, 3, H, 64).permute(2, 0, 3, 1, 4)
+        ref = torch.softmax(q @ k.transpose(-1, -2) / 8.0, dim=-1) @ v
+        ref = ref.transpose(1, 2).reshape(B, S, H * 64)
+        out = eng.short_attention(qkv, H, 1 / 8.0)
+        assert out.dtype == dt and out.shape == (B, S, H * 64)
+        torch.testing.assert_close(out.float(), ref, atol=tol, rtol=tol)
+    with pytest.raises(ValueError):
+        eng.short_attention(torch.zeros(2, 65, 3 * H * 64, device="cuda"), H, 0.125)

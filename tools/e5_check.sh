@@ -1,6 +1,6 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"; mkdir -p gpurun_out/e5; export TMPDIR=/tmp
-timeout -k 10 300 python -u -m pytest tests/test_gpu_engine.py tests/test_gpu_dropin.py -x -q --timeout 120 --timeout-method thread -k "layernorm or e5" > gpurun_out/e5/pytest.log 2>&1 || { tail -30 gpurun_out/e5/pytest.log; exit 1; }
+timeout -k 10 300 python -u -m pytest tests/test_gpu_engine.py tests/test_gpu_dropin.py -x -q --timeout 120 --timeout-method thread -k "layernorm or e5 or attention" > gpurun_out/e5/pytest.log 2>&1 || { tail -30 gpurun_out/e5/pytest.log; exit 1; }
 tail -2 gpurun_out/e5/pytest.log
 timeout -k 10 200 python -u tools/e5_probe.py > gpurun_out/e5/fused.log 2>&1 || { tail -20 gpurun_out/e5/fused.log; exit 1; }
 grep "graph unpadded=True" gpurun_out/e5/fused.log
