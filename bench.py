@@ -64,6 +64,8 @@ def parse_args():
     ap.add_argument("--no-e5", action="store_true", help="use perturbed corpus rows as query embeddings")
     ap.add_argument("--no-graph", action="store_true", help="run the E5 query encode eagerly (no hipGraph)")
     ap.add_argument("--serial", action="store_true", help="run BM25 on the main stream (no overlap with E5 + dense)")
+    ap.add_argument("--bm25-priority", type=int, default=0, help="HIP stream priority of the BM25 stream (-1 = high)")
+    ap.add_argument("--bm25-after-e5", action="store_true", help="launch BM25 after the E5 encode (overlap with dense)")
     ap.add_argument("--seq-len", type=int, default=256, help="ingest mode: tokens per chunk")
     ap.add_argument("--cpu-baseline", type=int, default=1)
     ap.add_argument("--cpu-queries", type=int, default=64)
@@ -200,7 +202,8 @@ def main():
     ev = []
 
     main = torch.cuda.current_stream(dev)
-    side = torch.cuda.Stream(device=dev) if (bm25 is not None and not args.serial) else main
+    side = (torch.cuda.Stream(device=dev, priority=args.bm25_priority)
+            if (bm25 is not None and not args.serial) else main)
 
     def run_bm25(e):
         # BM25 needs only the query term ids: it runs on its own stream, overlapping the E5
@@ -215,7 +218,7 @@ def main():
 
     def step(record=False):
         e = [torch.cuda.Event(enable_timing=True) for _ in range(4)] if record else None
-        if bm25 is not None:
+        if bm25 is not None and not args.bm25_after_e5:
             side.wait_stream(main)          # previous step's fusion has read bout
             bs, br = run_bm25(e)
         if use_e5:
@@ -226,6 +229,9 @@ def main():
                 q = emb.encode_token_ids(ids, mask, out=qbuf)
         else:
             q = qfix
+        if bm25 is not None and args.bm25_after_e5:
+            side.wait_stream(main)
+            bs, br = run_bm25(e)
         if record:
             e[0].record()
         d, r = dense.search_dev(q, P, out=dout, workspace=dws)
