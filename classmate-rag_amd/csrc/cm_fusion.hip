@@ -92,6 +92,82 @@ __global__ void __launch_bounds__(kMmrThreads) mmr_kernel(const float *__restric
   }
 }
 
+// Same MMR for pools of <= kMmrLdsPool items (the retriever's 24): the pool and the query are
+// staged in LDS with all loads in flight, the (n + 1) x n similarity table is computed at once
+// (one exact fp64 dot per thread, rounded once to fp32 as above, so the values are the ones
+// mmr_kernel computes), and one wave runs the greedy loop on registers + shuffles with no
+// block barriers: first max wins ties (strict '>' in ascending index order).
+constexpr int kMmrLdsPool = 32;
+constexpr int kMmrLdsDim = 1024;
+
+__global__ void __launch_bounds__(kMmrThreads) mmr_lds_kernel(const float *__restrict__ q, const float *__restrict__ cands,
+                                                              const int32_t *__restrict__ n_valid, int pool, int dim,
+                                                              int k, float lam32, float oml32,
+                                                              int32_t *__restrict__ out_order) {
+  extern __shared__ __attribute__((aligned(16))) float mm_lds[];
+  const int ld = dim + 1;                       // row pitch: rows start in different banks
+  float *rows = mm_lds;                         // [n + 1][ld]: pool rows, then the query
+  float *sim = mm_lds + (kMmrLdsPool + 1) * ld;  // [n + 1][kMmrLdsPool]: row n = sims_q
+  const int qi = blockIdx.x;
+  const int n = min(n_valid ? n_valid[qi] : pool, pool);
+  const int kk = min(k, n);
+  for (int i = threadIdx.x; i < k; i += kMmrThreads) out_order[(int64_t)qi * k + i] = -1;
+  if (n <= 0) return;  // uniform
+  const float *cv = cands + (int64_t)qi * pool * dim;
+  const float *qv = q + (int64_t)qi * dim;
+  for (int t = threadIdx.x; t < (n + 1) * dim; t += kMmrThreads) {
+    const int r = t / dim, d = t - r * dim;
+    rows[r * ld + d] = r < n ? cv[(int64_t)r * dim + d] : qv[d];
+  }
+  __syncthreads();
+  // pairs (i, j), i <= n (row n = the query), j < n, j <= i or i == n
+  for (int p = threadIdx.x; p < (n + 1) * n; p += kMmrThreads) {
+    const int i = p / n, j = p - i * n;
+    if (i < n && j > i) continue;
+    const float *a = rows + i * ld;
+    const float *b = rows + j * ld;
+    double acc = 0.0;
+    for (int d = 0; d < dim; ++d) acc += (double)a[d] * (double)b[d];
+    const float v = (float)acc;
+    sim[i * kMmrLdsPool + j] = v;
+    if (i < n) sim[j * kMmrLdsPool + i] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x >= 64) return;
+  const int lane = threadIdx.x;
+  const bool have = lane < n;
+  const float sq = have ? sim[n * kMmrLdsPool + lane] : -INFINITY;
+  bool sel = false;
+  float maxdiv = -INFINITY;
+  // argmax(sims_q), first maximum
+  auto wave_best = [&](float v, bool ok) {
+    int bi = ok ? lane : 0x7fffffff;
+    float bv = ok ? v : -INFINITY;
+    for (int o = 32; o > 0; o >>= 1) {
+      const float ov = __shfl_xor(bv, o);
+      const int oi = __shfl_xor(bi, o);
+      if (ov > bv || (ov == bv && oi < bi)) {
+        bv = ov;
+        bi = oi;
+      }
+    }
+    return bi;
+  };
+  int cur = wave_best(sq, have);
+  if (lane == cur) sel = true;
+  if (lane == 0) out_order[(int64_t)qi * k] = cur;
+  for (int step = 1; step < kk; ++step) {
+    if (have && !sel) maxdiv = fmaxf(maxdiv, sim[lane * kMmrLdsPool + cur]);
+    const float a = lam32 * sq;
+    const float b = oml32 * maxdiv;
+    const float sc = a - b;
+    cur = wave_best(sc, have && !sel && sc > -1e9f);
+    if (cur == 0x7fffffff) break;  // mmr_kernel would emit -1 here too (no candidate beats -1e9)
+    if (lane == cur) sel = true;
+    if (lane == 0) out_order[(int64_t)qi * k + step] = cur;
+  }
+}
+
 // HybridRetriever.retrieve's merge for one query per lane.
 __global__ void rrf_merge_kernel(const int64_t *__restrict__ vkeys, const float *__restrict__ vdist,
                                  const int32_t *__restrict__ vn, int kv, const int64_t *__restrict__ bkeys,
@@ -263,6 +339,18 @@ int cm_mmr_dev(const float *q_dev, const float *cands_dev, const int32_t *n_vali
   if (dim <= 0 || k <= 0) CM_FAIL(CM_EINVAL, "bad MMR arguments");
   const float lam32 = (float)lambd;
   const float oml32 = (float)(1.0 - lambd);
+  if (pool <= kMmrLdsPool && dim <= kMmrLdsDim) {
+    const size_t lds = ((size_t)(kMmrLdsPool + 1) * (dim + 1) + (size_t)(kMmrLdsPool + 1) * kMmrLdsPool) * 4;
+    static const hipError_t attr =
+        hipFuncSetAttribute(reinterpret_cast<const void *>(&mmr_lds_kernel),
+                            hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)(((kMmrLdsPool + 1) * (kMmrLdsDim + 1) + (kMmrLdsPool + 1) * kMmrLdsPool) * 4));
+    CM_HIP(attr);
+    hipLaunchKernelGGL(mmr_lds_kernel, dim3(nq), dim3(kMmrThreads), lds, (hipStream_t)stream, q_dev, cands_dev,
+                       n_valid_dev, pool, dim, k, lam32, oml32, order_dev);
+    CM_HIP(hipGetLastError());
+    return CM_OK;
+  }
   hipLaunchKernelGGL(mmr_kernel, dim3(nq), dim3(kMmrThreads), 0, (hipStream_t)stream, q_dev, cands_dev, n_valid_dev,
                      pool, dim, k, lam32, oml32, order_dev);
   CM_HIP(hipGetLastError());

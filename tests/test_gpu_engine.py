@@ -537,3 +537,24 @@ def test_short_attention_matches_torch(eng, S):
         torch.testing.assert_close(out.float(), ref, atol=tol, rtol=tol)
     with pytest.raises(ValueError):
         eng.short_attention(torch.zeros(2, 65, 3 * H * 64, device="cuda"), H, 0.125)
+
+
+@pytest.mark.parametrize("pool", [24, 32, 33, 48])
+def test_mmr_small_and_large_pools_match_oracle(eng, pool):
+    """Pools <= 32 run the LDS-staged MMR kernel, larger ones the streaming kernel: both give the
+    reference's greedy order (oracle: rag/retrieval/fusion.py:39-61 restated)."""
+    rng = np.random.default_rng(pool)
+    nq, dim = 40, 768
+    q = rng.standard_normal((nq, dim)).astype(np.float32)
+    q /= np.linalg.norm(q, axis=1, keepdims=True)
+    base = q[:, None, :] + 0.9 * rng.standard_normal((nq, pool, dim)).astype(np.float32) / np.sqrt(dim)
+    cands = (base / np.linalg.norm(base, axis=2, keepdims=True)).astype(np.float32)
+    nv = rng.integers(0, pool + 1, nq).astype(np.int32)
+    nv[:4] = pool
+    for k, lam in ((10, 0.5), (pool + 3, 0.3)):
+        order = eng.mmr_order_batch(q, cands, k, lam, n_valid=nv)
+        for i in range(nq):
+            n = int(nv[i])
+            want = orc.mmr_order(q[i], cands[i][:n], list(range(n)), k, lam)
+            assert order[i][: len(want)].tolist() == want, (i, n, k)
+            assert (order[i][len(want):] == -1).all()
