@@ -200,6 +200,26 @@ class E5MultilingualEmbedder:
         self._lean = fwd
         return fwd
 
+    @staticmethod
+    def _tuned_gemms() -> bool:
+        """Load the TunableOp table of hipBLASLt solutions measured on MI355X for the E5 GEMM
+        shapes of a 256 x 24-token query batch (tunableop_e5_gfx950.csv; tools/tune_probe.sh
+        regenerates it).  Lookup only (no tuning at run time, untuned shapes keep hipBLASLt's
+        default); results are written, if ever, to a temp file, never into the package.
+        CM_E5_TUNABLEOP=0 disables it."""
+        if os.environ.get("CM_E5_TUNABLEOP", "1") == "0":
+            return False
+        import tempfile
+        import torch.cuda.tunable as tun
+        table = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tunableop_e5_gfx950.csv")
+        if not os.path.exists(table):
+            return False
+        tun.tuning_enable(False)
+        tun.record_untuned_enable(False)
+        tun.set_filename(os.path.join(tempfile.gettempdir(), f"cm_tunableop_{os.getpid()}.csv"))
+        tun.enable(True)
+        return bool(tun.read_file(table))
+
     def capture_graph(self, batch: int, seq_len: int, unpadded: bool = False):
         """HIP-graph the device encode for a fixed (batch, seq_len) (hipGraph via torch.cuda.CUDAGraph:
         one replay instead of ~200 small launches per batch).  Returns (ids, mask, out, graph): fill
@@ -214,6 +234,7 @@ class E5MultilingualEmbedder:
         out = torch.empty((batch, self.model.config.hidden_size), dtype=torch.float32, device=dev)
 
         lean = self._lean_forward() if unpadded else None
+        self.tuned_gemms = self._tuned_gemms()
 
         def fwd():
             if lean is not None:
