@@ -13,6 +13,7 @@ namespace cm {
 
 constexpr int kMmrThreads = 256;
 constexpr int kMmrMaxPool = 256;
+constexpr int kRrfLdsCap = 32;  // kv + kb up to which rrf_merge_kernel keeps its lists in LDS (57 KB)
 
 // fp32 dot computed in fp64 and rounded once (closest fp32 to the exact dot).
 __device__ inline float wave_dot(const float *__restrict__ a, const float *__restrict__ b, int dim, int lane) {
@@ -169,6 +170,7 @@ __global__ void __launch_bounds__(kMmrThreads) mmr_lds_kernel(const float *__res
 }
 
 // HybridRetriever.retrieve's merge for one query per lane.
+template <bool kLds>
 __global__ void rrf_merge_kernel(const int64_t *__restrict__ vkeys, const float *__restrict__ vdist,
                                  const int32_t *__restrict__ vn, int kv, const int64_t *__restrict__ bkeys,
                                  const double *__restrict__ bscore, const int32_t *__restrict__ bn, int kb, int nq,
@@ -178,23 +180,29 @@ __global__ void rrf_merge_kernel(const int64_t *__restrict__ vkeys, const float 
                                  int32_t *__restrict__ out_n, int64_t *__restrict__ scratch_keys,
                                  double *__restrict__ scratch_f, double *__restrict__ scratch_v,
                                  int32_t *__restrict__ scratch_src) {
+  // per-query work arrays: this lane's slice of LDS (element j at [j * 64], no global round
+  // trips; kv + kb <= kRrfLdsCap) or, for longer lists, the caller's global scratch (stride 1)
+  extern __shared__ __attribute__((aligned(16))) unsigned char rrf_lds[];
   const int qi = blockIdx.x * blockDim.x + threadIdx.x;
   if (qi >= nq) return;
   const int nv = vn ? min(vn[qi], kv) : kv;
   const int nb = bn ? min(bn[qi], kb) : kb;
   const int cap = kv + kb;
-  int64_t *key = scratch_keys + (int64_t)qi * cap;
-  double *fused = scratch_f + (int64_t)qi * cap;
-  double *vdt = scratch_v + (int64_t)qi * cap;
-  int32_t *src = scratch_src + (int64_t)qi * cap;  // bit0: vec index+1 in low 16, bit16..: bm index+1
+  const int ln = threadIdx.x;
+  constexpr int ST = kLds ? 64 : 1;
+  int64_t *key = kLds ? reinterpret_cast<int64_t *>(rrf_lds) + ln : scratch_keys + (int64_t)qi * cap;
+  double *fused = kLds ? reinterpret_cast<double *>(rrf_lds + (size_t)cap * 64 * 8) + ln : scratch_f + (int64_t)qi * cap;
+  double *vdt = kLds ? reinterpret_cast<double *>(rrf_lds + (size_t)cap * 64 * 16) + ln : scratch_v + (int64_t)qi * cap;
+  // bit0: vec index+1 in low 16, bit16..: bm index+1
+  int32_t *src = kLds ? reinterpret_cast<int32_t *>(rrf_lds + (size_t)cap * 64 * 24) + ln : scratch_src + (int64_t)qi * cap;
   int m = 0;
   // by_id in insertion order: vector items (MMR order), then BM25-only items.
   for (int r = 0; r < nv; ++r) {
     const int64_t id = vkeys[(int64_t)qi * kv + r];
-    key[m] = id;
-    fused[m] = 0.0 + w_vec * (1.0 / (double)(rrf_k + (r + 1)));
-    vdt[m] = -(double)vdist[(int64_t)qi * kv + r];
-    src[m] = (r + 1);
+    key[(m) * ST] = id;
+    fused[(m) * ST] = 0.0 + w_vec * (1.0 / (double)(rrf_k + (r + 1)));
+    vdt[(m) * ST] = -(double)vdist[(int64_t)qi * kv + r];
+    src[(m) * ST] = (r + 1);
     ++m;
   }
   for (int r = 0; r < nb; ++r) {
@@ -202,47 +210,47 @@ __global__ void rrf_merge_kernel(const int64_t *__restrict__ vkeys, const float 
     const double c = w_bm25 * (1.0 / (double)(rrf_k + (r + 1)));
     int f = -1;
     for (int j = 0; j < nv; ++j)
-      if (key[j] == id) {
+      if (key[(j) * ST] == id) {
         f = j;
         break;
       }
     if (f >= 0) {
-      fused[f] = fused[f] + c;
-      src[f] |= (r + 1) << 16;
+      fused[(f) * ST] = fused[(f) * ST] + c;
+      src[(f) * ST] |= (r + 1) << 16;
     } else {
-      key[m] = id;
-      fused[m] = 0.0 + c;
-      vdt[m] = -0.0;
-      src[m] = (r + 1) << 16;
+      key[(m) * ST] = id;
+      fused[(m) * ST] = 0.0 + c;
+      vdt[(m) * ST] = -0.0;
+      src[(m) * ST] = (r + 1) << 16;
       ++m;
     }
   }
   // stable insertion sort by (fused, vd_term) descending
   for (int i = 1; i < m; ++i) {
-    const int64_t k0 = key[i];
-    const double f0 = fused[i], v0 = vdt[i];
-    const int32_t s0 = src[i];
+    const int64_t k0 = key[(i) * ST];
+    const double f0 = fused[(i) * ST], v0 = vdt[(i) * ST];
+    const int32_t s0 = src[(i) * ST];
     int j = i - 1;
-    while (j >= 0 && (fused[j] < f0 || (fused[j] == f0 && vdt[j] < v0))) {
-      key[j + 1] = key[j];
-      fused[j + 1] = fused[j];
-      vdt[j + 1] = vdt[j];
-      src[j + 1] = src[j];
+    while (j >= 0 && (fused[(j) * ST] < f0 || (fused[(j) * ST] == f0 && vdt[(j) * ST] < v0))) {
+      key[(j + 1) * ST] = key[(j) * ST];
+      fused[(j + 1) * ST] = fused[(j) * ST];
+      vdt[(j + 1) * ST] = vdt[(j) * ST];
+      src[(j + 1) * ST] = src[(j) * ST];
       --j;
     }
-    key[j + 1] = k0;
-    fused[j + 1] = f0;
-    vdt[j + 1] = v0;
-    src[j + 1] = s0;
+    key[(j + 1) * ST] = k0;
+    fused[(j + 1) * ST] = f0;
+    vdt[(j + 1) * ST] = v0;
+    src[(j + 1) * ST] = s0;
   }
   const int n_out = min(m, top_k);
   for (int i = 0; i < top_k; ++i) {
     const int64_t o = (int64_t)qi * top_k + i;
     if (i < n_out) {
-      const int vi = (src[i] & 0xffff) - 1;
-      const int bi = (src[i] >> 16) - 1;
-      out_keys[o] = key[i];
-      out_fused[o] = fused[i];
+      const int vi = (src[(i) * ST] & 0xffff) - 1;
+      const int bi = (src[(i) * ST] >> 16) - 1;
+      out_keys[o] = key[(i) * ST];
+      out_fused[o] = fused[(i) * ST];
       out_vdist[o] = vi >= 0 ? vdist[(int64_t)qi * kv + vi] : 0.f;
       out_bscore[o] = bi >= 0 ? bscore[(int64_t)qi * kb + bi] : 0.0;
       out_flags[o] = (vi >= 0 ? 1 : 0) | (bi >= 0 ? 2 : 0);
@@ -417,9 +425,14 @@ int cm_rrf_merge_dev(const int64_t *vkeys, const float *vdist, const int32_t *vn
   double *sf = c.take<double>((size_t)nq * cap);
   double *sv = c.take<double>((size_t)nq * cap);
   int32_t *ss = c.take<int32_t>((size_t)nq * cap);
-  hipLaunchKernelGGL(rrf_merge_kernel, dim3((unsigned)ceil_div(nq, 64)), dim3(64), 0, (hipStream_t)stream, vkeys,
-                     vdist, vn, kv, bkeys, bscore, bn, kb, nq, w_vec, w_bm25, rrf_k, top_k, out_keys, out_fused,
-                     out_vdist, out_bscore, out_flags, out_n, sk, sf, sv, ss);
+  if (cap <= kRrfLdsCap)
+    hipLaunchKernelGGL(rrf_merge_kernel<true>, dim3((unsigned)ceil_div(nq, 64)), dim3(64), (size_t)cap * 64 * 28,
+                       (hipStream_t)stream, vkeys, vdist, vn, kv, bkeys, bscore, bn, kb, nq, w_vec, w_bm25, rrf_k,
+                       top_k, out_keys, out_fused, out_vdist, out_bscore, out_flags, out_n, sk, sf, sv, ss);
+  else
+    hipLaunchKernelGGL(rrf_merge_kernel<false>, dim3((unsigned)ceil_div(nq, 64)), dim3(64), 0, (hipStream_t)stream,
+                       vkeys, vdist, vn, kv, bkeys, bscore, bn, kb, nq, w_vec, w_bm25, rrf_k, top_k, out_keys,
+                       out_fused, out_vdist, out_bscore, out_flags, out_n, sk, sf, sv, ss);
   CM_HIP(hipGetLastError());
   return CM_OK;
 }

@@ -558,3 +558,23 @@ def test_mmr_small_and_large_pools_match_oracle(eng, pool):
             want = orc.mmr_order(q[i], cands[i][:n], list(range(n)), k, lam)
             assert order[i][: len(want)].tolist() == want, (i, n, k)
             assert (order[i][len(want):] == -1).all()
+
+
+def test_rrf_merge_lds_and_global_paths_agree(eng):
+    """kv + kb <= 32 keeps the RRF merge lists in LDS, longer lists use global scratch: the same
+    valid items give the same fused lists (bit-identical) on both paths."""
+    rng = np.random.default_rng(7)
+    nq = 300
+    vk = np.stack([rng.choice(60, 20, replace=False) for _ in range(nq)]).astype(np.int64)
+    bk = np.stack([rng.choice(60, 20, replace=False) for _ in range(nq)]).astype(np.int64)
+    vd = rng.random((nq, 20)).astype(np.float32)
+    vd[:, 3] = vd[:, 2]                                     # equal distances: tie order
+    bs = rng.standard_normal((nq, 20))
+    vn = rng.integers(0, 17, nq).astype(np.int32)
+    bn = rng.integers(0, 17, nq).astype(np.int32)
+    kw = dict(w_vec=1.0, w_bm25=0.7, rrf_k=60, top_k=12)
+    small = eng.rrf_merge(vk[:, :16].copy(), vd[:, :16].copy(), vn, bk[:, :16].copy(), bs[:, :16].copy(), bn, **kw)
+    large = eng.rrf_merge(vk, vd, vn, bk, bs, bn, **kw)
+    for a, b in zip(small, large):
+        assert np.array_equal(np.asarray(a), np.asarray(b))
+    assert int(np.asarray(small[-1]).max()) > 0
