@@ -131,8 +131,10 @@ def main():
     import torch
     from classmate_hip import engine, parallel
 
-    rank, ws = parallel.init_from_env()
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    # CM_DIST_BACKEND=gloo + CM_BENCH_DEVICE=0: rehearse the N>1 path with every rank on one GPU
+    # (RCCL refuses two ranks per device); the driver's multi-GPU runs use the defaults
+    rank, ws = parallel.init_from_env(os.environ.get("CM_DIST_BACKEND") or None)
+    local = int(os.environ.get("CM_BENCH_DEVICE", os.environ.get("LOCAL_RANK", "0")))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if args.gpus != ws:
