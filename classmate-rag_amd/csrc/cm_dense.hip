@@ -1079,15 +1079,19 @@ __global__ void __launch_bounds__(256) dense_rerank_kernel(
     }
     return;  // the K1b pass writes this query's results
   }
-  // 2. gather the candidates
-  for (int b = wave; b < n_wg; b += 4) {
-    const uint32_t o = s_off[b], c = s_off[b + 1] - o;
-    const uint64_t *src = keys + (((int64_t)qp * n_wg + b) * kBQPass + ql) * kCBufCap;
-    for (uint32_t i = lane; i < c; i += 64) {
-      const uint64_t key = src[i];
-      s_keys[o + i] = key;
-      s_dist[o + i] = (uint32_t)(key >> 32);
+  // 2. gather the candidates: thread per candidate slot j (its buffer = the last b with
+  // s_off[b] <= j; empty buffers share offsets), so every load is independent instead of one
+  // global round trip per buffer and wave
+  for (int j = tid; j < total; j += 256) {
+    int lo = 0, hi = n_wg - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (s_off[mid] <= (uint32_t)j) lo = mid;
+      else hi = mid - 1;
     }
+    const uint64_t key = keys[(((int64_t)qp * n_wg + lo) * kBQPass + ql) * kCBufCap + (j - s_off[lo])];
+    s_keys[j] = key;
+    s_dist[j] = (uint32_t)(key >> 32);
   }
   for (int i = tid; i < dim; i += 256) s_q[i] = q[(int64_t)qi * dim + i];
   __syncthreads();
