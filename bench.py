@@ -61,6 +61,10 @@ def parse_args():
     ap.add_argument("--q-terms", type=int, default=8)
     ap.add_argument("--q-tokens", type=int, default=24)
     ap.add_argument("--e5-layers", type=int, default=12)
+    ap.add_argument("--e5-dtype", choices=["bfloat16", "float32"], default="bfloat16",
+                    help="E5 forward dtype of the headline step (the drop-in default is float32)")
+    ap.add_argument("--e5-fp32-leg", type=int, default=1,
+                    help="also time the step with the reference-precision fp32 E5 forward (reported as e5_fp32)")
     ap.add_argument("--no-e5", action="store_true", help="use perturbed corpus rows as query embeddings")
     ap.add_argument("--no-graph", action="store_true", help="run the E5 query encode eagerly (no hipGraph)")
     ap.add_argument("--serial", action="store_true", help="run BM25 on the main stream (no overlap with E5 + dense)")
@@ -125,8 +129,15 @@ def sample_query_terms(tokens, doc_off, B, q_terms, seed):
 
 
 # ---------------------------------------------------------------------------
+ABLATION_ENV = ("CM_DENSE_DEBUG", "CM_BM25_DEBUG")
+KNOB_ENV = ("CM_DENSE_PATH", "CM_E5_FUSED_LN", "CM_E5_FUSED_ATTN", "CM_E5_TUNABLEOP", "CM_E5_DTYPE")
+
+
 def main():
     args = parse_args()
+    bad = [e for e in ABLATION_ENV if os.environ.get(e, "0") not in ("", "0")]
+    if bad:   # timing ablations skip work; the product library ignores them, refuse anyway
+        sys.exit(f"bench.py: refusing to run with ablation switches set: {bad}")
     import numpy as np
     import torch
     from classmate_hip import engine, parallel
@@ -176,18 +187,24 @@ def main():
     emb = None
     if use_e5:
         from classmate_hip.embeddings import E5MultilingualEmbedder
-        emb = E5MultilingualEmbedder.random_init(seed=0, device=str(dev), num_layers=args.e5_layers)
         g = torch.Generator(device="cuda").manual_seed(args.seed * 13)
         ids = torch.randint(5, 250002, (B, args.q_tokens), device=dev, generator=g)
         ids[:, 0] = 0
         ids[:, -1] = 2
         mask = torch.ones_like(ids)
-        qbuf = torch.empty((B, D), dtype=torch.float32, device=dev)
-        graph = None
-        if not args.no_graph:   # one hipGraph replay per batch instead of ~200 launches
-            g_ids, g_mask, qbuf, graph = emb.capture_graph(B, args.q_tokens, unpadded=True)  # fixed-length queries
+
+        def make_e5(dtype):
+            """E5 query encoder of one dtype: (embedder, graph or None, output buffer)."""
+            m = E5MultilingualEmbedder.random_init(seed=0, device=str(dev), num_layers=args.e5_layers, dtype=dtype)
+            if args.no_graph:
+                return m, None, torch.empty((B, D), dtype=torch.float32, device=dev)
+            # one hipGraph replay per batch instead of ~200 launches (fixed-length queries: lean forward)
+            g_ids, g_mask, out_buf, gr = m.capture_graph(B, args.q_tokens, unpadded=True)
             g_ids.copy_(ids)
             g_mask.copy_(mask)
+            return m, gr, out_buf
+
+        e5 = dict(zip(("emb", "graph", "qbuf"), make_e5(args.e5_dtype)))
     else:
         g = torch.Generator(device="cuda").manual_seed(args.seed * 17)
         qfix = torch.randn(B, D, device=dev, generator=g)
@@ -224,11 +241,11 @@ def main():
             side.wait_stream(main)          # previous step's fusion has read bout
             bs, br = run_bm25(e)
         if use_e5:
-            if graph is not None:
-                graph.replay()
-                q = qbuf
+            if e5["graph"] is not None:
+                e5["graph"].replay()
+                q = e5["qbuf"]
             else:
-                q = emb.encode_token_ids(ids, mask, out=qbuf)
+                q = e5["emb"].encode_token_ids(ids, mask, out=e5["qbuf"])
         else:
             q = qfix
         if bm25 is not None and args.bm25_after_e5:
@@ -299,6 +316,31 @@ def main():
     fallbacks = dense.workspace_fallbacks(B, P, dws)
     rescored = bm25.workspace_rescored(B, q_terms.numel(), K, bws) if bm25 is not None else None
     qps = B * args.steps / elapsed
+    e5_fp32 = None
+    if use_e5 and args.e5_fp32_leg and args.e5_dtype != "float32":
+        # the same step with the reference-precision fp32 E5 forward (rag/embeddings/__init__.py:87-94)
+        dense.timing(False)
+        if bm25 is not None:
+            bm25.timing(False)
+        main_e5 = e5
+        e5 = dict(zip(("emb", "graph", "qbuf"), make_e5("float32")))
+        for _ in range(args.warmup):
+            step()
+        torch.cuda.synchronize()
+        if ws > 1:
+            torch.distributed.barrier()
+        t1 = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        torch.cuda.synchronize()
+        if ws > 1:
+            torch.distributed.barrier()
+        el32 = parallel.max_over_ranks(time.perf_counter() - t1, device=dev)
+        e5_fp32 = {"value": B * args.steps / el32, "unit": "queries/s", "ms_per_step": el32 / args.steps * 1e3,
+                   "e5_forward": "float32"}
+        log(f"fp32 E5 leg: {e5_fp32['value']:.1f} q/s ({e5_fp32['ms_per_step']:.3f} ms/step)")
+        del e5
+        e5 = main_e5
     log(f"{args.steps} steps in {elapsed:.3f}s -> {qps:.1f} q/s; dense search {search_ms:.3f} ms "
         f"(scan kernel {dense_ms:.3f} ms, {DENSE_KINDS[kind]}, {fallbacks} exact re-runs)"
         + (f", bm25 search {bsearch_ms:.3f} ms (K2a tail pass {bm25_ms:.3f} ms, {rescored} (query, range) pairs "
@@ -317,7 +359,8 @@ def main():
         "vs_baseline": None, "dtype": "f16+f64",
         "dtypes": {"dense_knn": {1: "f32 (MFMA)", 2: "f16x3 split (MFMA, f32-grade)",
                                  3: "f16 coarse (MFMA) + fp64 exact re-rank of the certified band"}[kind],
-                   "bm25": "f64", "e5_forward": "bf16" if use_e5 else None, "fusion": "f64"},
+                   "bm25": "f64", "e5_forward": args.e5_dtype if use_e5 else None, "fusion": "f64"},
+        "e5_fp32": e5_fp32,
         "data": "synthetic (seeded): unit-norm Gaussian chunk embeddings, Zipf BM25 postings, random-init "
                 "E5-base weights (no checkpoint offline)",
         "config": {"workload": ("hybrid retrieve: E5 query encode + cosine top-24 + MMR-10 + BM25 top-10 + RRF "
@@ -332,9 +375,10 @@ def main():
         "bm25_rescored_pairs": rescored,
         "roofline": roof,
         "rooflines": roofs,
+        "env": {e: os.environ[e] for e in KNOB_ENV if e in os.environ},
     }
     if rank == 0 and ws == 1 and args.cpu_baseline and args.mode == "hybrid":
-        cpu, recall = cpu_baseline_and_recall(args, dense, bm25, res, q_terms, qbuf if use_e5 else qfix)
+        cpu, recall = cpu_baseline_and_recall(args, dense, bm25, res, q_terms, e5["qbuf"] if use_e5 else qfix)
         out["cpu_baseline"] = cpu
         out["recall_at_10"] = recall
     else:

@@ -5,9 +5,12 @@ same constructor arguments, ``query: `` / ``passage: `` prefixes, batch 32,
 mean pooling over the attention mask and L2 normalisation, fp32 numpy output.
 
 * The XLM-R (E5-base: 12 layers, d=768, 12 heads, FFN 3072, vocab 250002)
-  forward runs in PyTorch-ROCm (bf16 by default; SDPA attention).
+  forward runs in PyTorch-ROCm, in fp32 by default -- the reference's precision
+  (sentence-transformers on torch fp32, rag/embeddings/__init__.py:87-94).
+  ``dtype="bfloat16"`` (or ``CM_E5_DTYPE=bfloat16``) is the opt-in fast path;
+  its drift from fp32 is bounded by tests/test_gpu_scale.py.
 * Mean-pool + L2-normalise is the hand-written HIP kernel K6
-  (``cm_meanpool_l2norm``), reading the bf16 hidden states in place.
+  (``cm_meanpool_l2norm``), reading the hidden states in place.
 
 Weights: ``model_name`` may be a local directory with a Hugging Face
 checkpoint (config + weights + tokenizer) or a hub id already present in the
@@ -19,6 +22,7 @@ torch fp32 reference).
 """
 from __future__ import annotations
 
+import contextlib
 import hashlib
 import math
 import os
@@ -33,6 +37,17 @@ E5_BASE_CONFIG = dict(vocab_size=250002, hidden_size=768, num_hidden_layers=12, 
                       intermediate_size=3072, max_position_embeddings=514, type_vocab_size=1,
                       layer_norm_eps=1e-5, pad_token_id=1, bos_token_id=0, eos_token_id=2)
 MAX_SEQ_LEN = 512  # sentence-transformers max_seq_length of multilingual-e5-base
+
+
+_DTYPES = {"float32": "float32", "fp32": "float32", "bfloat16": "bfloat16", "bf16": "bfloat16"}
+
+
+def _resolve_dtype(dtype: Optional[str]) -> str:
+    """Forward dtype: the argument, else $CM_E5_DTYPE, else fp32 (the reference's precision)."""
+    name = dtype or os.environ.get("CM_E5_DTYPE") or "float32"
+    if name not in _DTYPES:
+        raise ValueError(f"unsupported E5 dtype {name!r} (float32 or bfloat16)")
+    return _DTYPES[name]
 
 
 class HashTokenizer:
@@ -66,14 +81,17 @@ class HashTokenizer:
 
 class E5MultilingualEmbedder:
     def __init__(self, model_name: str = "intfloat/multilingual-e5-base", device: Optional[str] = None,
-                 normalize: bool = True, dtype: str = "bfloat16", _model=None, _tokenizer=None):
+                 normalize: bool = True, dtype: Optional[str] = None, _model=None, _tokenizer=None):
         import torch
         self.normalize = bool(normalize)
         self.model_name = model_name
         self.device = torch.device(device or ("cuda" if torch.cuda.is_available() else "cpu"))
         if self.device.type != "cuda":
-            raise RuntimeError("E5MultilingualEmbedder needs a ROCm GPU (the pooling epilogue is a HIP kernel)")
-        self.dtype = getattr(torch, dtype)
+            # deliberate divergence: the reference also runs on CPU; this
+            # build's pooling epilogue is a HIP kernel and there is no CPU fallback
+            raise RuntimeError("E5MultilingualEmbedder needs a ROCm GPU (the pooling epilogue is a HIP kernel); "
+                               f"device={device!r} is not supported")
+        self.dtype = getattr(torch, _resolve_dtype(dtype))
         if _model is None:
             _model, _tokenizer = self._load(model_name)
         self.model = _model.to(self.device, self.dtype).eval()
@@ -96,10 +114,12 @@ class E5MultilingualEmbedder:
 
     @classmethod
     def random_init(cls, seed: int = 0, device: Optional[str] = None, normalize: bool = True,
-                    dtype: str = "bfloat16", num_layers: int = 12):
-        """E5-base architecture with seeded random weights (no checkpoint available offline)."""
+                    dtype: Optional[str] = None, num_layers: int = 12):
+        """E5-base architecture with seeded random weights (no checkpoint available offline).
+        The weights are drawn in fp32 and then cast, so every dtype gets the same model."""
         import torch
         from transformers import XLMRobertaConfig, XLMRobertaModel
+        dtype = _resolve_dtype(dtype)
         cfg = XLMRobertaConfig(**{**E5_BASE_CONFIG, "num_hidden_layers": num_layers})
         cfg._attn_implementation = "sdpa"
         torch.manual_seed(seed)
@@ -201,24 +221,35 @@ class E5MultilingualEmbedder:
         return fwd
 
     @staticmethod
-    def _tuned_gemms() -> bool:
-        """Load the TunableOp table of hipBLASLt solutions measured on MI355X for the E5 GEMM
-        shapes of a 256 x 24-token query batch (tunableop_e5_gfx950.csv; tools/tune_probe.sh
-        regenerates it).  Lookup only (no tuning at run time, untuned shapes keep hipBLASLt's
-        default); results are written, if ever, to a temp file, never into the package.
+    @contextlib.contextmanager
+    def _tuned_gemms():
+        """TunableOp lookup of the hipBLASLt solutions measured on MI355X for the E5 GEMM shapes of
+        a 256 x 24-token query batch (tunableop_e5_gfx950.csv; tools/tune_probe.sh regenerates it),
+        scoped to a graph capture: the table is read first and lookup is switched on only if it
+        loaded; no tuning, no recording of untuned shapes, results file /dev/null; the previous
+        TunableOp state is restored on exit, so later GEMMs of the host application are untouched
+        (the captured graph keeps the tuned kernels).  Yields whether the table is in use.
         CM_E5_TUNABLEOP=0 disables it."""
-        if os.environ.get("CM_E5_TUNABLEOP", "1") == "0":
-            return False
-        import tempfile
         import torch.cuda.tunable as tun
         table = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tunableop_e5_gfx950.csv")
-        if not os.path.exists(table):
-            return False
-        tun.tuning_enable(False)
-        tun.record_untuned_enable(False)
-        tun.set_filename(os.path.join(tempfile.gettempdir(), f"cm_tunableop_{os.getpid()}.csv"))
-        tun.enable(True)
-        return bool(tun.read_file(table))
+        if os.environ.get("CM_E5_TUNABLEOP", "1") == "0" or not os.path.exists(table):
+            yield False
+            return
+        prev = (tun.is_enabled(), tun.tuning_is_enabled(), tun.record_untuned_is_enabled(), tun.get_filename())
+        ok = False
+        try:
+            tun.tuning_enable(False)
+            tun.record_untuned_enable(False)
+            tun.set_filename(os.devnull)
+            ok = bool(tun.read_file(table))
+            tun.enable(ok)
+            yield ok
+        finally:
+            tun.enable(prev[0])
+            tun.tuning_enable(prev[1])
+            tun.record_untuned_enable(prev[2])
+            if prev[3]:
+                tun.set_filename(prev[3])
 
     def capture_graph(self, batch: int, seq_len: int, unpadded: bool = False):
         """HIP-graph the device encode for a fixed (batch, seq_len) (hipGraph via torch.cuda.CUDAGraph:
@@ -234,7 +265,6 @@ class E5MultilingualEmbedder:
         out = torch.empty((batch, self.model.config.hidden_size), dtype=torch.float32, device=dev)
 
         lean = self._lean_forward() if unpadded else None
-        self.tuned_gemms = self._tuned_gemms()
 
         def fwd():
             if lean is not None:
@@ -244,7 +274,8 @@ class E5MultilingualEmbedder:
                 hidden = self.model(input_ids=ids, attention_mask=m4).last_hidden_state
             engine.meanpool_l2norm(hidden, mask, self.normalize, out=out)
 
-        with torch.inference_mode():
+        with torch.inference_mode(), self._tuned_gemms() as tuned:
+            self.tuned_gemms = tuned
             side = torch.cuda.Stream(device=dev)
             side.wait_stream(torch.cuda.current_stream(dev))
             with torch.cuda.stream(side):

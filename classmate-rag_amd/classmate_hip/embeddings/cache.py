@@ -6,7 +6,9 @@ unchanged: one ``<root>/<model>/<mode>/<sha1(text.strip())>.npy`` fp32 vector pe
 
 * root = ``cache_dir`` or ``$EMB_CACHE_DIR`` or ``./indexes/emb_cache`` (cache.py:48);
 * model sub-directory from ``base.model.name_or_path`` else ``base.model_name`` else
-  ``unknown-model``, sanitised to ``[A-Za-z0-9._-]`` (cache.py:52-59);
+  ``unknown-model``, sanitised to ``[A-Za-z0-9._-]`` (cache.py:52-59); a base embedder running
+  below the reference's fp32 (``dtype`` bfloat16, the opt-in fast path) gets ``__bfloat16``
+  appended, so its vectors never mix with fp32 ones under the same key;
 * a file that fails to load is a miss (cache.py:100-106); write errors are swallowed (cache.py:136-141);
 * all misses of one call go to the base embedder as ONE batch, in input order, duplicates
   included (cache.py:132-133) — with the HIP E5 path that is one padded forward + the K6
@@ -38,6 +40,9 @@ def _model_dirname(base) -> str:
         name = str(model.name_or_path)
     else:
         name = getattr(base, "model_name", "unknown-model")
+    dt = str(getattr(base, "dtype", "") or "")
+    if dt and not dt.endswith("float32"):          # e.g. torch.bfloat16 -> "__bfloat16"
+        name = f"{name}__{dt.rsplit('.', 1)[-1]}"
     return "".join(c if (c.isalnum() or c in "-_.") else "_" for c in name)
 
 

@@ -123,8 +123,11 @@ class HybridRetriever:
                 bn[i] = len(bm_batch[i])
             interns.append(intern)
         wv, wb = (self.weight_vector, self.weight_bm25) if hybrid else (1.0, 0.0)
+        # fused_list[:top_k] (fusion.py:167) with Python slice semantics: the device merge ranks
+        # every item (kv + kb of them) and a negative / zero top_k is applied to that full order
+        k_dev = top_k if top_k > 0 else kv + kb
         ok, of, _, _, ofl, on = engine.rrf_merge(vkeys, vdist, vn, bkeys, bscore, bn, w_vec=wv, w_bm25=wb,
-                                                 rrf_k=self.rrf_k, top_k=top_k)
+                                                 rrf_k=self.rrf_k, top_k=k_dev)
         out = []
         for i in range(nq):
             by_id: Dict[Any, Dict[str, object]] = {}
@@ -144,7 +147,9 @@ class HybridRetriever:
                 it["scores"]["bm25_score"] = r.get("score")
             names = {v: k for k, v in interns[i].items()}
             res = []
-            for j in range(int(on[i])):
+            m = int(on[i])
+            m = len(range(m)[:top_k])                    # Python slice of the full order
+            for j in range(m):
                 it = by_id[names[int(ok[i, j])]]
                 it["scores"]["fused"] = float(of[i, j])
                 res.append(it)
@@ -162,8 +167,6 @@ class HybridRetriever:
             bm25_res = self._bm25_search(query=question, where=bm_where, k=self.k_bm25)
         else:
             vec_res = self._vector_search(query=question, where=chroma_where, k=max(top_k, self.k_vector))
-        if top_k <= 0:
-            return []
         return self._merge(vec_res, bm25_res, top_k, hybrid)
 
     # ---- batched: one device launch per stage for the whole batch -----------------
@@ -214,6 +217,4 @@ class HybridRetriever:
                 bm_batch = [self.bm25_store.search(query=q, where=bm_where, top_k=self.k_bm25) for q in questions]
         else:
             bm_batch = [[] for _ in questions]
-        if top_k <= 0:
-            return [[] for _ in questions]
         return self._merge_batch(vec_batch, bm_batch, top_k, hybrid)

@@ -147,8 +147,13 @@ class GpuVectorStore:
         if (d / "meta.json").exists():
             os.remove(d / "meta.json")    # invalid until the rewrite below completes
         vecs = np.ascontiguousarray(self._index.export(), np.float32)
+        n, dim = len(self._ids), self._index.dim
         with open(d / "vectors.tmp.f32", "wb") as f:
-            f.write(vecs[: len(self._ids)].tobytes())
+            f.write(vecs[:n].tobytes())
+            # the device copy ends at the last row ever written after a reload (trailing rows that
+            # are tombstones were never re-uploaded): pad so the file always holds meta.rows rows
+            if vecs.shape[0] < n:
+                f.truncate(n * dim * 4)
         os.replace(d / "vectors.tmp.f32", d / "vectors.f32")
         with (d / "rows.tmp.jsonl").open("w", encoding="utf-8") as f:
             for r in range(len(self._ids)):

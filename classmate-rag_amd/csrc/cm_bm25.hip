@@ -1018,6 +1018,9 @@ int build_head_tiles(cm_bm25 *h, const std::vector<int32_t> &df) {
 
 // CM_BM25_DEBUG (ablation only): K2 bit0 skip scoring, bit1 skip the per-range top-k; bit2 full
 // scan instead of the pruned search; K2a bit4 skip candidate scoring, bit5 skip the ranking.
+// Timing ablations are compiled only into -DCM_ABLATION builds (tools/build_variant.sh); the
+// product library ignores CM_BM25_DEBUG, so no bench line can come from a disabled kernel.
+#ifdef CM_ABLATION
 int bm25_debug_flags() {
   static int f = [] {
     const char *e = getenv("CM_BM25_DEBUG");
@@ -1025,6 +1028,9 @@ int bm25_debug_flags() {
   }();
   return f;
 }
+#else
+int bm25_debug_flags() { return 0; }
+#endif
 
 struct BmWs {
   unsigned long long *thr;

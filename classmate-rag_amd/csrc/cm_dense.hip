@@ -1464,6 +1464,9 @@ int dense_grow(cm_dense *h, int64_t need_rows) {
 // without inserting survivors, bit5 (K1c) no sample pre-pass, bit6 (K1c) no MFMAs, bit7 (K1c) no
 // per-tile epilogue, bit9 no chunk barrier, bit10 no DMA issue, bit11 no fragment reads (K1c
 // timing ablations only: results are garbage under bits 9-11).
+// Timing ablations are compiled only into -DCM_ABLATION builds (tools/build_variant.sh); the
+// product library ignores CM_DENSE_DEBUG, so no bench line can come from a disabled kernel.
+#ifdef CM_ABLATION
 int dense_debug_flags() {
   static const int f = [] {
     const char *e = getenv("CM_DENSE_DEBUG");
@@ -1471,6 +1474,9 @@ int dense_debug_flags() {
   }();
   return f;
 }
+#else
+int dense_debug_flags() { return 0; }
+#endif
 
 // Scan kernel for (nq, k): K1c (coarse f16 + certified re-rank) whenever its list length fits,
 // K1b (f16x3) for other batched k <= 32, K1 (fp32) otherwise.  CM_DENSE_PATH=f32|f16x3|coarse

@@ -228,3 +228,49 @@ def test_e5_graph_replay_matches_eager():
     ugraph.replay()
     torch.cuda.synchronize()
     torch.testing.assert_close(u_out, emb.encode_token_ids(ids, mask), atol=2e-3, rtol=0)
+
+
+@pytest.mark.parametrize("top_k", [-3, 0, 1, 5])
+def test_retrieve_slice_semantics_of_top_k(stores, corpus, top_k):
+    """fused_list[:top_k] (rag/retrieval/fusion.py:167): negative and zero top_k slice the full
+    fused order the way Python does, on the single and batched paths (oracle: the restatement of
+    HybridRetriever.retrieve over the exact store)."""
+    from oracle import ref_semantics as orc
+    from classmate_hip.retrieval import HybridRetriever
+    vs, bm, _ = stores
+    emb = PresetEmbedder(corpus["qtexts"], corpus["qvecs"])
+    retr = HybridRetriever(vector_store=vs, bm25_store=bm, embedder=emb, k_vector=10, k_bm25=10)
+    ovs = orc.ExactVectorStore(corpus["ids"], corpus["texts"], corpus["metas"], corpus["emb"])
+    obm = orc.BM25Oracle()
+    obm.upsert_many(corpus["ids"], corpus["texts"], corpus["metas"])
+    batch = retr.retrieve_batch(questions=corpus["qtexts"][:4], top_k=top_k)
+    for i, q in enumerate(corpus["qtexts"][:4]):
+        want = orc.retrieve(ovs, obm, emb, question=q, top_k=top_k, k_vector=10, k_bm25=10)
+        w = _rows(want)
+        _check(_rows(retr.retrieve(question=q, top_k=top_k)), w)
+        _check(_rows(batch[i]), w)
+
+
+def test_vector_store_save_after_trailing_deletes(corpus, tmp_path):
+    """rows at the end of the store that were deleted before a reload never reach the
+    device copy again; save() must still write meta.rows rows so the store reopens."""
+    from classmate_hip.retrieval import GpuVectorStore
+    ids, emb = corpus["ids"][:64], corpus["emb"][:64]
+    vs = GpuVectorStore(persist_dir=tmp_path)
+    vs.upsert(ids=ids, documents=corpus["texts"][:64], metadatas=corpus["metas"][:64], embeddings=emb)
+    vs.delete(ids[40:])                                   # trailing tombstones
+    again = GpuVectorStore(persist_dir=tmp_path)
+    assert again.count() == 40
+    again.save()                                          # device copy holds 40 rows, meta says 64
+    third = GpuVectorStore(persist_dir=tmp_path)
+    assert third.count() == 40
+    q = corpus["qvecs"][0]
+    assert [r["id"] for r in third.query(query_embeddings=q, top_k=10)] == \
+        [r["id"] for r in vs.query(query_embeddings=q, top_k=10)]
+    third.delete(ids[:40])                                # every row a tombstone
+    fourth = GpuVectorStore(persist_dir=tmp_path)
+    assert fourth.count() == 0
+    fourth.save()
+    assert GpuVectorStore(persist_dir=tmp_path).count() == 0
+    fourth.upsert(ids=["new"], documents=["x"], metadatas=[{}], embeddings=emb[:1])
+    assert [r["id"] for r in GpuVectorStore(persist_dir=tmp_path).query(query_embeddings=emb[0], top_k=3)] == ["new"]

@@ -1,0 +1,388 @@
+"""GPU parity at the BASELINE.json configuration sizes ("Next round" item 1).
+
+* C2  -- 1M x 768 fp32 chunks, a 256-query batch (and a 16-query batch), k = 24: dense ids and
+  distances against an exact fp64 scan of every row (the oracle's distance,
+  rag/retrieval/vector_chroma.py:156 ``hnsw:space=cosine``: d = 1 - q.c / (|q| |c|)).
+* C4  -- the bench's 10M-chunk hybrid shard (bench.py generators), 16 queries: BM25 top-10
+  bit-exact against the C oracle (oracle/cm_oracle.c, rank_bm25 0.2.2 restated), dense top-24
+  against the exact fp64 scan, and the final fused top-10 keys (K4 MMR + K5 RRF) equal to the
+  CPU restatement of HybridRetriever.retrieve (rag/retrieval/fusion.py:108-167) on the same pools.
+* C3  -- E5-base (12 layers) at B = 32, S = 256: the lean and padded graph encodes in fp32
+  against the Hugging Face XLM-R module in fp32 (the reference's precision,
+  rag/embeddings/__init__.py:87-94), and the opt-in bf16 forward bounded against fp32
+  (embedding cosine, retrieval top-10 agreement).
+* C5  -- two ranks (gloo exchanges, both on cuda:0) each owning a 1M-row dense shard and a
+  1M-document BM25 shard: merged results equal the unsharded oracle.
+
+Tolerances are the ones north_star states: cosine distance within 1e-4 (set equality modulo
+oracle ties closer than 1e-5), BM25 scores bit-identical.
+"""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+DIST_TOL = 1e-4
+TIE = 1e-5
+
+
+# ---------------------------------------------------------------------------
+# exact fp64 oracle over big corpora (chunked numpy; test infrastructure)
+# ---------------------------------------------------------------------------
+def exact_topk(C, Q, kk, chunk=1 << 17):
+    """Per query the kk smallest exact distances d = 1 - q.c / (|q| |c|) (fp64), ties -> lower row.
+    Returns (dist (nq, kk) f64, rows (nq, kk) i64)."""
+    Q64 = np.asarray(Q, np.float64)
+    qn = np.linalg.norm(Q64, axis=1)
+    nq = Q64.shape[0]
+    best_d = np.full((nq, 0), np.inf)
+    best_r = np.zeros((nq, 0), np.int64)
+    for r0 in range(0, C.shape[0], chunk):
+        c = np.asarray(C[r0:r0 + chunk], np.float64)
+        cn = np.linalg.norm(c, axis=1)
+        d = 1.0 - (c @ Q64.T) / np.outer(cn, qn)                 # (chunk, nq)
+        m = min(kk, d.shape[0])
+        part = np.argpartition(d, m - 1, axis=0)[:m].T            # (nq, m)
+        cd = np.take_along_axis(d.T, part, 1)
+        best_d = np.concatenate([best_d, cd], 1)
+        best_r = np.concatenate([best_r, part + r0], 1)
+        o = np.lexsort((best_r, best_d), axis=1)[:, :kk]
+        best_d = np.take_along_axis(best_d, o, 1)
+        best_r = np.take_along_axis(best_r, o, 1)
+    return best_d, best_r
+
+
+def check_dense(dist, rows, o_dist, o_rows, k):
+    """GPU (dist, rows) vs the exact list of k + slack entries: distances within 1e-4, the top-k
+    set equal except rows within 1e-5 of the k-th exact distance, order strict wherever the
+    exact distances are separated by more than 1e-5."""
+    assert o_dist.shape[1] > k
+    for i in range(rows.shape[0]):
+        kth = o_dist[i, k - 1]
+        assert o_dist[i, -1] > kth + TIE, "slack too small for the tie analysis"
+        got = rows[i][rows[i] >= 0]
+        assert len(got) == k
+        np.testing.assert_allclose(dist[i][:k], o_dist[i, :k], atol=DIST_TOL)
+        unsure = set(o_rows[i][np.abs(o_dist[i] - kth) < TIE].tolist())
+        assert set(got.tolist()) ^ set(o_rows[i, :k].tolist()) <= unsure, i
+        sep = np.diff(o_dist[i, :k]) > TIE
+        for j in np.nonzero(sep)[0]:
+            assert got[j] == o_rows[i, j] or abs(dist[i][j] - o_dist[i, j]) < TIE, (i, j)
+
+
+def unit_rows(n, dim, seed, row0=0, block=1 << 16):
+    """Rows [row0, row0 + n) of a deterministic unit-norm Gaussian corpus, generated block by
+    block (row r's value does not depend on which shard asks for it; row0 % block == 0)."""
+    assert row0 % block == 0
+    out = np.empty((n, dim), np.float32)
+    for b0 in range(0, n, block):
+        rng = np.random.default_rng([seed, (row0 + b0) // block])
+        x = rng.standard_normal((min(block, n - b0), dim), dtype=np.float32)
+        x /= np.linalg.norm(x, axis=1, keepdims=True)
+        out[b0:b0 + x.shape[0]] = x
+    return out
+
+
+def mixed_queries(C, nq, seed, sigma=0.05):
+    """Half perturbed corpus rows (near-duplicate queries), half random directions."""
+    rng = np.random.default_rng(seed)
+    q = rng.standard_normal((nq, C.shape[1])).astype(np.float32)
+    h = nq // 2
+    q[:h] = C[rng.integers(0, C.shape[0], h)] + sigma * q[:h] / np.sqrt(C.shape[1])
+    return q
+
+
+# ---------------------------------------------------------------------------
+# C2: 1M x 768
+# ---------------------------------------------------------------------------
+@pytest.fixture(scope="module")
+def c2():
+    C = unit_rows(1_000_000, 768, seed=1)
+    Q = mixed_queries(C, 256, seed=2)
+    o_d, o_r = exact_topk(C, Q, 24 + 40)
+    return C, Q, o_d, o_r
+
+
+@pytest.mark.parametrize("nq", [256, 16, 1])
+def test_dense_1m_x_768(c2, nq):
+    from classmate_hip import engine
+    C, Q, o_d, o_r = c2
+    idx = engine.DenseIndex(768, capacity=C.shape[0])
+    idx.upsert(C, np.arange(C.shape[0], dtype=np.int64))
+    dist, rows = idx.search(Q[:nq], 24)
+    check_dense(dist, rows, o_d[:nq], o_r[:nq], 24)
+    assert idx.last_fallbacks() == 0
+    # deleted + filtered rows never come back; statistics of the survivors stay exact
+    drop = o_r[:nq, :3].ravel()
+    idx.delete(drop)
+    allow = np.ones(C.shape[0], bool)
+    allow[1::2] = False
+    words = np.packbits(allow, bitorder="little").view(np.uint32)
+    dist2, rows2 = idx.search(Q[:nq], 24, words)
+    assert not np.isin(rows2, drop).any() and (rows2 % 2 == 0).all()
+    idx.close()
+
+
+# ---------------------------------------------------------------------------
+# C4: the bench's 10M hybrid shard
+# ---------------------------------------------------------------------------
+def test_hybrid_10m_sample():
+    import torch
+    sys.path.insert(0, str(__import__("pathlib").Path(__file__).resolve().parents[1]))
+    import bench
+    from classmate_hip import engine
+    from oracle import corc
+    from oracle import ref_semantics as orc
+
+    N, D, B, K, P = 10_000_000, 768, 16, 10, 24
+    dense = engine.DenseIndex(D, capacity=N)
+    bench.gen_dense(dense, N, D, seed=1000)
+    tokens, doc_off = bench.gen_tokens(N, 1 << 20, 1.07, 120.0, seed=1500)
+    bm = engine.BM25Index()
+    bm.build_dev(tokens, doc_off, 1 << 20)
+    torch.cuda.synchronize()
+    qt = bench.sample_query_terms(tokens, doc_off, B, 8, seed=10)
+    del tokens, doc_off
+    torch.cuda.empty_cache()
+    C = dense.export()                                              # host copy (30.7 GB)
+    Q = mixed_queries(C, B, seed=11)
+    q_dev = torch.from_numpy(Q).cuda()
+    # GPU: the bench step's device pipeline at B = 16
+    d, r = dense.search_dev(q_dev, P)
+    vecs = dense.gather_dev(r.reshape(-1)).view(B, P, D)
+    order = engine.mmr_dev(q_dev, vecs, K, 0.5)
+    o = order.long().clamp(min=0)
+    vk, vd = torch.gather(r, 1, o), torch.gather(d, 1, o)
+    vn = (order >= 0).sum(1, dtype=torch.int32)
+    q_terms = qt.reshape(-1).contiguous()
+    q_off = (torch.arange(B + 1, device="cuda", dtype=torch.int32) * 8).contiguous()
+    bs, br = bm.search_dev(q_terms, q_off, K)
+    bn = (br >= 0).sum(1, dtype=torch.int32)
+    fused = engine.rrf_merge_dev(vk.contiguous(), vd.contiguous(), vn, br.contiguous(), bs.contiguous(), bn,
+                                 w_vec=1.0, w_bm25=1.0, rrf_k=60, top_k=K)
+    torch.cuda.synchronize()
+    d, r = d.cpu().numpy(), r.cpu().numpy()
+    # dense vs exact fp64
+    o_d, o_r = exact_topk(C, Q, P + 40)
+    check_dense(d, r, o_d, o_r, P)
+    # BM25 bit-exact vs the C oracle
+    csr = bm.export()
+    term_off = csr["term_off"]
+    df = np.diff(term_off)
+    first = np.full(df.shape[0], np.uint64(0xFFFFFFFFFFFFFFFF))
+    nz = df > 0
+    fp = term_off[:-1][nz]
+    first[nz] = (csr["post_doc"][fp].astype(np.uint64) << np.uint64(32)) | csr["post_pos"][fp].astype(np.uint64)
+    ccsr = dict(term_off=term_off, post_doc=csr["post_doc"], post_tf=csr["post_tf"], dl=csr["dl"],
+                vocab=int(df.shape[0]), ndocs=N)
+    idf, _ = corc.bm25_idf(df, first, N)
+    queries = qt.cpu().numpy().tolist()
+    o_sc, o_rw = corc.bm25_topk(ccsr, idf, float(csr["dl"].astype(np.int64).sum()) / N, queries, K)
+    assert np.array_equal(br.cpu().numpy(), o_rw) and np.array_equal(bs.cpu().numpy(), o_sc)
+    # fused top-10 == the CPU restatement of retrieve() over the exact pools
+    got = fused[0].cpu().numpy()
+    checked = 0
+    for i in range(B):
+        if o_d[i, P] - o_d[i, P - 1] <= TIE:                      # ambiguous pool boundary: skip
+            continue
+        pool = o_r[i, :P]
+        ordr = orc.mmr_order(Q[i], C[pool], list(range(P)), K, 0.5)
+        vec_ids = [int(pool[j]) for j in ordr]
+        bm_ids = [int(x) for x in o_rw[i] if x >= 0]
+        fz = orc.rrf_fuse(rank_lists=[vec_ids, bm_ids], weights=[1.0, 1.0], rrf_k=60)
+        vdist = {int(pool[j]): float(np.float32(o_d[i, j])) for j in ordr}
+        items = list(dict.fromkeys(vec_ids + bm_ids))
+        items.sort(key=lambda x: (fz[x], -vdist.get(x, 0.0)), reverse=True)
+        assert [int(x) for x in got[i] if x >= 0] == items[:K], i
+        checked += 1
+    assert checked >= B // 2
+    dense.close()
+    bm.close()
+
+
+# ---------------------------------------------------------------------------
+# C3: 12-layer E5 at B = 32, S = 256
+# ---------------------------------------------------------------------------
+def _hf_reference(model, ids, mask):
+    """sentence-transformers' Pooling(mean) + Normalize over the HF module, all fp32 torch."""
+    import torch
+    with torch.inference_mode():
+        h = model(input_ids=ids, attention_mask=mask).last_hidden_state.float()
+        m = mask.float().unsqueeze(-1)
+        v = (h * m).sum(1) / m.sum(1).clamp(min=1e-9)
+        return torch.nn.functional.normalize(v, p=2, dim=1)
+
+
+def test_e5_base_b32_s256_fp32_and_bf16_bound():
+    import torch
+    from classmate_hip.embeddings import E5MultilingualEmbedder
+    B, S = 32, 256
+    f32 = E5MultilingualEmbedder.random_init(seed=0, device="cuda", dtype="float32")
+    assert f32.dtype == torch.float32                     # the drop-in default is the reference's fp32
+    g = torch.Generator(device="cuda").manual_seed(3)
+    ids = torch.randint(5, 250002, (B, S), device="cuda", generator=g)
+    ids[:, 0] = 0
+    ids[:, -1] = 2
+    ones = torch.ones_like(ids)
+    ref = _hf_reference(f32.model, ids, ones)
+    # lean graph forward (fused QKV GEMM + SDPA + HIP add+LayerNorm + K6) == HF fp32
+    u_ids, _, u_out, ug = f32.capture_graph(B, S, unpadded=True)
+    u_ids.copy_(ids)
+    ug.replay()
+    torch.cuda.synchronize()
+    torch.testing.assert_close(u_out, ref, atol=2e-5, rtol=0)
+    # ragged batch through the padded graph (4-D mask) and the eager encode == HF fp32
+    mask = ones.clone()
+    lens = torch.randint(8, S + 1, (B,), generator=torch.Generator().manual_seed(4))
+    for b in range(B):
+        mask[b, int(lens[b]):] = 0
+        ids[b, int(lens[b]):] = 1
+    ref_r = _hf_reference(f32.model, ids, mask)
+    p_ids, p_mask, p_out, pg = f32.capture_graph(B, S)
+    p_ids.copy_(ids)
+    p_mask.copy_(mask)
+    pg.replay()
+    torch.cuda.synchronize()
+    torch.testing.assert_close(p_out, ref_r, atol=2e-5, rtol=0)
+    torch.testing.assert_close(f32.encode_token_ids(ids, mask), ref_r, atol=2e-5, rtol=0)
+    # bf16 opt-in (same weights): per-embedding cosine to fp32 >= 1 - 2e-3
+    b16 = E5MultilingualEmbedder.random_init(seed=0, device="cuda", dtype="bfloat16")
+    out16 = b16.encode_token_ids(ids, mask)
+    cos = (out16 * ref_r).sum(1)
+    assert float(cos.min()) >= 1 - 2e-3, float(cos.min())
+    print(f"\nE5 bf16 vs fp32 (B={B}, S<={S}): min cosine {float(cos.min()):.6f}, "
+          f"mean 1-cos {float((1 - cos).mean()):.2e}")
+
+
+def test_e5_bf16_retrieval_agreement():
+    """Top-10 passages of related queries under bf16 vs fp32 encodes (same random-init E5-base):
+    mean overlap >= 0.9 -- the retrieval impact of the opt-in bf16 path."""
+    import torch
+    from classmate_hip.embeddings import E5MultilingualEmbedder
+    f32 = E5MultilingualEmbedder.random_init(seed=1, device="cuda", dtype="float32")
+    b16 = E5MultilingualEmbedder.random_init(seed=1, device="cuda", dtype="bfloat16")
+    g = torch.Generator(device="cuda").manual_seed(7)
+    NP, NQ, S = 512, 32, 128
+    pas = torch.randint(5, 250002, (NP, S), device="cuda", generator=g)
+    src = torch.randint(0, NP, (NQ,), device="cuda", generator=g)
+    qry = pas[src].clone()
+    noise = torch.rand((NQ, S), device="cuda", generator=g) < 0.6
+    qry[noise] = torch.randint(5, 250002, (int(noise.sum()),), device="cuda", generator=g)
+    ones_p, ones_q = torch.ones_like(pas), torch.ones_like(qry)
+
+    def enc(m, x, msk):
+        return torch.cat([m.encode_token_ids(x[i:i + 64], msk[i:i + 64]) for i in range(0, x.shape[0], 64)])
+
+    tops = []
+    for m in (f32, b16):
+        P_, Q_ = enc(m, pas, ones_p), enc(m, qry, ones_q)
+        tops.append(torch.topk(Q_ @ P_.T, 10, dim=1).indices.cpu().numpy())
+    overlap = np.mean([len(set(a) & set(b)) / 10 for a, b in zip(*tops)])
+    print(f"\nE5 bf16 vs fp32 top-10 overlap: {overlap:.3f}")
+    assert overlap >= 0.9, overlap
+
+
+# ---------------------------------------------------------------------------
+# C5: two ranks, 1M rows each
+# ---------------------------------------------------------------------------
+N_RANK = 1 << 20                   # >= 1M rows per rank, a whole number of generator blocks
+VOCAB = 100_000
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _bm25_docs(lo, hi, block=1 << 16):
+    """Zipf(1.07) tokens of documents [lo, hi), generated per 64k-doc block (shard-independent)."""
+    toks, lens = [], []
+    for b0 in range(lo - lo % block, hi, block):
+        rng = np.random.default_rng([77, b0 // block])
+        ln = np.maximum(rng.poisson(60, block), 1)
+        p = 1.0 / np.arange(1, VOCAB + 1) ** 1.07
+        t = rng.choice(VOCAB, size=int(ln.sum()), p=p / p.sum()).astype(np.int32)
+        off = np.concatenate([[0], np.cumsum(ln)])
+        a, b = max(lo, b0) - b0, min(hi, b0 + block) - b0
+        toks.append(t[off[a]:off[b]])
+        lens.append(ln[a:b])
+    lens = np.concatenate(lens)
+    off = np.zeros(lens.shape[0] + 1, np.int64)
+    off[1:] = np.cumsum(lens)
+    return np.concatenate(toks), off
+
+
+def _queries():
+    rng = np.random.default_rng(5)
+    return [rng.integers(0, 3000, 8).tolist() for _ in range(12)] + [[0, 1], [VOCAB - 1], [4000, 4000, 17]]
+
+
+def _dense_queries():
+    rng = np.random.default_rng(6)
+    return rng.standard_normal((16, 768)).astype(np.float32)
+
+
+def _worker(rank, port, out_q):
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE="2")
+    dist.init_process_group("gloo", rank=rank, world_size=2)
+    try:
+        from classmate_hip import engine
+        from classmate_hip import parallel as P
+        row0 = rank * N_RANK
+        toks, off = _bm25_docs(row0, row0 + N_RANK)
+        bm = engine.BM25Index(device=0)
+        bm.build(toks, off, VOCAB)
+        df, fk = bm.term_stats()
+        st = bm.stats()
+        gdf, gfk, gn, gsum = P.allreduce_bm25_stats(df, fk, row0, st["n_live"], st["sum_len"])
+        idf, eps = P.bm25_idf_table(gdf, gfk, gn)
+        bm.set_stats(idf, gn, gsum, eps)
+        sc, rw, _ = bm.search(_queries(), 10)
+        S_, R_ = P.merge_bm25_topk(torch.from_numpy(sc), torch.from_numpy(np.where(rw >= 0, rw + row0, rw)), 10)
+        res = {"rank": rank, "bm25": (S_.numpy(), R_.numpy())}
+        bm.close()
+        dn = engine.DenseIndex(768, device=0, capacity=N_RANK)
+        dn.upsert(unit_rows(N_RANK, 768, seed=9, row0=row0), np.arange(N_RANK, dtype=np.int64))
+        d, r = dn.search(_dense_queries(), 24)
+        D_, R_ = P.merge_dense_topk(torch.from_numpy(d), torch.from_numpy(np.where(r >= 0, r + row0, r)), 24)
+        res["dense"] = (D_.numpy(), R_.numpy())
+        dn.close()
+        out_q.put(res)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_rank_shards_1m_rows_each():
+    import torch.multiprocessing as mp
+    from oracle import corc
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = sorted([q.get(timeout=280) for _ in range(2)], key=lambda x: x["rank"])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    # BM25: unsharded C oracle over all 2M documents, bit for bit
+    toks, off = _bm25_docs(0, 2 * N_RANK)
+    csr = corc.build_csr(toks, off, VOCAB)
+    idf, _ = corc.bm25_idf(csr["df"], csr["first_key"], 2 * N_RANK)
+    o_sc, o_rw = corc.bm25_topk(csr, idf, float(off[-1]) / (2 * N_RANK), _queries(), 10)
+    for res in out:
+        S_, R_ = res["bm25"]
+        assert np.array_equal(R_, o_rw) and np.array_equal(S_, o_sc)
+    # dense: the merged shard lists == the exact fp64 scan of the whole 2M rows
+    C = unit_rows(2 * N_RANK, 768, seed=9)
+    o_d, o_r = exact_topk(C, _dense_queries(), 24 + 40)
+    for res in out:
+        D_, R_ = res["dense"]
+        check_dense(D_, R_, o_d, o_r, 24)
