@@ -40,8 +40,9 @@ METRIC = "hybrid queries/sec + recall@10 vs reference, 10M×768 chunks, 1/2/4/8 
 PEAK_F32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 matrix (dense)
 PEAK_F16_MFMA_TFLOPS = 2500.0  # MI355X_MICROARCH.md: BF16/F16 matrix, dense (no sparsity)
 PEAK_HBM_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E spec
-DENSE_KINDS = {1: "K1 fp32 MFMA (dense_topk_kernel)", 2: "K1b f16x3 split planes (dense_split_kernel<2>)",
-               3: "K1c dense_coarse_scan_kernel (f16 hi plane, MFMA) + certified fp64 re-rank"}
+DENSE_KINDS = {1: "K1 fp32 MFMA (dense_topk_kernel)",
+               3: "K1c dense_coarse_scan_kernel (f16 plane, MFMA, 256-query resident passes) + certified fp64 re-rank",
+               4: "K1s dense_stream_scan_kernel (f16 plane, MFMA, per-wave HBM streams) + certified fp64 re-rank"}
 
 
 def parse_args():
@@ -194,17 +195,18 @@ def main():
         mask = torch.ones_like(ids)
 
         def make_e5(dtype):
-            """E5 query encoder of one dtype: (embedder, graph or None, output buffer)."""
+            """E5 query encoder of one dtype: dict(emb, graph or None, qbuf = output buffer, and the
+            graph's input buffers, which must stay alive as long as the graph is replayed)."""
             m = E5MultilingualEmbedder.random_init(seed=0, device=str(dev), num_layers=args.e5_layers, dtype=dtype)
             if args.no_graph:
-                return m, None, torch.empty((B, D), dtype=torch.float32, device=dev)
+                return dict(emb=m, graph=None, qbuf=torch.empty((B, D), dtype=torch.float32, device=dev))
             # one hipGraph replay per batch instead of ~200 launches (fixed-length queries: lean forward)
             g_ids, g_mask, out_buf, gr = m.capture_graph(B, args.q_tokens, unpadded=True)
             g_ids.copy_(ids)
             g_mask.copy_(mask)
-            return m, gr, out_buf
+            return dict(emb=m, graph=gr, qbuf=out_buf, ids=g_ids, mask=g_mask)
 
-        e5 = dict(zip(("emb", "graph", "qbuf"), make_e5(args.e5_dtype)))
+        e5 = make_e5(args.e5_dtype)
     else:
         g = torch.Generator(device="cuda").manual_seed(args.seed * 17)
         qfix = torch.randn(B, D, device=dev, generator=g)
@@ -323,7 +325,7 @@ def main():
         if bm25 is not None:
             bm25.timing(False)
         main_e5 = e5
-        e5 = dict(zip(("emb", "graph", "qbuf"), make_e5("float32")))
+        e5 = make_e5("float32")
         for _ in range(args.warmup):
             step()
         torch.cuda.synchronize()
@@ -357,8 +359,8 @@ def main():
         "value": qps, "unit": "queries/s", "n_gpus": ws, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "f16+f64",
-        "dtypes": {"dense_knn": {1: "f32 (MFMA)", 2: "f16x3 split (MFMA, f32-grade)",
-                                 3: "f16 coarse (MFMA) + fp64 exact re-rank of the certified band"}[kind],
+        "dtypes": {"dense_knn": {1: "f32 (MFMA)", 3: "f16 coarse (MFMA) + fp64 exact re-rank of the certified band",
+                                 4: "f16 coarse (MFMA) + fp64 exact re-rank of the certified band"}[kind],
                    "bm25": "f64", "e5_forward": args.e5_dtype if use_e5 else None, "fusion": "f64"},
         "e5_fp32": e5_fp32,
         "data": "synthetic (seeded): unit-norm Gaussian chunk embeddings, Zipf BM25 postings, random-init "
@@ -409,9 +411,7 @@ def _dense_roofline(kind, N, D, B, ms, traffic):
     storage format + live bitmap + query planes; flops as executed on the MFMA units."""
     if kind == 1:      # fp32 rows + invc
         bytes_, flops, peak = N * D * 4 + N * 4 + N / 8 + B * D * 4, 2.0 * N * D * B, PEAK_F32_MFMA_TFLOPS
-    elif kind == 2:    # hi + lo f16 planes, 3 products per block
-        bytes_, flops, peak = N * D * 4 + N / 8 + B * D * 4, 3 * 2.0 * N * D * B, PEAK_F16_MFMA_TFLOPS
-    else:              # hi plane only, 1 product per block
+    else:              # K1c / K1s: the f16 plane once + live bits + the f16 queries
         bytes_, flops, peak = N * D * 2 + N / 8 + B * D * 2, 2.0 * N * D * B, PEAK_F16_MFMA_TFLOPS
     r = _roof(bytes_, flops, peak, ms)
     r.update(traffic=traffic, kernel=DENSE_KINDS[kind], avg_launch_ms=ms,

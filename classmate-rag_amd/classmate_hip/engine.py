@@ -134,17 +134,18 @@ class DenseIndex:
         return out, mask
 
     # scan kernels (cm_dense_search_kind / cm_dense_set_path)
-    PATH_AUTO, PATH_F32, PATH_F16X3, PATH_COARSE = 0, 1, 2, 3
+    PATH_AUTO, PATH_F32, PATH_COARSE, PATH_STREAM = 0, 1, 3, 4
 
     def set_path(self, kind: int):
-        """Force the scan kernel (0 auto, 1 fp32 K1, 2 f16x3 K1b, 3 coarse+re-rank K1c)."""
+        """Force the scan kernel (0 auto, 1 fp32 K1, 3 K1c coarse + re-rank, 4 K1s <= 32-query streams
+        + re-rank; 2 = the retired K1b, automatic)."""
         L.check(L.fn["cm_dense_set_path"](self._h, int(kind)), "cm_dense_set_path")
 
     def search_kind(self, nq: int, k: int) -> int:
         return int(L.fn["cm_dense_search_kind"](self._h, int(nq), int(k)))
 
     def last_fallbacks(self) -> int:
-        """K1c queries re-run by the exact pass in the last host search()."""
+        """K1c/K1s queries re-run by the exact fp32 pass in the last host search()."""
         return int(L.fn["cm_dense_last_fallbacks"](self._h))
 
     def timing(self, enable: bool = True):
@@ -160,7 +161,7 @@ class DenseIndex:
         return buf[:min(n, cap)].tolist()
 
     def workspace_fallbacks(self, nq: int, k: int, workspace) -> int:
-        """K1c queries re-run by the exact pass in the last search_dev() that used `workspace`."""
+        """K1c/K1s queries re-run by the exact fp32 pass in the last search_dev() that used `workspace`."""
         return int(L.fn["cm_dense_workspace_fallbacks"](self._h, int(nq), int(k), L.ptr(workspace)))
 
     def workspace_bytes(self, nq: int, k: int) -> int:

@@ -87,10 +87,18 @@ __global__ void __launch_bounds__(kThreads, 2)
     dense_topk_kernel(const float *__restrict__ C, int ld, const float *__restrict__ invc,
                       const uint32_t *__restrict__ live, const uint32_t *__restrict__ allow, int64_t n_words,
                       const float *__restrict__ qp, const float *__restrict__ invq_g, int nq, int k,
-                      int64_t rows_per_block, int64_t rows_end, int n_cblocks, uint64_t *__restrict__ cand) {
+                      int64_t rows_per_block, int64_t rows_end, int n_cblocks, const int32_t *__restrict__ qmask,
+                      uint64_t *__restrict__ cand) {
   constexpr int QT = QB / 16;
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   const DenseLds L = dense_lds_layout(QB, KMAX, ld);
+  // qmask (K1c/K1s fallback): only queries with qmask[q] != 0 are searched; a workgroup whose
+  // query group has none exits before touching the corpus (block-uniform: no barrier skipped)
+  if (qmask) {
+    const int qq = (int)(blockIdx.x / n_cblocks) * QB + (int)threadIdx.x;
+    const int act = (threadIdx.x < QB && qq < nq) ? qmask[qq] : 0;
+    if (!__syncthreads_or(act)) return;
+  }
   f32x4 *qfrag = reinterpret_cast<f32x4 *>(lds + L.qfrag);
   float *invq = reinterpret_cast<float *>(lds + L.invq);
   uint32_t *cnt = reinterpret_cast<uint32_t *>(lds + L.cnt);
@@ -283,78 +291,38 @@ __global__ void __launch_bounds__(kThreads, 2)
 }
 
 // ---------------------------------------------------------------------------
-// K1b / K1c: batched cosine top-k on normalised fp16 planes, one template.
-//   xn = c * invc (hnswlib normalize_vector), Xh = f16(xn), Xl = f16(xn - Xh).
-//   NPL = 2 (K1b, "f16x3"): reads both planes; xn.qn = xh.qh + xh.ql + xl.qh
-//       (+ xl.ql dropped, <= 2^-22 relative) -> f32-grade distances.
-//   NPL = 1 (K1c, "coarse"): reads only Xh (2 B per element, half of K1/K1b's
-//       HBM bytes) and one product xh.qh per block; the lists hold k' = k + 4
-//       coarse keys per range and dense_rerank_kernel certifies them with a
-//       rigorous error bound before re-ranking the band exactly.
-// A chunk is always 1024 x 16 B = 128 rows x 2 sub-blocks x 32 f16 staged
-// through double-buffered LDS: for NPL = 2 the sub-blocks are the two planes of
-// one 32-deep k slice, for NPL = 1 the two halves of one 64-deep k slice of Xh,
-// so both variants share the LDS image, the load pattern and the fragment reads.
-//
-// One 512-thread workgroup per (corpus range, pass of 256 queries): the whole
-// query pass is resident (wave w owns queries 32w..32w+31, fragments streamed
-// from L2 one chunk ahead), so every corpus byte is read from HBM once per pass.
-// After each 128-row tile every wave filters its 32 x 128 distances against its
-// queries' running k-th keys (a per-query max over the lane's 32 values first, so
-// tiles without a survivor cost one compare per query) and rank-merges survivors
-// into per-query sorted lists in LDS.
+// K1c / K1s: coarse f16 scans + a certified exact re-rank.
+//   xn = c * invc (hnswlib normalize_vector), Xh = f16(xn): the only derived plane kept in HBM
+//   (2 B per element, half of the fp32 rows).  A scan computes xh.qh on the MFMA f16 pipe and
+//   appends every live + allowed row whose coarse distance is under the query's seed to a
+//   (range, query) candidate buffer; dense_rerank_kernel certifies the buffers with a rigorous
+//   error bound and re-ranks the band in fp64 from the fp32 rows.  Queries whose certificate
+//   fails are re-run exactly by K1 (fp32 rows, qmask).
+//   K1c dense_coarse_scan_kernel: a whole pass of 256 queries resident per CU (batched search);
+//   K1s dense_stream_scan_kernel: <= 32 queries, every wave an independent HBM stream of its own
+//     row range (small batches and single queries; no LDS, no barriers).
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
-// Plane layout (Xh, Xl): tile-major, so every 128-row x 64-f16 chunk the scans stream is one
-// contiguous 16 KB block (row-major planes made each chunk 128 row segments 1.5 KB apart and
-// reopened every DRAM page once per chunk):  element (row, k) of a plane with row pitch ld lives
-// at ((row / 128) * (ld / 64) + k / 64) * 8192 + (row % 128) * 64 + k % 64.
+// Plane layout (Xh): fragment-major.  Rows in 64-row tiles, columns in 64-wide chunks; each
+// (tile, chunk) is 8 KB = 8 blocks of 1 KB; block b = 2 rt + sb holds rows 16 rt .. 16 rt + 15 and
+// columns 32 sb .. 32 sb + 31 of the chunk in the MFMA A-operand lane order: lane l = 16 g + j owns
+// row 16 rt + j, columns 32 sb + 8 g .. + 7 (16 B at byte 16 l of the block).  One wave-instruction
+// -- an LDS-DMA piece (K1c) or a 16-B-per-lane load (K1s) -- moves exactly one block, 1 KB
+// contiguous, and the LDS image it leaves is read back conflict-free (lane l reads bytes 16 l).
 __host__ __device__ inline int64_t plane_off(int64_t row, int k, int ld) {
-  return (((row >> 7) * (ld >> 6) + (k >> 6)) << 13) + ((row & 127) << 6) + (k & 63);
+  const int64_t tile = row >> 6;
+  const int rr = (int)(row & 63), rt = rr >> 4, j = rr & 15;
+  const int c = k >> 6, cc = k & 63, sb = cc >> 5, g = (cc >> 3) & 3, e = cc & 7;
+  return (((tile * (ld >> 6) + c) * 8 + rt * 2 + sb) << 9) + ((g * 16 + j) << 3) + e;
 }
-constexpr int kBRows = 128;                 // corpus rows per tile
-constexpr int kBPad = 32;                   // f16 per LDS row (unpadded; 16-B chunks XOR-swizzled, see lds_swz)
-constexpr int kBQPass = 256;                // queries per pass (8 waves x 32)
-constexpr int kBQWave = 32;
-constexpr int kBSlots = 60;                 // per query: sorted list (len <= k) then unmerged survivors
-constexpr int kBMaxK = 32;                  // k <= 32 leaves >= 28 buffer slots (one sub-tile adds <= 16)
-constexpr int kBXBuf = 2 * kBRows * kBPad;  // f16 per LDS stage buffer (2 sub-blocks)
-// 16-B chunk swizzle of an LDS row: chunk c of row r lives at c ^ lds_swz(r).  Conflict-free for
-// both the MFMA fragment reads (ds_read_b128: lanes (g, j) read chunk g of row j; gfx950 serves
-// lane groups {0-3,12-15,20-27}, ... in one cycle each) and the staging writes (ds_write_b128,
-// 8 contiguous lanes = two rows x four chunks), checked exhaustively on the host.
-__host__ __device__ inline int lds_swz(int row) { return ((row >> 3) & 1) << 1; }
+constexpr int kBQPass = 256;                // K1c: queries per pass (4 waves x 64)
+constexpr int kSQ = 32;                     // K1s: queries per launch (<= 2 q-tiles of 16)
+constexpr int kBMaxK = 32;                  // coarse paths: k <= 32
 constexpr int kRerankCap = 1024;            // certified band size per query handled by the re-rank kernel
 
-struct K1bLds {
-  int xs, thr, thrd, cnt, len, list, buf, act, total;
-};
-__host__ __device__ inline K1bLds k1b_lds_layout() {
-  K1bLds L;
-  int off = 0;
-  L.xs = off;
-  off += 2 * kBXBuf * 2;
-  L.thr = off;
-  off += kBQPass * 8;
-  L.list = off;
-  off += kBQPass * kBSlots * 8;
-  L.buf = off;
-  L.thrd = off;
-  off += kBQPass * 4;
-  L.cnt = off;
-  off += kBQPass * 4;
-  L.len = off;
-  off += kBQPass * 4;
-  L.act = off;
-  off += 16;
-  L.total = off;
-  return L;
-}
-
-// Normalise + split queries into Qh/Ql [nq_pad][ld] (zero rows beyond nq) and
-// record per query {||q||, ||qh||, ||ql||} (fp32, for K1c's error bound).
+// Normalise queries into Qh [nq_pad][ld] (zero rows beyond nq) and record per query
+// {||q||, ||qh||, ||ql||} (fp32, ql = qn - qh: K1c/K1s's error bound).
 __global__ void __launch_bounds__(256) dense_prep_planes(const float *__restrict__ q, int nq, int dim, int ld,
-                                                         _Float16 *__restrict__ Qh, _Float16 *__restrict__ Ql,
-                                                         float *__restrict__ qnorm) {
+                                                         _Float16 *__restrict__ Qh, float *__restrict__ qnorm) {
   const int qi = blockIdx.x;
   const float *src = q + (int64_t)qi * dim;
   float s = 0.f;
@@ -372,11 +340,10 @@ __global__ void __launch_bounds__(256) dense_prep_planes(const float *__restrict
   for (int i = threadIdx.x; i < ld; i += 256) {
     const float v = (qi < nq && i < dim) ? src[i] * inv : 0.f;
     const _Float16 hi = (_Float16)v;
-    const _Float16 lo = (_Float16)(v - (float)hi);
+    const float lo = (float)(_Float16)(v - (float)hi);
     Qh[(int64_t)qi * ld + i] = hi;
-    Ql[(int64_t)qi * ld + i] = lo;
     sh += (float)hi * (float)hi;
-    sl += (float)lo * (float)lo;
+    sl += lo * lo;
   }
   for (int o = 32; o > 0; o >>= 1) {
     sh += __shfl_xor(sh, o);
@@ -395,267 +362,6 @@ __global__ void __launch_bounds__(256) dense_prep_planes(const float *__restrict
   }
 }
 
-// qmask (nullable): only queries with qmask[q] != 0 are searched (K1c's fallback
-// pass); a workgroup whose pass has none exits before touching the corpus.
-template <int NPL>
-__global__ void __launch_bounds__(512, 1)
-    dense_split_kernel(const _Float16 *__restrict__ Xh, const _Float16 *__restrict__ Xl, int ld,
-                       const uint32_t *__restrict__ live, const uint32_t *__restrict__ allow, int64_t n_words,
-                       const _Float16 *__restrict__ Qh, const _Float16 *__restrict__ Ql, int nq,
-                       const int32_t *__restrict__ qmask, int k, int64_t rows_per_wg, int64_t rows_end, int n_wg,
-                       uint64_t *__restrict__ cand, int dbg) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-  const K1bLds L = k1b_lds_layout();
-  _Float16 *xs = reinterpret_cast<_Float16 *>(lds + L.xs);
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int g = lane >> 4;
-  const int j = lane & 15;
-  const int wg = blockIdx.x % n_wg;
-  const int qp = blockIdx.x / n_wg;
-  const int qw0 = wave * kBQWave;            // wave's first query within the pass
-  const int qg0 = qp * kBQPass + qw0;        // ... globally
-  uint64_t *thr = reinterpret_cast<uint64_t *>(lds + L.thr) + qw0;
-  float *thrd = reinterpret_cast<float *>(lds + L.thrd) + qw0;
-  uint32_t *cnt = reinterpret_cast<uint32_t *>(lds + L.cnt) + qw0;
-  uint32_t *len = reinterpret_cast<uint32_t *>(lds + L.len) + qw0;
-  uint64_t *list = reinterpret_cast<uint64_t *>(lds + L.list) + (int64_t)qw0 * kBSlots;
-  int32_t *act = reinterpret_cast<int32_t *>(lds + L.act);
-  if (qmask) {
-    if (tid == 0) act[0] = 0;
-    __syncthreads();
-    const int qq = qp * kBQPass + tid;
-    if (tid < kBQPass && qq < nq && qmask[qq]) act[0] = 1;
-    __syncthreads();
-    if (act[0] == 0) return;  // whole workgroup: no query of this pass is active
-  }
-  if (lane < kBQWave) {
-    const int qq = qg0 + lane;
-    const bool real = qq < nq && (!qmask || qmask[qq]);
-    thr[lane] = real ? kEmptyKey : 0ull;  // padded / inactive queries accept nothing
-    thrd[lane] = real ? __builtin_inff() : -__builtin_inff();
-    cnt[lane] = 0;
-    len[lane] = 0;
-  }
-  const int64_t r_begin = (int64_t)wg * rows_per_wg;
-  const int64_t r_end = min(r_begin + rows_per_wg, rows_end);
-  const int ntiles = r_begin < r_end ? (int)((r_end - r_begin) / kBRows) : 0;
-  const int KC = ld / (32 * (3 - NPL));  // chunks per tile: 32-deep (NPL 2) or 64-deep (NPL 1)
-  const int total = ntiles * KC;
-
-  // staging pieces of a chunk: 1024 x 16 B (sub-block, row, 8-f16 part); thread takes tid and tid + 512
-  auto xsrc = [&](int gc, int p) -> const f16x8 * {
-    const int t = gc / KC, c = gc - t * KC;
-    const int sb = p >> 9, row = (p & 511) >> 2, part = p & 3;
-    const int64_t rg = r_begin + (int64_t)t * kBRows + row;
-    if (NPL == 2) return reinterpret_cast<const f16x8 *>((sb ? Xl : Xh) + plane_off(rg, c * 32 + part * 8, ld));
-    return reinterpret_cast<const f16x8 *>(Xh + plane_off(rg, c * 64 + sb * 32 + part * 8, ld));
-  };
-  auto xdst = [&](int b, int p) -> f16x8 * {
-    const int sb = p >> 9, row = (p & 511) >> 2, part = p & 3;
-    return reinterpret_cast<f16x8 *>(xs + b * kBXBuf + sb * kBRows * kBPad + row * kBPad + (part ^ lds_swz(row)) * 8);
-  };
-  // query fragments (B operand): lane (g, j) of q-tile qt holds q[qt*16 + j][.. + 8g .. +7] of
-  // sub-block 0 (qa) and 1 (qb): NPL 2 -> (Qh, Ql) of the 32-deep slice, NPL 1 -> Qh halves
-  auto qload = [&](f16x8 (&qa)[2], f16x8 (&qb)[2], int gc) {
-    const int c = gc % KC;
-#pragma unroll
-    for (int qt = 0; qt < 2; ++qt) {
-      const int64_t rb = (int64_t)(qg0 + qt * 16 + j) * ld;
-      if (NPL == 2) {
-        qa[qt] = *reinterpret_cast<const f16x8 *>(Qh + rb + c * 32 + g * 8);
-        qb[qt] = *reinterpret_cast<const f16x8 *>(Ql + rb + c * 32 + g * 8);
-      } else {
-        qa[qt] = *reinterpret_cast<const f16x8 *>(Qh + rb + c * 64 + g * 8);
-        qb[qt] = *reinterpret_cast<const f16x8 *>(Qh + rb + c * 64 + 32 + g * 8);
-      }
-    }
-  };
-  f32x4 acc[8][2];
-#pragma unroll
-  for (int rt = 0; rt < 8; ++rt) acc[rt][0] = acc[rt][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  // rank-merge query q's slots [0, len + cnt) in place into its sorted list (<= k): one key per lane
-  auto merge = [&](int q) {
-    uint64_t *sl = list + q * kBSlots;
-    const uint32_t n = len[q] + cnt[q];
-    const uint64_t key = (uint32_t)lane < n ? sl[lane] : kEmptyKey;
-    uint32_t rank = 0;
-    for (uint32_t i = 0; i < n; ++i) rank += (sl[i] < key) ? 1u : 0u;
-    __builtin_amdgcn_wave_barrier();  // every lane has read the old slots
-    if ((uint32_t)lane < n && rank < (uint32_t)k) {
-      sl[rank] = key;
-      if (rank == (uint32_t)k - 1) {
-        thr[q] = key;
-        thrd[q] = f32_unorder((uint32_t)(key >> 32));
-      }
-    }
-    if (lane == 0) {
-      len[q] = min(n, (uint32_t)k);
-      cnt[q] = 0;
-    }
-  };
-  auto wave_lds_sync = [] {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  };
-  // merge every query of the wave whose free slots could not take another sub-tile (or all
-  // queries with anything buffered, at the end)
-  auto merge_pending = [&](bool all) {
-    wave_lds_sync();
-    bool need = false;
-    if (lane < kBQWave) {
-      const uint32_t c = cnt[lane];
-      need = all ? c > 0 : len[lane] + c + 16 > (uint32_t)kBSlots;
-    }
-    uint64_t m = __ballot(need);
-    while (m) {
-      const int q = __builtin_ctzll(m);
-      m &= m - 1;
-      merge(q);
-      wave_lds_sync();
-    }
-  };
-  // epilogue of tile t (wave-private queries, no block barrier): survivors of the running
-  // k-th key are appended to the query's free slots; a sub-tile adds <= 16 per query (4 lanes
-  // x 4 rows), and queries are merged only when fewer than 16 slots remain
-  auto epilogue = [&](int t) {
-    const int64_t row0 = r_begin + (int64_t)t * kBRows;
-    uint32_t bits[4];
-#pragma unroll
-    for (int w = 0; w < 4; ++w) {
-      const int64_t wi = (row0 >> 5) + w;
-      bits[w] = wi < n_words ? (live[wi] & (allow ? allow[wi] : 0xffffffffu)) : 0u;
-    }
-#pragma unroll
-    for (int qt = 0; qt < 2; ++qt) {
-      const int ql_ = qt * 16 + j;
-      // quick reject: the lane's best of its 32 rows for this query against the running k-th
-      float mx = acc[0][qt][0];
-#pragma unroll
-      for (int rt = 0; rt < 8; ++rt)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) mx = fmaxf(mx, acc[rt][qt][r]);
-      if (__ballot(1.0f - mx <= thrd[ql_]) == 0) continue;
-#pragma unroll
-      for (int rt = 0; rt < 8; ++rt) {
-        const float td = thrd[ql_];
-        const uint64_t tk = thr[ql_];
-        bool added = false;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int rr = rt * 16 + 4 * g + r;  // row within the tile
-          const float dist = 1.0f - acc[rt][qt][r];
-          if (((bits[rr >> 5] >> (rr & 31)) & 1u) && dist <= td) {
-            const uint64_t key = ((uint64_t)f32_order(dist) << 32) | (uint64_t)(uint32_t)(row0 + rr);
-            if (key < tk && !(dbg & 16)) {
-              list[ql_ * kBSlots + len[ql_] + atomicAdd(&cnt[ql_], 1u)] = key;
-              added = true;
-            }
-          }
-        }
-        if (__ballot(added)) merge_pending(false);
-      }
-    }
-#pragma unroll
-    for (int rt = 0; rt < 8; ++rt) acc[rt][0] = acc[rt][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-  };
-
-  if (total > 0) {
-    // X chunks gc+1..gc+4 in flight in a 4-deep register ring (HBM latency ~ 3-4 chunks of
-    // MFMA work); query fragments one chunk ahead (L2).  KC is a multiple of 4 (checked on
-    // the host), so a tile is a whole number of ring turns and the epilogue (no vector-memory
-    // loads) sits outside the unrolled bodies: every wait is a counted vmcnt, not a drain.
-    f16x8 qa[2], qb[2], nqa[2], nqb[2];
-    f16x8 ra0, ra1, rb0, rb1, rc0, rc1, rd0, rd1;
-    auto xload = [&](f16x8 &x0, f16x8 &x1, int gc) {
-      const int gl = min(gc, total - 1);  // clamped: one control path
-      x0 = *xsrc(gl, tid);
-      x1 = *xsrc(gl, tid + 512);
-    };
-    xload(ra0, ra1, 0);
-    *xdst(0, tid) = ra0;
-    *xdst(0, tid + 512) = ra1;
-    qload(qa, qb, 0);
-    xload(ra0, ra1, 1);
-    xload(rb0, rb1, 2);
-    xload(rc0, rc1, 3);
-    xload(rd0, rd1, 4);
-    __syncthreads();
-    auto body = [&](int gc, f16x8 &x0, f16x8 &x1) {
-      qload(nqa, nqb, min(gc + 1, total - 1));
-      const _Float16 *xb = xs + (gc & 1) * kBXBuf;
-      auto frag = [&](int rt, int sb) -> f16x8 {
-        return *reinterpret_cast<const f16x8 *>(xb + sb * kBRows * kBPad + (rt * 16 + j) * kBPad +
-                                                (g ^ lds_swz(j)) * 8);
-      };
-      // LDS fragments one 16-row sub-tile ahead of the MFMAs that use them
-      f16x8 xa = frag(0, 0), xb1 = frag(0, 1);
-#pragma unroll
-      for (int rt = 0; rt < 8; ++rt) {
-        f16x8 na = xa, nb = xb1;
-        if (rt < 7) {
-          na = frag(rt + 1, 0);
-          nb = frag(rt + 1, 1);
-        }
-#pragma unroll
-        for (int qt = 0; qt < 2; ++qt) {
-          if (NPL == 2) {
-            acc[rt][qt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xa, qa[qt], acc[rt][qt], 0, 0, 0);
-            acc[rt][qt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xa, qb[qt], acc[rt][qt], 0, 0, 0);
-            acc[rt][qt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xb1, qa[qt], acc[rt][qt], 0, 0, 0);
-          } else {
-            acc[rt][qt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xa, qa[qt], acc[rt][qt], 0, 0, 0);
-            acc[rt][qt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xb1, qb[qt], acc[rt][qt], 0, 0, 0);
-          }
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        xa = na;
-        xb1 = nb;
-      }
-      *xdst((gc + 1) & 1, tid) = x0;  // chunk gc+1 (loaded four chunks ago)
-      *xdst((gc + 1) & 1, tid + 512) = x1;
-      xload(x0, x1, gc + 5);
-      __syncthreads();
-#pragma unroll
-      for (int qt = 0; qt < 2; ++qt) {
-        qa[qt] = nqa[qt];
-        qb[qt] = nqb[qt];
-      }
-    };
-    for (int t = 0; t < ntiles; ++t) {
-      for (int c = 0; c < KC; c += 4) {
-        const int gc = t * KC + c;
-        body(gc, ra0, ra1);
-        body(gc + 1, rb0, rb1);
-        body(gc + 2, rc0, rc1);
-        body(gc + 3, rd0, rd1);
-      }
-      if (dbg & 1) {  // ablation: consume the accumulators without the top-k epilogue
-        float z = 0.f;
-#pragma unroll
-        for (int rt = 0; rt < 8; ++rt)
-#pragma unroll
-          for (int qt = 0; qt < 2; ++qt) z += acc[rt][qt][0] + acc[rt][qt][3];
-        if (z == 12345.f) thrd[lane & 31] = z;
-#pragma unroll
-        for (int rt = 0; rt < 8; ++rt) acc[rt][0] = acc[rt][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-      } else {
-        epilogue(t);
-      }
-    }
-  }
-  merge_pending(true);
-  // this range's sorted lists (layout of dense_merge_kernel with QB = kBQPass)
-  for (int idx = lane; idx < kBQWave * k; idx += 64) {
-    const int q = idx / k, i = idx - q * k;
-    const uint64_t v = (uint32_t)i < len[q] ? list[q * kBSlots + i] : kEmptyKey;
-    cand[(((int64_t)qp * n_wg + wg) * kBQPass + qw0 + q) * k + i] = v;
-  }
-}
-
 // Waves per K1c workgroup.  4 (one per SIMD) is the measured best: 8 (two per SIMD, 32 queries
 // each, 256 VGPRs with 16 spilled at tile boundaries) ran 5.63 vs 4.96 ms on the 10M x 768 scan --
 // the second wave did not hide barrier/epilogue time.  Kept selectable for experiments.
@@ -664,29 +370,13 @@ __global__ void __launch_bounds__(512, 1)
 #endif
 constexpr int kK1cWaves = K1C_WAVES;
 
-// K1c's per-query error bound E (see dense_rerank_kernel).
+// K1c/K1s per-query error bound E (see dense_rerank_kernel).
 __device__ inline float coarse_err(const float *qnorm, int qi, const float *row_norms, int dim) {
   const float qh = qnorm[4 * qi + 1], qlo = qnorm[4 * qi + 2];
   const float mxh = row_norms[0], mxl = row_norms[1];
   return (qlo * mxh + mxl * qh + mxl * qlo + (float)dim * 5.9604645e-8f * mxh * qh + 2e-6f) * 1.001f;
 }
 
-// ---------------------------------------------------------------------------
-// K1c scan (coarse f16, Xh plane only), resident-query form for ld = 64 KC.
-// 64 W threads (W = kK1cWaves: 4 -> one wave per SIMD, 8 -> two, so one wave's barrier wait, DMA
-// issue and epilogue hide under the other's MFMAs); wave w owns queries 256w/W.. of the 256-query pass and
-// keeps their Qh fragments resident -- chunks 0..KC-NQL-1 in registers (32 VGPRs each), the last
-// NQL chunks in LDS -- so the corpus is the only memory stream: 64-row x 64-f16 chunks (8 KB; one
-// glds wave-instruction = 8 rows x 128 B, full lines) LDS-DMA'd into a kRRing-slot ring, retired
-// by a counted vmcnt and published by a raw s_barrier: no vmcnt(0) and no query reloads in the
-// loop.  The ring image is 128-B rows with 16-B chunks XOR-swizzled by (row >> 1) & 7 on the glds
-// SOURCE address (the DMA writes lane-linearly) and on the ds_read address: conflict-free
-// fragment reads (checked exhaustively on the host).  Compute tiles are 64 rows.
-//   MINONLY (sample pre-pass): per query, the minimum coarse distance over the workgroup's
-//     live+allowed rows -> out_min[pass][wg][q].
-//   main pass: every live+allowed row with coarse distance <= seed[q] is appended to the
-//     (range, query) candidate buffer out_keys[pass][wg][q][kCBufCap] (LDS slot counter);
-//     out_cnt[pass][wg][q] = appended count (> kCBufCap: the buffer overflowed).
 #ifndef K1C_RING
 #define K1C_RING 8
 #endif
@@ -694,13 +384,77 @@ constexpr int kRRing = K1C_RING;  // LDS ring slots (8 KB each): kRRing - 1 chun
 constexpr int kRRows = 64;      // rows per compute tile / chunk
 constexpr int kCBufCap = 64;    // candidate slots per (range, query)
 
+// Per-tile candidate epilogue shared by K1c and K1s.  acc[rt][qt][r] is the coarse product of
+// row rt*16 + 4g + r of the tile with query qt*16 + j (lane (g, j)); tmask its 64 live & allow
+// bits.  MINONLY: running minimum coarse distance per query.  Otherwise every row with coarse
+// distance <= sd[qt] is appended to the query's buffer dst(qt) (slots by ballot + popcount among
+// the 4 lanes g = 0..3 sharing query j; the count lives in lane j's register, no LDS atomics).
+template <int QT, bool MINONLY, typename Dst>
+__device__ __attribute__((always_inline)) inline void coarse_epilogue(const f32x4 (&acc)[4][QT], uint64_t tmask,
+                                                                      int64_t row0, const float (&sd)[QT],
+                                                                      float (&best)[QT], uint32_t (&qcnt)[QT],
+                                                                      Dst dst) {
+  const int lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15;
+#pragma unroll
+  for (int qt = 0; qt < QT; ++qt) {
+    if (MINONLY) {
+      float m = __builtin_inff();
+#pragma unroll
+      for (int rt = 0; rt < 4; ++rt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if ((tmask >> (rt * 16 + 4 * g + r)) & 1u) m = fminf(m, 1.0f - acc[rt][qt][r]);
+      best[qt] = fminf(best[qt], m);
+    } else {
+      float mx = -__builtin_inff();
+#pragma unroll
+      for (int rt = 0; rt < 4; ++rt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) mx = fmaxf(mx, acc[rt][qt][r]);
+      if (__ballot(1.0f - mx <= sd[qt]) == 0) continue;  // no row of the tile under any seed
+      const uint64_t samej = 0x0001000100010001ull << j;
+      uint64_t *d = dst(qt);
+#pragma unroll
+      for (int rt = 0; rt < 4; ++rt) {
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int rr = rt * 16 + 4 * g + r;
+          const float dist = 1.0f - acc[rt][qt][r];
+          const bool pred = ((tmask >> rr) & 1u) && dist <= sd[qt];
+          const uint64_t m = __ballot(pred);
+          if (m == 0) continue;
+          const uint32_t base = __shfl(qcnt[qt], j);
+          const uint32_t slot = base + (uint32_t)__popcll(m & samej & ((1ull << lane) - 1ull));
+          if (pred && slot < (uint32_t)kCBufCap)
+            d[slot] = ((uint64_t)f32_order(dist) << 32) | (uint64_t)(uint32_t)(row0 + rr);
+          if (g == 0) qcnt[qt] += (uint32_t)__popcll(m & samej);
+        }
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// K1c scan (coarse f16, Xh plane only), resident-query form for ld = 64 KC.
+// 64 W threads (W = kK1cWaves: 4 -> one wave per SIMD, 8 -> two); wave w owns queries 256w/W.. of
+// the 256-query pass and keeps their Qh fragments resident -- chunks 0..KC-NQL-1 in registers (32
+// VGPRs each), the last NQL chunks in LDS -- so the corpus is the only memory stream: 64-row x
+// 64-f16 chunks (8 KB = 8 fragment blocks; one glds wave-instruction = one 1 KB block) LDS-DMA'd
+// into a kRRing-slot ring, retired by a counted vmcnt and published by a raw s_barrier: no
+// vmcnt(0) and no query reloads in the loop.  The ring image is the plane's fragment-major block
+// order, read back lane-linearly (conflict-free).  Compute tiles are 64 rows.
+//   MINONLY (sample pre-pass): per query, the minimum coarse distance over the workgroup's
+//     live+allowed rows -> out_min[pass][wg][q].
+//   main pass: every live+allowed row with coarse distance <= seed[q] is appended to the
+//     (range, query) candidate buffer out_keys[pass][wg][q][kCBufCap];
+//     out_cnt[pass][wg][q] = appended count (> kCBufCap: the buffer overflowed).
 template <int NQL>
 struct K1rLds {
   static constexpr int ring = 0;
   static constexpr int qf = ring + kRRing * 8192;          // [NQL][W waves][32/W frags][64 lanes] x 16 B
   static constexpr int total = qf + NQL * 4 * 8 * 1024;
 };
-__device__ inline int ring_swz(int row) { return (row >> 1) & 7; }
 
 template <int KC, int NQL, bool MINONLY, int W>
 __global__ void __launch_bounds__(64 * W, 1)
@@ -714,7 +468,7 @@ __global__ void __launch_bounds__(64 * W, 1)
   using LL = K1rLds<NQL>;
   constexpr int QT = 16 / W;        // 16-query tiles per wave
   constexpr int NF = 2 * QT;        // query fragments per wave and chunk
-  constexpr int PCS = 8 / W;        // 16-B DMA pieces per thread and chunk
+  constexpr int PCS = 8 / W;        // 1 KB DMA pieces per wave and chunk
   static_assert(W == 4 || W == 8, "K1c: 4 or 8 waves");
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   const int tid = threadIdx.x;
@@ -762,21 +516,19 @@ __global__ void __launch_bounds__(64 * W, 1)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();  // LDS query fragments ready; no DMA in flight yet
 
-  // glds source of wave-instruction i (< PCS) of chunk gc: ring cell o16 = 64 W i + tid holds the
-  // 16-B piece (row o16 >> 3, logical chunk (o16 & 7) ^ ring_swz(row)) of the tile-major plane
+  // glds of chunk gc: wave-instruction i moves fragment block o = W i + wave (1 KB, lane-linear)
+  const __attribute__((address_space(1))) unsigned char *Xb =
+      (const __attribute__((address_space(1))) unsigned char *)Xh;
   auto issue = [&](int gc) __attribute__((always_inline)) {
     const int gl = min(gc, total - 1);  // clamped: one control path past the end
     const int t = gl / KC, c = gl - t * KC;
-    const int64_t R0 = r_begin + (int64_t)t * kRRows;
+    const int64_t tile = (r_begin >> 6) + t;
     unsigned char *slot = lds + LL::ring + (gc % kRRing) * 8192;
 #pragma unroll
     for (int i = 0; i < PCS; ++i) {
-      const int o16 = 64 * W * i + tid;
-      const int row = o16 >> 3, lg = (o16 & 7) ^ ring_swz(row);
-      const _Float16 *src = Xh + ((((R0 >> 7) * KC + c) << 13) + (((R0 & 127) + row) << 6) + lg * 8);
-      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)src,
-                                       (__attribute__((address_space(3))) void *)(slot + i * W * 1024 + wave * 1024), 16,
-                                       0, 0);
+      const int o = W * i + wave;
+      __builtin_amdgcn_global_load_lds(Xb + (((tile * KC + c) * 8 + o) << 10) + lane * 16,
+                                       (__attribute__((address_space(3))) void *)(slot + o * 1024), 16, 0, 0);
     }
   };
   f32x4 acc[4][QT];
@@ -788,59 +540,15 @@ __global__ void __launch_bounds__(64 * W, 1)
   uint32_t tile_words = 0;  // lanes 0, 1: live & allow words of the current tile
   auto epilogue = [&](int t) __attribute__((always_inline)) {
     const int64_t row0 = r_begin + (int64_t)t * kRRows;
-    const int64_t w0 = row0 >> 5;  // wave-uniform: scalar loads, outside the DMA's vmcnt queue
     // lane (g, j) holds rows rt*16 + 4g + r: bit (16 rt + 4 g + r) of the 64-bit tile mask, whose
-    // two words lanes 0 and 1 loaded when the tile started (tile_words: a vector load that lands
-    // during the tile's chunks instead of a scalar load waited for here)
-    (void)w0;
-    auto tile_mask = [&]() -> uint64_t {
-      const uint32_t b0 = (uint32_t)__builtin_amdgcn_readlane((int)tile_words, 0);
-      const uint32_t b1 = (uint32_t)__builtin_amdgcn_readlane((int)tile_words, 1);
-      return ((uint64_t)b1 << 32) | b0;
-    };
-    const uint64_t tmask = MINONLY ? tile_mask() : 0ull;
-#pragma unroll
-    for (int qt = 0; qt < QT; ++qt) {
-      if (MINONLY) {
-        float m = __builtin_inff();
-#pragma unroll
-        for (int rt = 0; rt < 4; ++rt)
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            if ((tmask >> (rt * 16 + 4 * g + r)) & 1u) m = fminf(m, 1.0f - acc[rt][qt][r]);
-        best[qt] = fminf(best[qt], m);
-      } else {
-        float mx = -__builtin_inff();
-#pragma unroll
-        for (int rt = 0; rt < 4; ++rt)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) mx = fmaxf(mx, acc[rt][qt][r]);
-        if (__ballot(1.0f - mx <= sd[qt]) == 0) continue;  // no row of the tile under any seed
-        const uint64_t tmask = tile_mask();
-        // slots by ballot + popcount among the 4 lanes (g = 0..3) sharing query j; the count
-        // lives in lane j's register (no LDS atomics: those would wait for the ring's DMAs)
-        const int q = qc0 + qt * 16 + j;
-        const uint64_t samej = 0x0001000100010001ull << j;
-        uint64_t *dst = out_keys + (((int64_t)qp * n_wg + wg) * kBQPass + q) * kCBufCap;
-#pragma unroll
-        for (int rt = 0; rt < 4; ++rt) {
-          __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int rr = rt * 16 + 4 * g + r;
-            const float dist = 1.0f - acc[rt][qt][r];
-            const bool pred = ((tmask >> rr) & 1u) && dist <= sd[qt];
-            const uint64_t m = __ballot(pred);
-            if (m == 0) continue;
-            const uint32_t base = __shfl(qcnt[qt], j);
-            const uint32_t slot = base + (uint32_t)__popcll(m & samej & ((1ull << lane) - 1ull));
-            if (pred && slot < (uint32_t)kCBufCap)
-              dst[slot] = ((uint64_t)f32_order(dist) << 32) | (uint64_t)(uint32_t)(row0 + rr);
-            if (g == 0) qcnt[qt] += (uint32_t)__popcll(m & samej);
-          }
-        }
-      }
-    }
+    // two words lanes 0 and 1 loaded when the tile started (a vector load that lands during the
+    // tile's chunks instead of a scalar load waited for here)
+    const uint32_t b0 = (uint32_t)__builtin_amdgcn_readlane((int)tile_words, 0);
+    const uint32_t b1 = (uint32_t)__builtin_amdgcn_readlane((int)tile_words, 1);
+    const uint64_t tmask = ((uint64_t)b1 << 32) | b0;
+    coarse_epilogue<QT, MINONLY>(acc, tmask, row0, sd, best, qcnt, [&](int qt) {
+      return out_keys + (((int64_t)qp * n_wg + wg) * kBQPass + qc0 + qt * 16 + j) * kCBufCap;
+    });
 #pragma unroll
     for (int rt = 0; rt < 4; ++rt)
 #pragma unroll
@@ -856,8 +564,7 @@ __global__ void __launch_bounds__(64 * W, 1)
     // barrier, DMA issue and LDS read thus sits behind >= 16 MFMAs instead of in front of them.
     auto frag = [&](int gc, int rt, int sb) -> f16x8 {
       const unsigned char *slot = lds + LL::ring + (gc % kRRing) * 8192;
-      const int row = rt * 16 + j;
-      return *reinterpret_cast<const f16x8 *>(slot + row * 128 + (((sb * 4 + g) ^ ring_swz(row)) << 4));
+      return *reinterpret_cast<const f16x8 *>(slot + (rt * 2 + sb) * 1024 + lane * 16);
     };
 #pragma unroll
     for (int p = 0; p < kRRing - 1; ++p) issue(p);
@@ -955,19 +662,133 @@ __global__ void __launch_bounds__(64 * W, 1)
   }
 }
 
+// ---------------------------------------------------------------------------
+// K1s: coarse f16 scan for nq <= 16 QT queries (single queries, small batches: SURVEY §8d C2'
+// at B = 16), HBM streaming.  Every wave is an independent "virtual group" vg owning a contiguous
+// run of 64-row tiles; its queries' Qh fragments stay in registers for the whole launch, the
+// plane's fragment blocks go straight to registers (each load instruction = one contiguous 1 KB
+// block, 16 B per lane) through a ring of R chunks (R - 1 in flight: 24 KB per wave, 96 KB per
+// CU) and feed v_mfma_f32_16x16x32_f16 without any LDS round trip, barrier or cross-wave
+// hand-off.  Output layout = K1c's with n_wg = n_vg groups and a pass of qs queries, so the seed
+// and re-rank kernels are shared.
+template <int KC, int QT, bool MINONLY>
+__global__ void __launch_bounds__(256, 1)
+    dense_stream_scan_kernel(const _Float16 *__restrict__ Xh, const uint32_t *__restrict__ live,
+                             const uint32_t *__restrict__ allow, int64_t n_words, const _Float16 *__restrict__ Qh,
+                             int nq, const float *__restrict__ seed, int64_t rows_per_vg, int64_t rows_end, int n_vg,
+                             int qs, uint64_t *__restrict__ out_keys, uint32_t *__restrict__ out_cnt,
+                             float *__restrict__ out_min) {
+  constexpr int ld = 64 * KC;
+  constexpr int R = (KC % 4 == 0) ? 4 : 3;  // register ring (chunks), KC % R == 0 keeps indices static
+  static_assert(KC % R == 0, "K1s: ring must divide the chunks per tile");
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int g = lane >> 4, j = lane & 15;
+  const int vg = blockIdx.x * 4 + wave;
+  if (vg >= n_vg) return;  // wave-uniform; the kernel has no barriers
+  const int64_t r_begin = (int64_t)vg * rows_per_vg;
+  const int64_t r_end = min(r_begin + rows_per_vg, rows_end);
+  const int ntiles = r_begin < r_end ? (int)((r_end - r_begin) / kRRows) : 0;
+  const int total = ntiles * KC;
+
+  f16x8 qf[KC][2][QT];
+#pragma unroll
+  for (int c = 0; c < KC; ++c)
+#pragma unroll
+    for (int sb = 0; sb < 2; ++sb)
+#pragma unroll
+      for (int qt = 0; qt < QT; ++qt)
+        qf[c][sb][qt] = *reinterpret_cast<const f16x8 *>(Qh + (int64_t)(qt * 16 + j) * ld + c * 64 + sb * 32 + g * 8);
+  float sd[QT], best[QT];
+  uint32_t qcnt[QT];
+#pragma unroll
+  for (int qt = 0; qt < QT; ++qt) {
+    best[qt] = __builtin_inff();
+    qcnt[qt] = 0u;
+    const int qq = qt * 16 + j;
+    sd[qt] = MINONLY ? 0.f : (qq < nq ? seed[qq] : -__builtin_inff());
+  }
+  f32x4 acc[4][QT];
+#pragma unroll
+  for (int rt = 0; rt < 4; ++rt)
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt) acc[rt][qt] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if (total > 0) {
+    const f16x8 *Xv = reinterpret_cast<const f16x8 *>(Xh);
+    const int64_t tile0 = r_begin >> 6;
+    f16x8 xb[R][8];
+    auto load = [&](f16x8 (&b)[8], int gc) __attribute__((always_inline)) {
+      const int gl = min(gc, total - 1);  // clamped: one control path past the end
+      const int t = gl / KC, c = gl - t * KC;
+      const f16x8 *p = Xv + ((tile0 + t) * KC + c) * 512 + lane;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) b[i] = p[i * 64];
+    };
+#pragma unroll
+    for (int p = 0; p < R - 1; ++p) load(xb[p], p);
+    for (int t = 0; t < ntiles; ++t) {
+      uint32_t tile_words;
+      {
+        const int64_t wi = ((r_begin + (int64_t)t * kRRows) >> 5) + (lane & 1);
+        tile_words = wi < n_words ? (live[wi] & (allow ? allow[wi] : 0xffffffffu)) : 0u;
+      }
+#pragma unroll
+      for (int c = 0; c < KC; ++c) {
+        const int gc = t * KC + c;
+        load(xb[(c + R - 1) % R], gc + R - 1);  // into the slot chunk gc - 1 used
+        __builtin_amdgcn_sched_barrier(0);
+        const int s = c % R;
+#pragma unroll
+        for (int rt = 0; rt < 4; ++rt)
+#pragma unroll
+          for (int sb = 0; sb < 2; ++sb)
+#pragma unroll
+            for (int qt = 0; qt < QT; ++qt)
+              acc[rt][qt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xb[s][rt * 2 + sb], qf[c][sb][qt], acc[rt][qt], 0,
+                                                                  0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      const int64_t row0 = r_begin + (int64_t)t * kRRows;
+      const uint32_t b0 = (uint32_t)__builtin_amdgcn_readlane((int)tile_words, 0);
+      const uint32_t b1 = (uint32_t)__builtin_amdgcn_readlane((int)tile_words, 1);
+      coarse_epilogue<QT, MINONLY>(acc, ((uint64_t)b1 << 32) | b0, row0, sd, best, qcnt, [&](int qt) {
+        return out_keys + ((int64_t)vg * qs + qt * 16 + j) * kCBufCap;
+      });
+#pragma unroll
+      for (int rt = 0; rt < 4; ++rt)
+#pragma unroll
+        for (int qt = 0; qt < QT; ++qt) acc[rt][qt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  }
+  if (MINONLY) {
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt) {
+      float m = best[qt];
+      m = fminf(m, __shfl_xor(m, 16));
+      m = fminf(m, __shfl_xor(m, 32));
+      if (g == 0) out_min[(int64_t)vg * qs + qt * 16 + j] = m;
+    }
+  } else if (g == 0) {
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt) out_cnt[(int64_t)vg * qs + qt * 16 + j] = qcnt[qt];
+  }
+}
+
 // K1c seed from the sample pre-pass: the k-th smallest of the n_wg per-workgroup minima bounds the
 // k-th smallest coarse distance of the whole corpus (k distinct rows lie at or under it); + 2E.
 // +inf when fewer than k groups hold an allowed row.
-__global__ void __launch_bounds__(256) dense_seed_kernel(const float *__restrict__ mins, int n_wg, int k, int nq,
-                                                         const float *__restrict__ qnorm,
+// qs = queries per pass in the buffer layout (K1c: kBQPass, K1s: kSQ).
+__global__ void __launch_bounds__(256) dense_seed_kernel(const float *__restrict__ mins, int n_wg, int qs, int k,
+                                                         int nq, const float *__restrict__ qnorm,
                                                          const float *__restrict__ row_norms, int dim,
                                                          float *__restrict__ seed) {
   const int qi = blockIdx.x;
   if (qi >= nq) return;
-  const int qp = qi / kBQPass, ql = qi - qp * kBQPass;
+  const int qp = qi / qs, ql = qi - qp * qs;
   __shared__ float v[2048];
   const int n = min(n_wg, 2048);
-  for (int i = threadIdx.x; i < n; i += 256) v[i] = mins[((int64_t)qp * n_wg + i) * kBQPass + ql];
+  for (int i = threadIdx.x; i < n; i += 256) v[i] = mins[((int64_t)qp * n_wg + i) * qs + ql];
   __syncthreads();
   // the k-th smallest by rank counting (n <= 2048, ties broken by index)
   __shared__ float kth;
@@ -1020,19 +841,19 @@ __device__ inline uint32_t block_select_u32(const uint32_t *vals, int n, int kk,
 //   the recursive-summation bound, 2e-6 for the normalisations).  With c_k the k-th smallest
 //   coarse distance, every row of the exact top-k has c <= T = c_k + 2E <= seed, so it sits in
 //   one of the n_wg candidate buffers unless that buffer overflowed (or the band exceeds
-//   kRerankCap): then the query is flagged for the exact K1b pass.  Otherwise the band's rows are
+//   kRerankCap): then the query is flagged for the exact fp32 K1 pass.  Otherwise the band's rows are
 //   re-ranked with fp64 dot products of the stored fp32 rows,
 //   d = 1 - (c.q) / ((||c|| + 1e-30)(||q|| + 1e-30)), ties -> lower row.
 constexpr int kGatherCap = 8192;  // candidates gathered per query
 __global__ void __launch_bounds__(256) dense_rerank_kernel(
-    const uint64_t *__restrict__ keys, const uint32_t *__restrict__ cnts, int n_wg, int k, int nq,
+    const uint64_t *__restrict__ keys, const uint32_t *__restrict__ cnts, int n_wg, int qs, int k, int nq,
     const float *__restrict__ C, int ld, int dim, const float *__restrict__ q, const float *__restrict__ qnorm,
     const float *__restrict__ row_norms, float *__restrict__ out_dist, int64_t *__restrict__ out_row,
     int32_t *__restrict__ fb_mask, int32_t *__restrict__ fb_count) {
   const int qi = blockIdx.x;
   if (qi >= nq) return;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int qp = qi / kBQPass, ql = qi - qp * kBQPass;
+  const int qp = qi / qs, ql = qi - qp * qs;
   extern __shared__ __attribute__((aligned(16))) unsigned char dyn[];
   uint64_t *s_keys = reinterpret_cast<uint64_t *>(dyn);                        // [kGatherCap]
   uint32_t *s_dist = reinterpret_cast<uint32_t *>(dyn + kGatherCap * 8);      // [kGatherCap]
@@ -1052,7 +873,7 @@ __global__ void __launch_bounds__(256) dense_rerank_kernel(
     uint32_t run = 0;
     for (int b0 = 0; b0 < n_wg; b0 += 64) {
       const int b = b0 + lane;
-      uint32_t c = b < n_wg ? cnts[((int64_t)qp * n_wg + b) * kBQPass + ql] : 0u;
+      uint32_t c = b < n_wg ? cnts[((int64_t)qp * n_wg + b) * qs + ql] : 0u;
       if (c > (uint32_t)kCBufCap) {
         s_flag = 1;
         c = kCBufCap;
@@ -1077,7 +898,7 @@ __global__ void __launch_bounds__(256) dense_rerank_kernel(
       fb_mask[qi] = 1;
       atomicAdd(fb_count, 1);
     }
-    return;  // the K1b pass writes this query's results
+    return;  // the exact K1 pass writes this query's results
   }
   // 2. gather the candidates: thread per candidate slot j (its buffer = the last b with
   // s_off[b] <= j; empty buffers share offsets), so every load is independent instead of one
@@ -1089,7 +910,7 @@ __global__ void __launch_bounds__(256) dense_rerank_kernel(
       if (s_off[mid] <= (uint32_t)j) lo = mid;
       else hi = mid - 1;
     }
-    const uint64_t key = keys[(((int64_t)qp * n_wg + lo) * kBQPass + ql) * kCBufCap + (j - s_off[lo])];
+    const uint64_t key = keys[(((int64_t)qp * n_wg + lo) * qs + ql) * kCBufCap + (j - s_off[lo])];
     s_keys[j] = key;
     s_dist[j] = (uint32_t)(key >> 32);
   }
@@ -1210,14 +1031,15 @@ __global__ void __launch_bounds__(256) dense_merge_kernel(const uint64_t *__rest
   }
 }
 
-// Scatter n rows (staging n x dim) into C at rows[i] (or row0+i), set invc + live,
-// and the row's normalised fp16 split planes (K1b): xn = x * invc (hnswlib
-// normalize_vector), Xh = f16(xn), Xl = f16(xn - Xh).
+// Scatter n rows (staging n x dim) into C at rows[i] (or row0+i), set invc + live, and the
+// row's normalised f16 plane (K1c/K1s): xn = x * invc (hnswlib normalize_vector), Xh = f16(xn).
+// The residual xl = xn - Xh is not stored (the exact passes read the fp32 rows); only its
+// norm enters the running maximum of K1c's error bound.
 __global__ void __launch_bounds__(256) dense_scatter_kernel(const float *__restrict__ src, const int64_t *__restrict__ rows,
                                                             int64_t row0, int64_t n, int dim, int ld,
                                                             float *__restrict__ C, float *__restrict__ invc,
                                                             uint32_t *__restrict__ live, _Float16 *__restrict__ Xh,
-                                                            _Float16 *__restrict__ Xl, uint32_t *__restrict__ rnorm) {
+                                                            uint32_t *__restrict__ rnorm) {
   const int64_t i = blockIdx.x;
   if (i >= n) return;
   const int64_t r = rows ? rows[i] : row0 + i;
@@ -1230,6 +1052,7 @@ __global__ void __launch_bounds__(256) dense_scatter_kernel(const float *__restr
     acc += v * v;
   }
   __shared__ float red[4];
+  __shared__ float red2[4];
   for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
   __syncthreads();
@@ -1243,11 +1066,10 @@ __global__ void __launch_bounds__(256) dense_scatter_kernel(const float *__restr
   for (int c = threadIdx.x; c < ld; c += 256) {
     const float xn = (c < dim ? s[c] : 0.f) * inv;
     const _Float16 hi = (_Float16)xn;
-    const _Float16 lo = (_Float16)(xn - (float)hi);
+    const float lo = (float)(_Float16)(xn - (float)hi);
     Xh[plane_off(r, c, ld)] = hi;
-    Xl[plane_off(r, c, ld)] = lo;
     sh += (float)hi * (float)hi;
-    sl += (float)lo * (float)lo;
+    sl += lo * lo;
   }
   // running maxima of ||Xh_r|| and ||Xl_r|| (K1c's error bound; non-negative floats order as
   // their bit patterns); never lowered by deletes, so the bound stays conservative
@@ -1258,9 +1080,8 @@ __global__ void __launch_bounds__(256) dense_scatter_kernel(const float *__restr
   __syncthreads();
   if ((threadIdx.x & 63) == 0) {
     red[threadIdx.x >> 6] = sh;
+    red2[threadIdx.x >> 6] = sl;
   }
-  __shared__ float red2[4];
-  if ((threadIdx.x & 63) == 0) red2[threadIdx.x >> 6] = sl;
   __syncthreads();
   if (threadIdx.x == 0) {
     const float nh = sqrtf((red[0] + red[1]) + (red[2] + red[3]));
@@ -1308,8 +1129,8 @@ struct cm_dense {
   int64_t size = 0;        // high-water row count
   float *C = nullptr;
   float *invc = nullptr;
-  _Float16 *Xh = nullptr, *Xl = nullptr;  // normalised f16 split planes (K1b/K1c)
-  float *rnorm = nullptr;                  // device {max ||Xh_r||, max ||Xl_r||} (K1c bound)
+  _Float16 *Xh = nullptr;                 // normalised f16 plane, fragment-major (K1c/K1s)
+  float *rnorm = nullptr;                  // device {max ||Xh_r||, max ||xn_r - Xh_r||} (K1c bound)
   int path = 0;                            // cm_dense_set_path (0 = automatic)
   int32_t last_fallbacks = -1;             // K1c queries re-run exactly by the last host search
   KernelTimer timer;                       // scan-kernel events (cm_dense_timing)
@@ -1367,7 +1188,7 @@ DenseCfg dense_config(const cm_dense *h, int nq, int k) {
 
 template <int QB, int CH, int KMAX>
 int launch_dense_t(const DenseCfg &c, const cm_dense *h, const uint32_t *allow, const float *qp, const float *invq,
-                   int nq, int k, uint64_t *cand, hipStream_t st) {
+                   int nq, int k, const int32_t *qmask, uint64_t *cand, hipStream_t st) {
   static std::once_flag once;
   static hipError_t attr_err = hipSuccess;
   std::call_once(once, [] {
@@ -1378,15 +1199,17 @@ int launch_dense_t(const DenseCfg &c, const cm_dense *h, const uint32_t *allow, 
   const int64_t n_words = ceil_div(h->size, 32);
   dim3 grid(c.n_cblocks * c.n_qgroups);
   hipLaunchKernelGGL((dense_topk_kernel<QB, CH, KMAX>), grid, dim3(kThreads), c.lds, st, h->C, h->ld, h->invc,
-                     h->live, allow, n_words, qp, invq, nq, k, c.rows_per_block, c.rows_end, c.n_cblocks, cand);
+                     h->live, allow, n_words, qp, invq, nq, k, c.rows_per_block, c.rows_end, c.n_cblocks, qmask,
+                     cand);
   CM_HIP(hipGetLastError());
   return CM_OK;
 }
 
 int launch_dense(const DenseCfg &c, const cm_dense *h, const uint32_t *allow, const float *qp, const float *invq,
-                 int nq, int k, uint64_t *cand, hipStream_t st) {
+                 int nq, int k, const int32_t *qmask, uint64_t *cand, hipStream_t st) {
 #define CM_DENSE_CASE(QB_, CH_, KM_) \
-  if (c.QB == QB_ && c.CH == CH_ && c.KMAX == KM_) return launch_dense_t<QB_, CH_, KM_>(c, h, allow, qp, invq, nq, k, cand, st);
+  if (c.QB == QB_ && c.CH == CH_ && c.KMAX == KM_)   \
+    return launch_dense_t<QB_, CH_, KM_>(c, h, allow, qp, invq, nq, k, qmask, cand, st);
   CM_DENSE_CASE(16, 12, 64)
   CM_DENSE_CASE(32, 12, 64)
   CM_DENSE_CASE(16, 12, 256)
@@ -1426,12 +1249,11 @@ int dense_grow(cm_dense *h, int64_t need_rows) {
   cap = round_up(std::max<int64_t>(cap, kStepRows), kStepRows);
   float *C2 = nullptr, *ic2 = nullptr;
   uint32_t *lv2 = nullptr;
-  _Float16 *xh2 = nullptr, *xl2 = nullptr;
+  _Float16 *xh2 = nullptr;
   const size_t nel = (size_t)cap * h->ld;
   if (hipMalloc(&C2, nel * 4) != hipSuccess || hipMalloc(&ic2, (size_t)cap * 4) != hipSuccess ||
-      hipMalloc(&lv2, (size_t)cap / 8) != hipSuccess || hipMalloc(&xh2, nel * 2) != hipSuccess ||
-      hipMalloc(&xl2, nel * 2) != hipSuccess) {
-    for (void *p : {(void *)C2, (void *)ic2, (void *)lv2, (void *)xh2, (void *)xl2})
+      hipMalloc(&lv2, (size_t)cap / 8) != hipSuccess || hipMalloc(&xh2, nel * 2) != hipSuccess) {
+    for (void *p : {(void *)C2, (void *)ic2, (void *)lv2, (void *)xh2})
       if (p) (void)hipFree(p);
     CM_FAIL(CM_ENOMEM, "dense: out of device memory");
   }
@@ -1439,31 +1261,25 @@ int dense_grow(cm_dense *h, int64_t need_rows) {
   CM_HIP(hipMemsetAsync(ic2, 0, (size_t)cap * 4, h->stream));
   CM_HIP(hipMemsetAsync(lv2, 0, (size_t)cap / 8, h->stream));
   CM_HIP(hipMemsetAsync(xh2, 0, nel * 2, h->stream));
-  CM_HIP(hipMemsetAsync(xl2, 0, nel * 2, h->stream));
   if (h->rows_alloc) {
+    // the plane is tile-major (64-row tiles, rows_alloc a multiple of 128): a prefix copy keeps it
     const size_t old = (size_t)h->rows_alloc * h->ld;
     CM_HIP(hipMemcpyAsync(C2, h->C, old * 4, hipMemcpyDeviceToDevice, h->stream));
     CM_HIP(hipMemcpyAsync(ic2, h->invc, (size_t)h->rows_alloc * 4, hipMemcpyDeviceToDevice, h->stream));
     CM_HIP(hipMemcpyAsync(lv2, h->live, (size_t)h->rows_alloc / 8, hipMemcpyDeviceToDevice, h->stream));
     CM_HIP(hipMemcpyAsync(xh2, h->Xh, old * 2, hipMemcpyDeviceToDevice, h->stream));
-    CM_HIP(hipMemcpyAsync(xl2, h->Xl, old * 2, hipMemcpyDeviceToDevice, h->stream));
   }
   CM_HIP(hipStreamSynchronize(h->stream));
-  for (void *p : {(void *)h->C, (void *)h->invc, (void *)h->live, (void *)h->Xh, (void *)h->Xl})
+  for (void *p : {(void *)h->C, (void *)h->invc, (void *)h->live, (void *)h->Xh})
     if (p) (void)hipFree(p);
   h->C = C2;
   h->invc = ic2;
   h->live = lv2;
   h->Xh = xh2;
-  h->Xl = xl2;
   h->rows_alloc = cap;
   return CM_OK;
 }
 
-// CM_DENSE_DEBUG (ablation only) for the scan kernels: bit0 skip the top-k epilogue, bit4 filter
-// without inserting survivors, bit5 (K1c) no sample pre-pass, bit6 (K1c) no MFMAs, bit7 (K1c) no
-// per-tile epilogue, bit9 no chunk barrier, bit10 no DMA issue, bit11 no fragment reads (K1c
-// timing ablations only: results are garbage under bits 9-11).
 // Timing ablations are compiled only into -DCM_ABLATION builds (tools/build_variant.sh); the
 // product library ignores CM_DENSE_DEBUG, so no bench line can come from a disabled kernel.
 #ifdef CM_ABLATION
@@ -1478,184 +1294,185 @@ int dense_debug_flags() {
 int dense_debug_flags() { return 0; }
 #endif
 
-// Scan kernel for (nq, k): K1c (coarse f16 + certified re-rank) whenever its list length fits,
-// K1b (f16x3) for other batched k <= 32, K1 (fp32) otherwise.  CM_DENSE_PATH=f32|f16x3|coarse
-// forces a path (A/B probes; an ineligible forced path falls back to the default rule).
+// Scan kernel for (nq, k), the "search kind":
+//   CM_DENSE_STREAM (K1s)  nq <= kSQ queries: per-wave HBM streams of the f16 plane + re-rank;
+//   CM_DENSE_COARSE (K1c)  larger batches: 256-query resident passes + re-rank;
+//   CM_DENSE_F32   (K1)    exact fp32 scan: k > 32, dims other than 384 / 768, corpora under
+//                          16384 rows (and the certificate's fallback).
+// CM_DENSE_PATH=f32|coarse|stream (or cm_dense_set_path) forces a kind for A/B probes; an
+// ineligible forced kind falls back to the automatic rule.  The retired K1b (f16x3 split planes,
+// kind 2) maps to the automatic rule.
 int dense_kind(const cm_dense *h, int nq, int k) {
   static const int env_force = [] {
     const char *e = getenv("CM_DENSE_PATH");
     if (!e) return 0;
     const std::string s(e);
-    return s == "f32" ? CM_DENSE_F32 : s == "f16x3" ? CM_DENSE_F16X3 : s == "coarse" ? CM_DENSE_COARSE : 0;
+    return s == "f32" ? CM_DENSE_F32 : s == "coarse" ? CM_DENSE_COARSE : s == "stream" ? CM_DENSE_STREAM : 0;
   }();
   const int force = h->path ? h->path : env_force;
-  // K1c: resident-query scan instances (ld 768 / 384), a sample of >= 1024 rows for the seed
+  // coarse scans: resident-query instances for ld 768 / 384, a sample of >= 1024 rows for the seed
   const bool coarse_ok = k <= kBMaxK && (h->ld == 768 || h->ld == 384) && h->size >= 16384;
-  const bool split_ok = k <= kBMaxK && h->ld % 128 == 0;
-  if (force == CM_DENSE_F32) return CM_DENSE_F32;
-  if (force == CM_DENSE_F16X3 && split_ok) return CM_DENSE_F16X3;
-  if (force == CM_DENSE_COARSE && coarse_ok) return CM_DENSE_COARSE;
-  if (coarse_ok) return CM_DENSE_COARSE;
-  if (split_ok && nq >= 64) return CM_DENSE_F16X3;
-  return CM_DENSE_F32;
+  if (force == CM_DENSE_F32 || !coarse_ok) return CM_DENSE_F32;
+  if (force == CM_DENSE_COARSE) return CM_DENSE_COARSE;
+  if (force == CM_DENSE_STREAM && nq <= kSQ) return CM_DENSE_STREAM;
+  return nq <= kSQ ? CM_DENSE_STREAM : CM_DENSE_COARSE;
 }
 
-struct K1bCfg {
-  int n_wg, n_pass;
-  int64_t rows_per_wg, rows_end;
+// Coarse-scan geometry.  K1c: a pass of kBQPass queries per workgroup, one workgroup per CU and
+// pass; K1s: one pass of kSQ queries, n_wg = "virtual groups" = waves (4 per CU).  The sample
+// pre-pass runs the same kernel over a prefix of 1/64 of the rows (1/16 below 1M rows).
+struct CoarseCfg {
+  bool stream;
+  int qs, n_pass, n_wg, n_wg_sample;
+  int64_t rows_per_wg, rows_end, rows_per_wg_sample, rows_end_sample;
 };
-K1bCfg k1b_config(const cm_dense *h, int nq) {
-  K1bCfg c{};
-  c.n_pass = (int)ceil_div(nq, kBQPass);
-  c.rows_end = round_up(std::max<int64_t>(h->size, 1), kBRows);
-  const int64_t tiles = c.rows_end / kBRows;
-  const int64_t want = std::max(1, num_cus(h->dev) / c.n_pass);
-  const int64_t per = ceil_div(tiles, std::min<int64_t>(want, tiles));
-  c.rows_per_wg = per * kBRows;
-  c.n_wg = (int)ceil_div(tiles, per);
+CoarseCfg coarse_config(const cm_dense *h, int nq, bool stream) {
+  CoarseCfg c{};
+  c.stream = stream;
+  c.qs = stream ? kSQ : kBQPass;
+  c.n_pass = stream ? 1 : (int)ceil_div(nq, kBQPass);
+  c.rows_end = round_up(std::max<int64_t>(h->size, 1), kStepRows);
+  const int64_t groups = stream ? (int64_t)num_cus(h->dev) * 4 : std::max(1, num_cus(h->dev) / c.n_pass);
+  auto split = [&](int64_t rows_end, int64_t &per, int &n) {
+    const int64_t tiles = rows_end / kRRows;
+    per = ceil_div(tiles, std::min<int64_t>(groups, tiles)) * kRRows;
+    n = (int)ceil_div(rows_end, per);
+  };
+  split(c.rows_end, c.rows_per_wg, c.n_wg);
+  const int64_t frac = c.rows_end >= (1 << 20) ? 64 : 16;
+  c.rows_end_sample = round_up(std::max<int64_t>(c.rows_end / frac, 1), kRRows);
+  split(c.rows_end_sample, c.rows_per_wg_sample, c.n_wg_sample);
   return c;
 }
 
-// K1c sample pre-pass geometry: a prefix of 1/64 of the rows (1/16 below 1M rows) in 64-row
-// groups, one group range per workgroup, as many workgroups per pass as the main scan.
-struct K1cSample {
-  int n_wg;
-  int64_t rows_per_wg, rows_end;
-};
-K1cSample k1c_sample(const cm_dense *h, const K1bCfg &c) {
-  K1cSample s{};
-  const int64_t frac = c.rows_end >= (1 << 20) ? 64 : 16;
-  s.rows_end = round_up(std::max<int64_t>(c.rows_end / frac, 1), kRRows);
-  const int64_t tiles = s.rows_end / kRRows;
-  const int64_t want = std::max(1, num_cus(h->dev) / c.n_pass);
-  const int64_t per = ceil_div(tiles, std::min<int64_t>(want, tiles));
-  s.rows_per_wg = per * kRRows;
-  s.n_wg = (int)ceil_div(tiles, per);
-  return s;
-}
-
-struct K1bWs {
-  _Float16 *qh, *ql;
-  float *qnorm;
-  uint64_t *cand;     // K1b lists (k per range) -- K1c: fallback pass
-  uint64_t *keys;     // K1c candidate buffers [pass][range][query][kCBufCap]
-  uint32_t *cnt;      // K1c buffer fill counts [pass][range][query]
-  float *mins;        // K1c sample minima [pass][sample range][query]
-  float *seed;        // K1c per-query insertion bound from the sample
-  int32_t *fb_mask;   // K1c: queries sent to the fallback pass
+struct CoarseWs {
+  _Float16 *qh;       // [nq_pad][ld] normalised f16 queries
+  float *qnorm;       // [nq_pad][4]
+  uint64_t *keys;     // candidate buffers [pass][group][qs][kCBufCap]
+  uint32_t *cnt;      // buffer fill counts [pass][group][qs]
+  float *mins;        // sample minima [pass][sample group][qs]
+  float *seed;        // per-query insertion bound from the sample
+  int32_t *fb_mask;   // queries sent to the exact K1 pass
   int32_t *fb_count;
+  DenseWs k1;         // the exact K1 pass's own workspace (used only for fb_mask queries)
   size_t total;
 };
-K1bWs k1b_ws_layout(const cm_dense *h, const K1bCfg &c, int k, bool coarse, void *base) {
-  K1bWs w{};
+CoarseWs coarse_ws_layout(const cm_dense *h, const CoarseCfg &c, int nq, int k, void *base) {
+  CoarseWs w{};
   char *p = reinterpret_cast<char *>(base);
   size_t off = 0;
-  const int64_t nq_pad = (int64_t)c.n_pass * kBQPass;
+  const int64_t nq_pad = (int64_t)c.n_pass * c.qs;
   auto take = [&](int64_t bytes) -> char * {
     char *r = p + off;
     off += round_up(std::max<int64_t>(bytes, 1), 256);
     return r;
   };
   w.qh = reinterpret_cast<_Float16 *>(take(nq_pad * h->ld * 2));
-  w.ql = reinterpret_cast<_Float16 *>(take(nq_pad * h->ld * 2));
   w.qnorm = reinterpret_cast<float *>(take(nq_pad * 16));
-  w.cand = reinterpret_cast<uint64_t *>(take((int64_t)c.n_pass * c.n_wg * kBQPass * k * 8));
-  if (coarse) {
-    w.keys = reinterpret_cast<uint64_t *>(take((int64_t)c.n_pass * c.n_wg * kBQPass * kCBufCap * 8));
-    w.cnt = reinterpret_cast<uint32_t *>(take((int64_t)c.n_pass * c.n_wg * kBQPass * 4));
-    const K1cSample sm = k1c_sample(h, c);
-    w.mins = reinterpret_cast<float *>(take((int64_t)c.n_pass * sm.n_wg * kBQPass * 4));
-    w.seed = reinterpret_cast<float *>(take(nq_pad * 4));
-    w.fb_mask = reinterpret_cast<int32_t *>(take(nq_pad * 4));
-    w.fb_count = reinterpret_cast<int32_t *>(take(4));
-  }
+  w.keys = reinterpret_cast<uint64_t *>(take((int64_t)c.n_pass * c.n_wg * c.qs * kCBufCap * 8));
+  w.cnt = reinterpret_cast<uint32_t *>(take((int64_t)c.n_pass * c.n_wg * c.qs * 4));
+  w.mins = reinterpret_cast<float *>(take((int64_t)c.n_pass * c.n_wg_sample * c.qs * 4));
+  w.seed = reinterpret_cast<float *>(take(nq_pad * 4));
+  w.fb_mask = reinterpret_cast<int32_t *>(take(nq_pad * 4));
+  w.fb_count = reinterpret_cast<int32_t *>(take(4));
+  const DenseCfg kc = dense_config(h, nq, k);
+  w.k1 = dense_ws_layout(h, kc, nq, k, p ? p + off : nullptr);
+  off += w.k1.total;
   w.total = off;
   return w;
 }
 
-template <int NPL>
-int set_split_lds() {
+int set_coarse_attrs() {
   static std::once_flag once;
   static hipError_t err = hipSuccess;
   std::call_once(once, [] {
-    err = hipFuncSetAttribute(reinterpret_cast<const void *>(&dense_split_kernel<NPL>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, k1b_lds_layout().total);
+    const std::pair<const void *, int> fs[] = {
+        {reinterpret_cast<const void *>(&dense_coarse_scan_kernel<12, 3, false, kK1cWaves>), K1rLds<3>::total},
+        {reinterpret_cast<const void *>(&dense_coarse_scan_kernel<12, 3, true, kK1cWaves>), K1rLds<3>::total},
+        {reinterpret_cast<const void *>(&dense_coarse_scan_kernel<6, 0, false, kK1cWaves>), K1rLds<0>::total},
+        {reinterpret_cast<const void *>(&dense_coarse_scan_kernel<6, 0, true, kK1cWaves>), K1rLds<0>::total},
+        {reinterpret_cast<const void *>(&dense_rerank_kernel), kGatherCap * 12}};
+    for (const auto &f : fs) {
+      const hipError_t e = hipFuncSetAttribute(f.first, hipFuncAttributeMaxDynamicSharedMemorySize, f.second);
+      if (e != hipSuccess) err = e;
+    }
   });
   CM_HIP(err);
   return CM_OK;
 }
 
-// K1b: f16x3 scan of every query + tournament merge.  K1c: coarse scan -> certification and
-// exact re-rank -> f16x3 pass restricted to the queries the certificate rejected (its
-// workgroups exit at once when there are none) -> merge of those queries only.
-int launch_split(cm_dense *h, const float *q_dev, int nq, int k, bool coarse, const uint32_t *allow,
-                 float *dist_dev, int64_t *row_dev, void *ws, int64_t ws_bytes, hipStream_t st) {
+using StreamFn = void (*)(const _Float16 *, const uint32_t *, const uint32_t *, int64_t, const _Float16 *, int,
+                          const float *, int64_t, int64_t, int, int, uint64_t *, uint32_t *, float *);
+StreamFn stream_kernel(int ld, int nq, bool minonly) {
+  const bool two = nq > 16;
+  if (ld == 768)
+    return two ? (minonly ? &dense_stream_scan_kernel<12, 2, true> : &dense_stream_scan_kernel<12, 2, false>)
+               : (minonly ? &dense_stream_scan_kernel<12, 1, true> : &dense_stream_scan_kernel<12, 1, false>);
+  return two ? (minonly ? &dense_stream_scan_kernel<6, 2, true> : &dense_stream_scan_kernel<6, 2, false>)
+             : (minonly ? &dense_stream_scan_kernel<6, 1, true> : &dense_stream_scan_kernel<6, 1, false>);
+}
+
+// K1c / K1s: sample pre-pass -> seed -> coarse scan -> certificate + exact re-rank; the queries
+// whose certificate fails (fb_mask) are re-searched by the exact fp32 K1 and merged (every
+// workgroup of those launches exits at once when there are none: graph-capturable, no host sync).
+int launch_coarse(cm_dense *h, const float *q_dev, int nq, int k, bool stream, const uint32_t *allow,
+                  float *dist_dev, int64_t *row_dev, void *ws, int64_t ws_bytes, hipStream_t st) {
   int rc;
-  if ((rc = set_split_lds<2>())) return rc;
-  if (coarse) {
-    static std::once_flag once;
-    static hipError_t err = hipSuccess;
-    std::call_once(once, [] {
-      const std::pair<const void *, int> fs[] = {
-          {reinterpret_cast<const void *>(&dense_coarse_scan_kernel<12, 3, false, kK1cWaves>), K1rLds<3>::total},
-          {reinterpret_cast<const void *>(&dense_coarse_scan_kernel<12, 3, true, kK1cWaves>), K1rLds<3>::total},
-          {reinterpret_cast<const void *>(&dense_coarse_scan_kernel<6, 0, false, kK1cWaves>), K1rLds<0>::total},
-          {reinterpret_cast<const void *>(&dense_coarse_scan_kernel<6, 0, true, kK1cWaves>), K1rLds<0>::total},
-          {reinterpret_cast<const void *>(&dense_rerank_kernel), kGatherCap * 12}};
-      for (const auto &f : fs) {
-        const hipError_t e = hipFuncSetAttribute(f.first, hipFuncAttributeMaxDynamicSharedMemorySize, f.second);
-        if (e != hipSuccess) err = e;
-      }
-    });
-    CM_HIP(err);
-  }
-  const K1bCfg c = k1b_config(h, nq);
-  const K1bWs w = k1b_ws_layout(h, c, k, coarse, ws);
+  if ((rc = set_coarse_attrs())) return rc;
+  const CoarseCfg c = coarse_config(h, nq, stream);
+  const CoarseWs w = coarse_ws_layout(h, c, nq, k, ws);
   if ((int64_t)w.total > ws_bytes || !ws) CM_FAIL(CM_EINVAL, "dense workspace too small");
-  const size_t lds = k1b_lds_layout().total;
   const int64_t n_words = ceil_div(h->size, 32);
-  const dim3 grid(c.n_wg * c.n_pass);
-  hipLaunchKernelGGL(dense_prep_planes, dim3(c.n_pass * kBQPass), dim3(256), 0, st, q_dev, nq, h->dim, h->ld, w.qh,
-                     w.ql, w.qnorm);
+  hipLaunchKernelGGL(dense_prep_planes, dim3(c.n_pass * c.qs), dim3(256), 0, st, q_dev, nq, h->dim, h->ld, w.qh,
+                     w.qnorm);
   CM_HIP(hipGetLastError());
-  const int32_t *mask = nullptr;
-  if (coarse) {
-    CM_HIP(hipMemsetAsync(w.fb_count, 0, 4, st));
-    const K1cSample sm = k1c_sample(h, c);
-    const bool d768 = h->ld == 768;
-    auto scan = [&](bool minonly) {
-      if (d768) return minonly ? &dense_coarse_scan_kernel<12, 3, true, kK1cWaves> : &dense_coarse_scan_kernel<12, 3, false, kK1cWaves>;
-      return minonly ? &dense_coarse_scan_kernel<6, 0, true, kK1cWaves> : &dense_coarse_scan_kernel<6, 0, false, kK1cWaves>;
-    };
-    const size_t slds = d768 ? K1rLds<3>::total : K1rLds<0>::total;
-    // 1. sample pre-pass (per-group minima) -> seed
-    hipLaunchKernelGGL(scan(true), dim3(sm.n_wg * c.n_pass), dim3(64 * kK1cWaves), slds, st, h->Xh, h->live, allow, n_words,
-                       w.qh, nq, (const float *)nullptr, sm.rows_per_wg, sm.rows_end, sm.n_wg, (uint64_t *)nullptr,
-                       (uint32_t *)nullptr, w.mins, 0);
-    CM_HIP(hipGetLastError());
-    hipLaunchKernelGGL(dense_seed_kernel, dim3(nq), dim3(256), 0, st, w.mins, sm.n_wg, k, nq, w.qnorm, h->rnorm,
-                       h->dim, w.seed);
-    CM_HIP(hipGetLastError());
-    // 2. coarse scan: rows under the seed -> candidate buffers
-    h->timer.begin(st);
-    hipLaunchKernelGGL(scan(false), grid, dim3(64 * kK1cWaves), slds, st, h->Xh, h->live, allow, n_words, w.qh, nq,
-                       (const float *)w.seed, c.rows_per_wg, c.rows_end, c.n_wg, w.keys, w.cnt, (float *)nullptr,
-                       dense_debug_flags());
-    h->timer.end(st);
-    CM_HIP(hipGetLastError());
-    // 3. certificate + exact re-rank (failures -> fb_mask)
-    hipLaunchKernelGGL(dense_rerank_kernel, dim3(nq), dim3(256), kGatherCap * 12, st, w.keys, w.cnt, c.n_wg, k, nq,
-                       h->C, h->ld, h->dim, q_dev, w.qnorm, h->rnorm, dist_dev, row_dev, w.fb_mask, w.fb_count);
-    CM_HIP(hipGetLastError());
-    mask = w.fb_mask;
+  CM_HIP(hipMemsetAsync(w.fb_count, 0, 4, st));
+  const bool d768 = h->ld == 768;
+  const size_t slds = d768 ? K1rLds<3>::total : K1rLds<0>::total;
+  auto k1c = [&](bool minonly) {
+    if (d768) return minonly ? &dense_coarse_scan_kernel<12, 3, true, kK1cWaves> : &dense_coarse_scan_kernel<12, 3, false, kK1cWaves>;
+    return minonly ? &dense_coarse_scan_kernel<6, 0, true, kK1cWaves> : &dense_coarse_scan_kernel<6, 0, false, kK1cWaves>;
+  };
+  // 1. sample pre-pass (per-group minima) -> seed
+  if (stream) {
+    hipLaunchKernelGGL(stream_kernel(h->ld, nq, true), dim3((unsigned)ceil_div(c.n_wg_sample, 4)), dim3(256), 0, st,
+                       h->Xh, h->live, allow, n_words, w.qh, nq, (const float *)nullptr, c.rows_per_wg_sample,
+                       c.rows_end_sample, c.n_wg_sample, c.qs, (uint64_t *)nullptr, (uint32_t *)nullptr, w.mins);
+  } else {
+    hipLaunchKernelGGL(k1c(true), dim3(c.n_wg_sample * c.n_pass), dim3(64 * kK1cWaves), slds, st, h->Xh, h->live,
+                       allow, n_words, w.qh, nq, (const float *)nullptr, c.rows_per_wg_sample, c.rows_end_sample,
+                       c.n_wg_sample, (uint64_t *)nullptr, (uint32_t *)nullptr, w.mins, 0);
   }
-  if (!coarse) h->timer.begin(st);
-  hipLaunchKernelGGL(dense_split_kernel<2>, grid, dim3(512), lds, st, h->Xh, h->Xl, h->ld, h->live, allow, n_words,
-                     w.qh, w.ql, nq, mask, k, c.rows_per_wg, c.rows_end, c.n_wg, w.cand, dense_debug_flags());
-  if (!coarse) h->timer.end(st);
   CM_HIP(hipGetLastError());
-  hipLaunchKernelGGL(dense_merge_kernel, dim3(nq), dim3(256), 0, st, w.cand, c.n_wg, kBQPass, k, nq, mask, dist_dev,
-                     row_dev);
+  hipLaunchKernelGGL(dense_seed_kernel, dim3(nq), dim3(256), 0, st, w.mins, c.n_wg_sample, c.qs, k, nq, w.qnorm,
+                     h->rnorm, h->dim, w.seed);
+  CM_HIP(hipGetLastError());
+  // 2. coarse scan: rows under the seed -> candidate buffers
+  h->timer.begin(st);
+  if (stream) {
+    hipLaunchKernelGGL(stream_kernel(h->ld, nq, false), dim3((unsigned)ceil_div(c.n_wg, 4)), dim3(256), 0, st, h->Xh,
+                       h->live, allow, n_words, w.qh, nq, (const float *)w.seed, c.rows_per_wg, c.rows_end, c.n_wg,
+                       c.qs, w.keys, w.cnt, (float *)nullptr);
+  } else {
+    hipLaunchKernelGGL(k1c(false), dim3(c.n_wg * c.n_pass), dim3(64 * kK1cWaves), slds, st, h->Xh, h->live, allow,
+                       n_words, w.qh, nq, (const float *)w.seed, c.rows_per_wg, c.rows_end, c.n_wg, w.keys, w.cnt,
+                       (float *)nullptr, dense_debug_flags());
+  }
+  h->timer.end(st);
+  CM_HIP(hipGetLastError());
+  // 3. certificate + exact re-rank (failures -> fb_mask)
+  hipLaunchKernelGGL(dense_rerank_kernel, dim3(nq), dim3(256), kGatherCap * 12, st, w.keys, w.cnt, c.n_wg, c.qs, k,
+                     nq, h->C, h->ld, h->dim, q_dev, w.qnorm, h->rnorm, dist_dev, row_dev, w.fb_mask, w.fb_count);
+  CM_HIP(hipGetLastError());
+  // 4. exact fp32 K1 for the rejected queries only, merged into their rows of the output
+  const DenseCfg kc = dense_config(h, nq, k);
+  if (kc.lds > 163840) CM_FAIL(CM_EUNSUPPORTED, "dim/k too large for the LDS-resident query tile");
+  hipLaunchKernelGGL(dense_prep_queries, dim3(kc.n_qgroups * kc.QB), dim3(256), 0, st, q_dev, nq, h->dim, h->ld,
+                     w.k1.qp, w.k1.invq);
+  CM_HIP(hipGetLastError());
+  if ((rc = launch_dense(kc, h, allow, w.k1.qp, w.k1.invq, nq, k, w.fb_mask, w.k1.cand, st))) return rc;
+  hipLaunchKernelGGL(dense_merge_kernel, dim3(nq), dim3(256), 0, st, w.k1.cand, kc.n_cblocks, kc.QB, k, nq,
+                     (const int32_t *)w.fb_mask, dist_dev, row_dev);
   CM_HIP(hipGetLastError());
   return CM_OK;
 }
@@ -1704,7 +1521,6 @@ void cm_dense_destroy(cm_dense *h) {
   if (h->invc) (void)hipFree(h->invc);
   if (h->live) (void)hipFree(h->live);
   if (h->Xh) (void)hipFree(h->Xh);
-  if (h->Xl) (void)hipFree(h->Xl);
   if (h->rnorm) (void)hipFree(h->rnorm);
   h->timer.release();
   h->staging.release();
@@ -1743,7 +1559,7 @@ int cm_dense_upsert(cm_dense *h, const float *vecs, const int64_t *rows, int64_t
     CM_HIP(hipMemcpyAsync(h->staging.ptr, vecs + s * h->dim, (size_t)m * h->dim * 4, hipMemcpyHostToDevice, h->stream));
     CM_HIP(hipMemcpyAsync(h->rows_buf.ptr, rows + s, (size_t)m * 8, hipMemcpyHostToDevice, h->stream));
     hipLaunchKernelGGL(dense_scatter_kernel, dim3((unsigned)m), dim3(256), 0, h->stream, h->staging.as<float>(),
-                       h->rows_buf.as<int64_t>(), (int64_t)0, m, h->dim, h->ld, h->C, h->invc, h->live, h->Xh, h->Xl,
+                       h->rows_buf.as<int64_t>(), (int64_t)0, m, h->dim, h->ld, h->C, h->invc, h->live, h->Xh,
                        reinterpret_cast<uint32_t *>(h->rnorm));
     CM_HIP(hipGetLastError());
     CM_HIP(hipStreamSynchronize(h->stream));
@@ -1768,7 +1584,7 @@ int cm_dense_upsert_dev(cm_dense *h, const float *vecs_dev, int64_t row0, int64_
     const int64_t m = std::min(batch, n - s);
     hipLaunchKernelGGL(dense_scatter_kernel, dim3((unsigned)m), dim3(256), 0, st, vecs_dev + s * h->dim,
                        (const int64_t *)nullptr, row0 + s, m, h->dim, h->ld, h->C, h->invc, h->live, h->Xh,
-                       h->Xl, reinterpret_cast<uint32_t *>(h->rnorm));
+                       reinterpret_cast<uint32_t *>(h->rnorm));
     CM_HIP(hipGetLastError());
   }
   h->size = std::max(h->size, row0 + n);
@@ -1797,7 +1613,6 @@ int cm_dense_reset(cm_dense *h) {
   CM_HIP(hipMemsetAsync(h->invc, 0, (size_t)h->rows_alloc * 4, h->stream));
   CM_HIP(hipMemsetAsync(h->C, 0, (size_t)h->rows_alloc * h->ld * 4, h->stream));
   CM_HIP(hipMemsetAsync(h->Xh, 0, (size_t)h->rows_alloc * h->ld * 2, h->stream));
-  CM_HIP(hipMemsetAsync(h->Xl, 0, (size_t)h->rows_alloc * h->ld * 2, h->stream));
   CM_HIP(hipMemsetAsync(h->rnorm, 0, 8, h->stream));
   CM_HIP(hipStreamSynchronize(h->stream));
   h->size = 0;
@@ -1826,23 +1641,26 @@ int64_t cm_dense_live_count(cm_dense *h) {
 int64_t cm_dense_search_workspace(cm_dense *h, int32_t nq, int32_t k) {
   if (!h || nq <= 0 || k <= 0 || k > kMaxTopK) return -1;
   const int kind = dense_kind(h, nq, k);
-  if (kind != CM_DENSE_F32) return (int64_t)k1b_ws_layout(h, k1b_config(h, nq), k, kind == CM_DENSE_COARSE, nullptr).total;
+  if (kind != CM_DENSE_F32)
+    return (int64_t)coarse_ws_layout(h, coarse_config(h, nq, kind == CM_DENSE_STREAM), nq, k, nullptr).total;
   DenseCfg c = dense_config(h, nq, k);
   return (int64_t)dense_ws_layout(h, c, nq, k, nullptr).total;
 }
 
 int cm_dense_set_path(cm_dense *h, int32_t kind) {
   if (!h) CM_FAIL(CM_EINVAL, "null handle");
-  if (kind < 0 || kind > CM_DENSE_COARSE) CM_FAIL(CM_EINVAL, "unknown dense path");
+  if (kind < 0 || kind > CM_DENSE_STREAM) CM_FAIL(CM_EINVAL, "unknown dense path");
   h->path = kind;
   return CM_OK;
 }
 
 int32_t cm_dense_workspace_fallbacks(cm_dense *h, int32_t nq, int32_t k, const void *workspace_dev) {
   if (!h || !workspace_dev || nq <= 0 || k <= 0 || k > kMaxTopK) return -1;
-  if (dense_kind(h, nq, k) != CM_DENSE_COARSE) return 0;
+  const int kind = dense_kind(h, nq, k);
+  if (kind == CM_DENSE_F32) return 0;
   DeviceGuard dg(h->dev);
-  const K1bWs w = k1b_ws_layout(h, k1b_config(h, nq), k, true, const_cast<void *>(workspace_dev));
+  const CoarseWs w = coarse_ws_layout(h, coarse_config(h, nq, kind == CM_DENSE_STREAM), nq, k,
+                                      const_cast<void *>(workspace_dev));
   int32_t c = -1;
   if (hipMemcpy(&c, w.fb_count, 4, hipMemcpyDeviceToHost) != hipSuccess) return -1;
   return c;
@@ -1881,8 +1699,8 @@ int cm_dense_search_dev(cm_dense *h, const float *q_dev, int32_t nq, int32_t k, 
   hipStream_t st = (hipStream_t)stream;  // NULL = the null stream (torch default)
   const int kind = dense_kind(h, nq, k);
   if (kind != CM_DENSE_F32)
-    return launch_split(h, q_dev, nq, k, kind == CM_DENSE_COARSE, allow_dev, dist_dev, row_dev, workspace_dev,
-                        workspace_bytes, st);
+    return launch_coarse(h, q_dev, nq, k, kind == CM_DENSE_STREAM, allow_dev, dist_dev, row_dev, workspace_dev,
+                         workspace_bytes, st);
   DenseCfg c = dense_config(h, nq, k);
   if (c.lds > 163840) CM_FAIL(CM_EUNSUPPORTED, "dim/k too large for the LDS-resident query tile");
   DenseWs w = dense_ws_layout(h, c, nq, k, workspace_dev);
@@ -1891,7 +1709,7 @@ int cm_dense_search_dev(cm_dense *h, const float *q_dev, int32_t nq, int32_t k, 
   hipLaunchKernelGGL(dense_prep_queries, dim3(nq_pad), dim3(256), 0, st, q_dev, nq, h->dim, h->ld, w.qp, w.invq);
   CM_HIP(hipGetLastError());
   h->timer.begin(st);
-  int rc = launch_dense(c, h, allow_dev, w.qp, w.invq, nq, k, w.cand, st);
+  int rc = launch_dense(c, h, allow_dev, w.qp, w.invq, nq, k, (const int32_t *)nullptr, w.cand, st);
   h->timer.end(st);
   if (rc) return rc;
   hipLaunchKernelGGL(dense_merge_kernel, dim3(nq), dim3(256), 0, st, w.cand, c.n_cblocks, c.QB, k, nq,
@@ -1971,8 +1789,9 @@ int cm_dense_search(cm_dense *h, const float *q, int32_t nq, int32_t k, const ui
   CM_HIP(hipMemcpyAsync(out_row, d_row, (size_t)nq * k * 8, hipMemcpyDeviceToHost, h->stream));
   if (out_vec) CM_HIP(hipMemcpyAsync(out_vec, d_vec, vbytes, hipMemcpyDeviceToHost, h->stream));
   h->last_fallbacks = 0;
-  if (dense_kind(h, nq, k) == CM_DENSE_COARSE) {
-    const K1bWs w = k1b_ws_layout(h, k1b_config(h, nq), k, true, h->ws.ptr);
+  const int kind = dense_kind(h, nq, k);
+  if (kind != CM_DENSE_F32) {
+    const CoarseWs w = coarse_ws_layout(h, coarse_config(h, nq, kind == CM_DENSE_STREAM), nq, k, h->ws.ptr);
     CM_HIP(hipMemcpyAsync(&h->last_fallbacks, w.fb_count, 4, hipMemcpyDeviceToHost, h->stream));
   }
   CM_HIP(hipStreamSynchronize(h->stream));

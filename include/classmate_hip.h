@@ -88,26 +88,29 @@ int cm_dense_search(cm_dense *h, const float *q, int32_t nq, int32_t k, const ui
 /* workspace bytes cm_dense_search_dev needs for (nq, k). */
 int64_t cm_dense_search_workspace(cm_dense *h, int32_t nq, int32_t k);
 /* which scan kernel cm_dense_search[_dev] runs for (nq, k): CM_DENSE_F32
- * (K1, fp32 MFMA, reads 4 B/element), CM_DENSE_F16X3 (K1b, split-f16
- * planes, 4 B/element), CM_DENSE_COARSE (K1c, f16 hi plane, 2 B/element,
- * certified exact re-rank); -1 on error.  Lets callers price the launch
- * against the right roofline.                                            */
+ * (K1, fp32 MFMA, reads 4 B/element: k > 32, other dims, small corpora),
+ * CM_DENSE_COARSE (K1c, f16 plane, 2 B/element, 256-query resident passes,
+ * certified exact re-rank), CM_DENSE_STREAM (K1s, f16 plane, 2 B/element,
+ * nq <= 32, per-wave HBM streams, same re-rank); -1 on error.  Lets callers
+ * price the launch against the right roofline.  CM_DENSE_F16X3 (the retired
+ * split-plane K1b) is accepted by cm_dense_set_path and means automatic.  */
 #define CM_DENSE_F32 1
 #define CM_DENSE_F16X3 2
 #define CM_DENSE_COARSE 3
+#define CM_DENSE_STREAM 4
 int32_t cm_dense_search_kind(cm_dense *h, int32_t nq, int32_t k);
 /* force a scan kernel for this handle (0 = automatic; an ineligible forced
  * kind falls back to the automatic choice).  Results agree within the 1e-4
  * distance tolerance on every path; used for A/B probes and parity tests. */
 int cm_dense_set_path(cm_dense *h, int32_t kind);
-/* K1c: number of queries of the search that last used `workspace_dev` whose
- * certificate failed and that were re-run by the exact f16x3 pass
+/* K1c/K1s: number of queries of the search that last used `workspace_dev` whose
+ * certificate failed and that were re-run by the exact fp32 pass
  * (synchronous read; 0 for other paths, -1 on error).                    */
 int32_t cm_dense_workspace_fallbacks(cm_dense *h, int32_t nq, int32_t k, const void *workspace_dev);
 /* same, for the last host-array cm_dense_search on this handle. */
 int32_t cm_dense_last_fallbacks(cm_dense *h);
 /* kernel timing (bench roofline): while enabled, every search records HIP
- * events on its launch stream around its scan kernel (K1 / K1b / K1c coarse
+ * events on its launch stream around its scan kernel (K1 / K1c / K1s coarse
  * scan); _drain synchronises on them, writes up to cap elapsed ms values and
  * returns how many were recorded (< 0 on error).                         */
 int cm_dense_timing(cm_dense *h, int32_t enable);

@@ -65,7 +65,7 @@ def test_dense_golden_corpus(eng, corpus, golden):
         np.testing.assert_allclose(dist[i], [w[1] for w in want], atol=DIST_TOL)
 
 
-PATHS = [0, 1, 2, 3]   # auto, K1 fp32, K1b f16x3, K1c coarse + certified re-rank
+PATHS = [0, 1, 3, 4]   # auto, K1 fp32, K1c coarse (256-query passes), K1s coarse (<= 32-query streams)
 
 
 @pytest.mark.parametrize("path", PATHS[1:])
@@ -110,11 +110,12 @@ def test_dense_shapes(eng, n, nq, k, dim, path):
 
 @pytest.mark.parametrize("n,nq,k,dim", [(30000, 64, 24, 768), (12345, 100, 10, 384), (5000, 300, 32, 100),
                                         (40000, 256, 1, 768), (257, 80, 32, 64)])
-@pytest.mark.parametrize("path", [2, 3])
+@pytest.mark.parametrize("path", [2, 3, 4])
 def test_dense_batched_split_paths(eng, n, nq, k, dim, path):
-    """K1b (f16x3 split planes) and K1c (coarse f16 scan + certified exact re-rank),
-    all queries of a pass resident: distances within 1e-4, sets/order as the oracle,
-    deletes and filters honoured, multiple query passes (nq > 256)."""
+    """K1c (coarse f16 scan, all queries of a pass resident) and K1s (<= 32 queries, per-wave
+    streams), both + certified exact re-rank; path 2 (the retired K1b) means automatic:
+    distances within 1e-4, sets/order as the oracle, deletes and filters honoured, multiple
+    query passes (nq > 256)."""
     rng = np.random.default_rng(n + nq + k)
     emb = rng.standard_normal((n, dim)).astype(np.float32) * rng.uniform(0.1, 10, (n, 1)).astype(np.float32)
     q = rng.standard_normal((nq, dim)).astype(np.float32)
@@ -133,18 +134,20 @@ def test_dense_batched_split_paths(eng, n, nq, k, dim, path):
     _check_dense(dist, rows, emb, q, k, live)
 
 
-def test_dense_coarse_certificate(eng):
-    """K1c: on well-separated data every query is certified (no exact re-run); on a
-    cluster of near-duplicates wider than the coarse lists the certificate fails and
-    the exact f16x3 pass takes over -- results stay within tolerance either way."""
+@pytest.mark.parametrize("path", [3, 4])
+def test_dense_coarse_certificate(eng, path):
+    """K1c / K1s: on well-separated data every query is certified (no exact re-run); on a
+    cluster of near-duplicates wider than the coarse lists the certificate fails and the
+    exact fp32 K1 pass takes over for those queries -- results stay within tolerance."""
     rng = np.random.default_rng(77)
     n, dim = 30000, 768
     emb = rng.standard_normal((n, dim)).astype(np.float32)
-    q = rng.standard_normal((64, dim)).astype(np.float32)
+    nq = 64 if path == 3 else 16
+    q = rng.standard_normal((nq, dim)).astype(np.float32)
     idx = eng.DenseIndex(dim)
-    idx.set_path(3)
+    idx.set_path(path)
     idx.upsert(emb, np.arange(n))
-    assert idx.search_kind(64, 24) == 3
+    assert idx.search_kind(nq, 24) == path
     dist, rows = idx.search(q, 24)
     _check_dense(dist, rows, emb, q, 24)
     assert idx.last_fallbacks() == 0

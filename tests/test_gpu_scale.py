@@ -249,11 +249,11 @@ def test_e5_base_b32_s256_fp32_and_bf16_bound():
     torch.cuda.synchronize()
     torch.testing.assert_close(p_out, ref_r, atol=2e-5, rtol=0)
     torch.testing.assert_close(f32.encode_token_ids(ids, mask), ref_r, atol=2e-5, rtol=0)
-    # bf16 opt-in (same weights): per-embedding cosine to fp32 >= 1 - 2e-3
+    # bf16 opt-in (same weights): per-embedding cosine to fp32 >= 1 - 2e-4
     b16 = E5MultilingualEmbedder.random_init(seed=0, device="cuda", dtype="bfloat16")
     out16 = b16.encode_token_ids(ids, mask)
     cos = (out16 * ref_r).sum(1)
-    assert float(cos.min()) >= 1 - 2e-3, float(cos.min())
+    assert float(cos.min()) >= 1 - 2e-4, float(cos.min())      # measured 1 - 2.4e-5 on MI355X
     print(f"\nE5 bf16 vs fp32 (B={B}, S<={S}): min cosine {float(cos.min()):.6f}, "
           f"mean 1-cos {float((1 - cos).mean()):.2e}")
 
