@@ -352,6 +352,106 @@ class BM25Index:
         return out
 
 
+    # ---- filtered device search (quirk Q2 on the device; SURVEY §8e for shards) -----------------
+    FILT_EPS_MISSING, FILT_ZERO_DIV, FILT_TABLE = 1, 2, 4
+
+    def prepare_filtered(self, max_docs: int = 0):
+        """Upload the log table the device idf needs (once per index, before any graph capture;
+        max_docs = the global corpus size when this index is a shard)."""
+        L.check(L.fn["cm_bm25_prepare_filtered"](self._h, int(max_docs)), "cm_bm25_prepare_filtered")
+
+    def filter_stats_dev(self, allow, q_terms, stats=None, df=None):
+        """Candidate statistics of a device allow bitmap: stats int64 (2,) = {Nc, sum of lengths},
+        df int64 (T,) per query term (device tensors, torch's stream, async)."""
+        dev = q_terms.device
+        if stats is None:
+            stats = torch.empty(2, dtype=torch.int64, device=dev)
+        if df is None:
+            df = torch.empty(max(q_terms.numel(), 1), dtype=torch.int64, device=dev)
+        L.check(L.fn["cm_bm25_filter_stats_dev"](self._h, L.ptr(allow), L.ptr(q_terms), int(q_terms.numel()),
+                                                 L.ptr(stats), L.ptr(df), _stream(self.device)),
+                "cm_bm25_filter_stats_dev")
+        return stats, df
+
+    def filter_term_stats_dev(self, allow):
+        """Per-term candidate df (int64 (V,)) and first-occurrence keys (int64 view of the uint64
+        row << 32 | position keys, -1 = none) of a device allow bitmap."""
+        dev = torch.device("cuda", self.device)
+        df = torch.empty(max(self.vocab, 1), dtype=torch.int64, device=dev)
+        fk = torch.empty(max(self.vocab, 1), dtype=torch.int64, device=dev)
+        L.check(L.fn["cm_bm25_filter_term_stats_dev"](self._h, L.ptr(allow), L.ptr(df), L.ptr(fk),
+                                                      _stream(self.device)), "cm_bm25_filter_term_stats_dev")
+        return df[: self.vocab], fk[: self.vocab]
+
+    def filter_eps(self, allow) -> float:
+        """rank_bm25's epsilon floor over the candidates of one filter (host or device words)."""
+        ab = allow if hasattr(allow, "data_ptr") else _c(allow, np.uint32)
+        e = C.c_double(0.0)
+        L.check(L.fn["cm_bm25_filter_eps"](self._h, L.ptr(ab), C.byref(e)), "cm_bm25_filter_eps")
+        return e.value
+
+    def search_stats_dev(self, q_terms, q_off, k: int, allow, stats, df, eps=None, out=None, status=None,
+                         workspace=None):
+        """Device search of the allowed documents with the given candidate statistics (device
+        tensors; eps: device float64 (1,) or None).  Returns (scores, rows, status int32 (1,))."""
+        nq = q_off.numel() - 1
+        total = q_terms.numel()
+        dev = q_terms.device
+        wsb = self.workspace_bytes(nq, total, k)
+        if workspace is None:
+            if self._ws is None or self._ws.numel() < wsb:
+                self._ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
+            workspace = self._ws
+        if out is None:
+            out = (torch.empty((nq, k), dtype=torch.float64, device=dev),
+                   torch.empty((nq, k), dtype=torch.int64, device=dev))
+        if status is None:
+            status = torch.empty(1, dtype=torch.int32, device=dev)
+        L.check(L.fn["cm_bm25_search_stats_dev"](self._h, L.ptr(q_terms), L.ptr(q_off), nq, total, int(k),
+                                                 L.ptr(allow), L.ptr(stats), L.ptr(df), L.ptr(eps), L.ptr(out[0]),
+                                                 L.ptr(out[1]), L.ptr(status), L.ptr(workspace),
+                                                 int(workspace.numel()), _stream(self.device)),
+                "cm_bm25_search_stats_dev")
+        return out[0], out[1], status
+
+    def search_filtered_dev(self, q_terms, q_off, k: int, allow, eps=None, out=None, status=None, workspace=None):
+        """One-index filtered device search (statistics over the allowed candidates on the device,
+        graph-capturable).  Returns (scores, rows, status); see FILT_* for the status bits."""
+        nq = q_off.numel() - 1
+        total = q_terms.numel()
+        dev = q_terms.device
+        wsb = self.workspace_bytes(nq, total, k)
+        if workspace is None:
+            if self._ws is None or self._ws.numel() < wsb:
+                self._ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
+            workspace = self._ws
+        if out is None:
+            out = (torch.empty((nq, k), dtype=torch.float64, device=dev),
+                   torch.empty((nq, k), dtype=torch.int64, device=dev))
+        if status is None:
+            status = torch.empty(1, dtype=torch.int32, device=dev)
+        L.check(L.fn["cm_bm25_search_filtered_dev"](self._h, L.ptr(q_terms), L.ptr(q_off), nq, total, int(k),
+                                                    L.ptr(allow), L.ptr(eps), L.ptr(out[0]), L.ptr(out[1]),
+                                                    L.ptr(status), L.ptr(workspace), int(workspace.numel()),
+                                                    _stream(self.device)), "cm_bm25_search_filtered_dev")
+        return out[0], out[1], status
+
+    def search_filtered(self, q_terms, q_off, k: int, allow):
+        """search_filtered_dev with the eps recovery step: when an idf is negative the filter's
+        epsilon is computed (cm_bm25_filter_eps) and the batch searched again.  Synchronises."""
+        s, r, st = self.search_filtered_dev(q_terms, q_off, k, allow)
+        code = int(st.item())
+        if code & self.FILT_EPS_MISSING:
+            eps = torch.tensor([self.filter_eps(allow)], dtype=torch.float64, device=q_terms.device)
+            s, r, st = self.search_filtered_dev(q_terms, q_off, k, allow, eps=eps)
+            code = int(st.item())
+        if code & self.FILT_ZERO_DIV:
+            raise ZeroDivisionError("float division by zero (candidate documents have no tokens)")
+        if code:
+            raise RuntimeError(f"filtered BM25 search status {code}")
+        return s, r
+
+
 # ---------------------------------------------------------------------------
 # Fusion and pooling ops
 # ---------------------------------------------------------------------------

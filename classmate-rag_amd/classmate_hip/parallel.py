@@ -11,7 +11,14 @@ global rows [row0_r, row0_r + n_r).  Exchanges, and only these:
 * per query batch — all-gather of each shard's top-k (dense: distance + global
   row; BM25: score + global row), then a deterministic merge identical on all
   ranks; the MMR pool's embeddings are assembled with one all-reduce SUM (each
-  rank contributes the rows it owns, zeros elsewhere).
+  rank contributes the rows it owns, zeros elsewhere);
+* per filtered BM25 batch (quirk Q2: rank_bm25's statistics over the filtered
+  candidates, rag/retrieval/bm25.py:184-191) — one all-reduce SUM of the
+  candidate count, their total length and the candidate df of the query terms,
+  so every shard scores with the global filtered idf/avgdl; only when some idf
+  is negative (a term in more than half of the candidates) a second exchange of
+  every term's candidate df (SUM) and first-occurrence key (MIN) gives the
+  epsilon floor in the global first-occurrence order.
 
 The merges are torch ops so they run on either backend; the per-shard search is
 the HIP path (classmate_hip.engine).
@@ -150,6 +157,55 @@ def merge_bm25_topk(score_t, rows_t, k: int, group=None):
     i2 = torch.argsort(-S1, dim=1, stable=True)  # ... then score desc (stable keeps row order)
     idx = torch.gather(i1, 1, i2)[:, :k]
     return torch.gather(S, 1, idx), torch.gather(R, 1, idx)
+
+
+def allreduce_filtered_stats(stats_t, df_t, group=None):
+    """Sum the shards' candidate statistics ({Nc, sum of lengths} and per-query-term df, int64
+    tensors, in place; identity when world == 1).  Runs on the collective's device."""
+    _, ws = world()
+    if ws == 1:
+        return stats_t, df_t
+    dev = _coll_device(group)
+    for t in (stats_t, df_t):
+        x = t.to(dev)
+        dist.all_reduce(x, op=dist.ReduceOp.SUM, group=group)
+        if x.data_ptr() != t.data_ptr():
+            t.copy_(x)
+    return stats_t, df_t
+
+
+def filtered_eps_global(df_v: np.ndarray, first_key: np.ndarray, row0: int, n_cand: int, group=None) -> float:
+    """rank_bm25's epsilon over the global candidate set: every term's candidate df summed and its
+    first (global row, position) key minimised over the shards, then the idf average in that
+    first-occurrence order (bm25_idf_table)."""
+    gdf, gfk, _, _ = allreduce_bm25_stats(np.asarray(df_v, np.int64), np.asarray(first_key, np.uint64), row0, 0, 0,
+                                          group=group)
+    _, eps = bm25_idf_table(gdf, gfk, int(n_cand))
+    return eps
+
+
+def bm25_search_filtered_sharded(bm, q_terms, q_off, k: int, allow, row0: int, group=None):
+    """Filtered BM25 over a sharded corpus: local candidate statistics -> all-reduce -> every shard
+    scores its allowed documents with the global statistics (device idf) -> all-gather merge.
+    bm: this rank's engine.BM25Index (prepare_filtered(global docs) called); allow: this shard's
+    device allow words.  Returns the global (scores, global rows) top-k, identical on all ranks."""
+    stats, df = bm.filter_stats_dev(allow, q_terms)
+    allreduce_filtered_stats(stats, df, group)
+    s, r, st = bm.search_stats_dev(q_terms, q_off, k, allow, stats, df)
+    code = int(st.item())
+    if code & bm.FILT_EPS_MISSING:          # the same on every rank: the statistics are global
+        dfv, fkv = bm.filter_term_stats_dev(allow)
+        eps = filtered_eps_global(dfv.cpu().numpy(), fkv.cpu().numpy().view(np.uint64), row0,
+                                  int(stats[0].item()), group)
+        eps_t = torch.tensor([eps], dtype=torch.float64, device=q_terms.device)
+        s, r, st = bm.search_stats_dev(q_terms, q_off, k, allow, stats, df, eps=eps_t)
+        code = int(st.item())
+    if code & bm.FILT_ZERO_DIV:
+        raise ZeroDivisionError("float division by zero (candidate documents have no tokens)")
+    if code:
+        raise RuntimeError(f"filtered BM25 search status {code}")
+    rg = torch.where(r >= 0, r + row0, r)
+    return merge_bm25_topk(s, rg, k, group)
 
 
 def assemble_pool_vectors(rows_t, local_vecs, row0: int, n_local: int, group=None):

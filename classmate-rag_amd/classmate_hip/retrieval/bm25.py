@@ -240,8 +240,7 @@ class BM25Store:
         k = min(k, n_cand)
         if k <= 0:
             return out
-        if k > engine.L.max_topk():
-            raise ValueError(f"top_k={top_k} exceeds the GPU top-k limit {engine.L.max_topk()}")
+        # k beyond the fused kernels' lists (cm_max_topk) runs the full-order device path
         qids = [self._query_ids(queries[i]) for i in live]
         scores, rows, nvalid = self._index.search(qids, k, allow)
         for j, i in enumerate(live):

@@ -222,8 +222,7 @@ class GpuVectorStore:
         k = min(int(top_k), n_ok)
         if k <= 0:
             return None
-        if k > engine.L.max_topk():
-            raise ValueError(f"top_k={top_k} exceeds the GPU top-k limit {engine.L.max_topk()}")
+        # k beyond the fused kernels' lists (cm_max_topk) runs the full-order device path
         return self._index.search(q, k, allow, return_vectors=include_embeddings)
 
     def _items(self, dist, rows, vecs, i, include_documents, include_embeddings) -> List[Dict[str, Any]]:

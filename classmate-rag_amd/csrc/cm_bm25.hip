@@ -240,7 +240,8 @@ __device__ inline double kd_of(int32_t dlen, double avgdl) {
   t = 0.25 + t;
   return 1.5 * t;
 }
-__global__ void bm25_lut_kernel(double avgdl, int dmin, double *__restrict__ lut) {
+__global__ void bm25_lut_kernel(const double *__restrict__ avgdl_p, int dmin, double *__restrict__ lut) {
+  const double avgdl = *avgdl_p;
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= kLutW * kLutTF) return;
   const int tf = i % kLutTF, dl = dmin + i / kLutTF;
@@ -288,14 +289,18 @@ __global__ void __launch_bounds__(kBmThreads) __attribute__((amdgpu_waves_per_eu
                       const TF *__restrict__ post_tf, const int32_t *__restrict__ head_id,
                       const uint8_t *__restrict__ headtf, int64_t npad, const int32_t *__restrict__ dl,
                       const uint32_t *__restrict__ live, const uint32_t *__restrict__ allow, int64_t ndocs,
-                      double avgdl, const double *__restrict__ lut, int lut_dmin, int k,
+                      const double *__restrict__ avgdl_p, const double *__restrict__ lut, int lut_dmin, int k,
                       uint64_t *__restrict__ cand_key, uint32_t *__restrict__ cand_row,
                       unsigned long long *__restrict__ thr_key, const uint8_t *__restrict__ need, int32_t vocab,
                       int dbg) {
   __shared__ double s_lut[kLutW * kLutTF];
+#ifndef CM_ABLATION
+  dbg = 0;  // product build: the ablation branches fold away
+#endif
   __shared__ int32_t s_pdoc[kBmThreads / 64][kTailCapW];
   __shared__ uint16_t s_ptf[kBmThreads / 64][kTailCapW];
   __shared__ uint64_t s_keys[kBmThreads / 64][16 * 64];
+  const double avgdl = *avgdl_p;
   for (int i = threadIdx.x; i < kLutW * kLutTF; i += kBmThreads) s_lut[i] = lut[i];
   __syncthreads();  // the only block-wide barrier
   const int lane = threadIdx.x & 63;
@@ -756,7 +761,7 @@ __global__ void bm25_filtered_stats_kernel(const int32_t *__restrict__ dl, const
 // Per listed term: number of candidate postings and the first candidate
 // posting's (doc << 32 | first position) key (terms' dict order).
 __global__ void __launch_bounds__(256) bm25_term_df_kernel(const int32_t *__restrict__ terms, int n_terms,
-                                                           const int64_t *__restrict__ term_off,
+                                                           int32_t vocab, const int64_t *__restrict__ term_off,
                                                            const int32_t *__restrict__ post_doc,
                                                            const uint32_t *__restrict__ post_pos,
                                                            const uint32_t *__restrict__ live,
@@ -765,6 +770,13 @@ __global__ void __launch_bounds__(256) bm25_term_df_kernel(const int32_t *__rest
   const int i = blockIdx.x;
   if (i >= n_terms) return;
   const int32_t t = terms ? terms[i] : i;
+  if (t < 0 || t >= vocab) {  // unknown query term: not in the candidate vocabulary
+    if (threadIdx.x == 0) {
+      out_df[i] = 0;
+      if (out_first) out_first[i] = ~0ull;
+    }
+    return;
+  }
   __shared__ unsigned long long red_c[4];
   __shared__ unsigned long long red_m[4];
   unsigned long long c = 0, m = ~0ull;
@@ -854,6 +866,68 @@ __global__ void first_key_kernel(const int64_t *__restrict__ term_off, const int
   first[t] = p < term_off[t + 1] ? (((uint64_t)(uint32_t)post_doc[p] << 32) | post_pos[p]) : ~0ull;
 }
 
+// k > kMaxTopK (BM25Store.search with a large top_k, rag/retrieval/bm25.py:199): every candidate's
+// score.  One launch per query term in query order adds the term's contribution to each of its
+// postings' documents (a document appears once per term: no atomics; the sums follow rank_bm25's
+// term order, and the quotient is the IEEE division the fused kernels' ratio table / Newton
+// sequence reproduce bit for bit); then one key per document for a stable descending sort.
+__global__ void bm25_scatter_term_kernel(int64_t lo, int64_t hi, const int32_t *__restrict__ post_doc,
+                                         const uint16_t *__restrict__ post_tf, const int32_t *__restrict__ dl,
+                                         double idf, double avgdl, double *__restrict__ score) {
+  const int64_t p = lo + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= hi) return;
+  const int32_t d = post_doc[p];
+  score[d] = score[d] + bm25_contrib(idf, (uint32_t)post_tf[p], kd_of(dl[d], avgdl));
+}
+__global__ void bm25_score_keys_kernel(const double *__restrict__ score, const uint32_t *__restrict__ live,
+                                       const uint32_t *__restrict__ allow, int64_t ndocs, uint64_t *__restrict__ keys,
+                                       int32_t *__restrict__ rows) {
+  const int64_t d = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (d >= ndocs) return;
+  const uint32_t w = live[d >> 5] & (allow ? allow[d >> 5] : 0xffffffffu);
+  keys[d] = ((w >> (d & 31)) & 1u) ? score_key(score[d]) : kEmptyKey;
+  rows[d] = (int32_t)d;
+}
+
+__global__ void bm25_set_f64_kernel(double v, double *__restrict__ out) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) *out = v;
+}
+
+// Statistics over a filtered candidate set (quirk Q2, rag/retrieval/bm25.py:184-191) on the device:
+// stats = {Nc, sum of candidate lengths} (global sums on a sharded index), df[i] = candidate df of
+// query term i.  idf = L[Nc - df] - L[df] with L[x] = glibc log(x + 0.5) precomputed on the host
+// (cm_bm25_prepare_filtered), i.e. the same two logs and one subtraction as rank_bm25's
+// math.log(Nc - df + 0.5) - math.log(df + 0.5): bit-identical to the host path.  A negative idf
+// takes the candidate vocabulary's epsilon from *eps_dev (NaN / NULL: status bit 0 -- the caller
+// computes it with cm_bm25_filter_eps and searches again).  status bit 1: candidates without
+// tokens (rank_bm25's ZeroDivisionError), bit 2: Nc beyond the prepared log table.
+__global__ void bm25_stats_idf_kernel(const int32_t *__restrict__ q_terms, int n, int32_t vocab,
+                                      const int64_t *__restrict__ stats, const int64_t *__restrict__ df,
+                                      const double *__restrict__ logtab, int64_t log_n,
+                                      const double *__restrict__ eps_dev, double *__restrict__ q_idf,
+                                      double *__restrict__ avgdl, int32_t *__restrict__ status) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t nc = stats[0], sl = stats[1];
+  if (i == 0) {
+    *avgdl = nc > 0 ? (double)sl / (double)nc : 1.0;  // Nc == 0: nothing is scored
+    if (nc > 0 && sl == 0) atomicOr(status, 2);
+    if (nc > log_n) atomicOr(status, 4);
+  }
+  if (i >= n) return;
+  const int32_t t = q_terms[i];
+  const int64_t d = df[i];
+  double v = 0.0;
+  if (t >= 0 && t < vocab && d > 0 && nc <= log_n) {
+    v = logtab[nc - d] - logtab[d];
+    if (v < 0) {
+      const double e = eps_dev ? *eps_dev : __builtin_nan("");
+      if (e != e) atomicOr(status, 1);
+      v = e;
+    }
+  }
+  q_idf[i] = v;
+}
+
 }  // namespace cm
 
 using namespace cm;
@@ -868,6 +942,8 @@ struct cm_bm25 {
   bool empty_vocab = false;  // live docs exist but no tokens (ZeroDivisionError on search)
   DevBuf term_off, post_doc, post_tf, post_pos, dl, live, idf;
   DevBuf headtf, head_id;  // dense tf tiles for high-df terms (K2 fast path)
+  DevBuf logtab;           // L[x] = log(x + 0.5), x <= log_n (filtered device statistics)
+  int64_t log_n = -1;
   DevBuf head_maxtf, range_mindl;  // pruned search: per-(head, range) max tf, per-range min length
   DevBuf blk_maxtf, blk_mindl;     // the same per 64-doc block
   int32_t path = 0;                // 0 auto (pruned), 1 full K2 scan, 2 pruned
@@ -1043,6 +1119,9 @@ struct BmWs {
   uint64_t *items;  // K2b work items (pruned search)
   uint8_t *qcand;   // per query term: postings walked
   uint32_t *item_count;
+  double *avgdl;    // the search's avgdl (unfiltered, host-computed or device-computed statistics)
+  int64_t *stats;   // filtered entry: {Nc, sum of candidate lengths}
+  int64_t *df;      // filtered entry: candidate df per query term
   size_t total;
 };
 
@@ -1071,14 +1150,20 @@ BmWs bm_ws_layout(const cm_bm25 *h, int nq, int total_terms, int k, void *base) 
   off += 256;
   w.qcand = reinterpret_cast<uint8_t *>(p + off);
   off += round_up(std::max(total_terms, 1), 256);
+  w.avgdl = reinterpret_cast<double *>(p + off);
+  off += 256;
+  w.stats = reinterpret_cast<int64_t *>(p + off);
+  off += 256;
+  w.df = reinterpret_cast<int64_t *>(p + off);
+  off += round_up((int64_t)std::max(total_terms, 1) * 8, 256);
   w.total = off;
   return w;
 }
 
-// Launch K2 + merge given q_idf already in the workspace.
+// Launch K2 + merge given q_idf and *avgdl already in the workspace.
 int bm25_launch_core(cm_bm25 *h, const int32_t *q_terms_dev, const int32_t *q_off_dev, int nq, int total_terms, int k,
-                     const uint32_t *allow_dev, double avgdl, const BmWs &w, double *score_dev, int64_t *row_dev,
-                     hipStream_t st) {
+                     const uint32_t *allow_dev, const BmWs &w, double *score_dev, int64_t *row_dev, hipStream_t st) {
+  const double *avgdl = w.avgdl;
   const int nr = (int)std::max<int64_t>(1, ceil_div(h->ndocs, kRange));
   if (nr > kMergePer * kMergeThreads) CM_FAIL(CM_EUNSUPPORTED, "BM25 shard too large (> 16.7M docs)");
   const int ngroups = (nr + 1 + kBoundsGroup - 1) / kBoundsGroup;
@@ -1095,7 +1180,8 @@ int bm25_launch_core(cm_bm25 *h, const int32_t *q_terms_dev, const int32_t *q_of
     CM_HIP(hipGetLastError());
   }
   CM_HIP(hipMemsetAsync(w.thr, 0xff, (size_t)nq * 8, st));  // no threshold yet
-  hipLaunchKernelGGL(bm25_lut_kernel, dim3(kLutW * kLutTF / 256), dim3(256), 0, st, avgdl, h->lut_dmin, w.lut);
+  hipLaunchKernelGGL(bm25_lut_kernel, dim3(kLutW * kLutTF / 256), dim3(256), 0, st, (const double *)avgdl, h->lut_dmin,
+                     w.lut);
   CM_HIP(hipGetLastError());
   // ranges per wave: enough waves to fill 256 CUs many times over, long runs otherwise
   const int64_t nqg = ceil_div(nq, kQPerWave);
@@ -1168,6 +1254,89 @@ void bm25_free(cm_bm25 *h) {
                     &h->qbuf, &h->obuf, &h->allow_buf, &h->tmp, &h->headtf, &h->head_id, &h->head_maxtf,
                     &h->range_mindl, &h->blk_maxtf, &h->blk_mindl})
     b->release();
+}
+
+// Host-array search with k > kMaxTopK: full per-document scores (bm25_scatter_term_kernel, query
+// term order), a stable radix sort by (score desc) over the documents in row order (ties keep the
+// lower row first, zero scores pad in insertion order: quirk Q1), the first k candidates.
+int bm25_search_full(cm_bm25 *h, const int32_t *q_terms, const int32_t *q_off, int nq, int k, const double *q_idf,
+                     double avgdl, const uint32_t *allow_dev, int64_t n_cand, double *out_score, int64_t *out_row) {
+  const int64_t n = std::max<int64_t>(h->ndocs, 1);
+  int rc;
+  size_t tmp_bytes = 0;
+  CM_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, (const uint64_t *)nullptr, (uint64_t *)nullptr,
+                                            (const int32_t *)nullptr, (int32_t *)nullptr, (int)n, 0, 64, h->stream));
+  const size_t off1 = round_up((int64_t)tmp_bytes, 256);
+  const size_t need = off1 + (size_t)round_up(n * 8, 256) * 3 + (size_t)round_up(n * 4, 256) * 2;
+  if ((rc = h->ws.ensure(need))) return rc;
+  char *base = h->ws.as<char>();
+  double *score = reinterpret_cast<double *>(base + off1);
+  uint64_t *keys = reinterpret_cast<uint64_t *>(base + off1 + round_up(n * 8, 256));
+  uint64_t *skeys = reinterpret_cast<uint64_t *>(base + off1 + 2 * round_up(n * 8, 256));
+  int32_t *rows = reinterpret_cast<int32_t *>(base + off1 + 3 * round_up(n * 8, 256));
+  int32_t *srows = rows + round_up(n * 4, 256) / 4;
+  const int64_t kk = std::min<int64_t>(k, n_cand);
+  std::vector<uint64_t> hk((size_t)std::max<int64_t>(kk, 1));
+  std::vector<int32_t> hr((size_t)std::max<int64_t>(kk, 1));
+  for (int i = 0; i < nq; ++i) {
+    CM_HIP(hipMemsetAsync(score, 0, (size_t)n * 8, h->stream));
+    for (int32_t j = q_off[i]; j < q_off[i + 1]; ++j) {
+      const int32_t t = q_terms[j];
+      if (t < 0 || t >= h->vocab || q_idf[j] == 0.0) continue;  // adds idf * ratio = +-0: no change
+      int64_t lh[2];
+      CM_HIP(hipMemcpyAsync(lh, h->term_off.as<int64_t>() + t, 16, hipMemcpyDeviceToHost, h->stream));
+      CM_HIP(hipStreamSynchronize(h->stream));
+      if (lh[1] <= lh[0]) continue;
+      hipLaunchKernelGGL(bm25_scatter_term_kernel, dim3((unsigned)ceil_div(lh[1] - lh[0], 256)), dim3(256), 0,
+                         h->stream, lh[0], lh[1], h->post_doc.as<int32_t>(), h->post_tf.as<uint16_t>(),
+                         h->dl.as<int32_t>(), q_idf[j], avgdl, score);
+      CM_HIP(hipGetLastError());
+    }
+    hipLaunchKernelGGL(bm25_score_keys_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, h->stream, score,
+                       h->live.as<uint32_t>(), allow_dev, h->ndocs, keys, rows);
+    CM_HIP(hipGetLastError());
+    CM_HIP(hipcub::DeviceRadixSort::SortPairs(base, tmp_bytes, keys, skeys, rows, srows, (int)n, 0, 64, h->stream));
+    if (kk > 0) {
+      CM_HIP(hipMemcpyAsync(hk.data(), skeys, (size_t)kk * 8, hipMemcpyDeviceToHost, h->stream));
+      CM_HIP(hipMemcpyAsync(hr.data(), srows, (size_t)kk * 4, hipMemcpyDeviceToHost, h->stream));
+    }
+    CM_HIP(hipStreamSynchronize(h->stream));
+    for (int j = 0; j < k; ++j) {
+      const bool ok = j < kk;
+      out_score[(int64_t)i * k + j] = ok ? f64_unorder(~hk[j]) : 0.0;
+      out_row[(int64_t)i * k + j] = ok ? (int64_t)hr[j] : -1;
+    }
+  }
+  return CM_OK;
+}
+
+// rank_bm25's epsilon over a candidate set: 0.25 x the mean idf of the candidate vocabulary, summed
+// in the terms' first-occurrence order (the reference's dict order), glibc logs, host fp64 adds.
+// The per-term candidate df and first (doc, position) keys come from one device pass.
+int filtered_eps(cm_bm25 *h, const uint32_t *allow_dev, int64_t n_cand, double *eps) {
+  const int32_t V = h->vocab;
+  int rc;
+  if ((rc = h->obuf.ensure((size_t)std::max(V, 1) * 16))) return rc;
+  int64_t *dfv = h->obuf.as<int64_t>();
+  uint64_t *fkv = reinterpret_cast<uint64_t *>(h->obuf.as<char>() + (size_t)V * 8);
+  hipLaunchKernelGGL(bm25_term_df_kernel, dim3((unsigned)V), dim3(256), 0, h->stream, (const int32_t *)nullptr, (int)V,
+                     V, h->term_off.as<int64_t>(), h->post_doc.as<int32_t>(), h->post_pos.as<uint32_t>(),
+                     h->live.as<uint32_t>(), allow_dev, dfv, fkv);
+  CM_HIP(hipGetLastError());
+  std::vector<int64_t> dfh((size_t)V);
+  std::vector<uint64_t> fkh((size_t)V);
+  CM_HIP(hipMemcpyAsync(dfh.data(), dfv, (size_t)V * 8, hipMemcpyDeviceToHost, h->stream));
+  CM_HIP(hipMemcpyAsync(fkh.data(), fkv, (size_t)V * 8, hipMemcpyDeviceToHost, h->stream));
+  CM_HIP(hipStreamSynchronize(h->stream));
+  std::vector<int32_t> order;
+  for (int32_t t = 0; t < V; ++t)
+    if (dfh[t] > 0) order.push_back(t);
+  if (order.empty()) CM_FAIL(CM_EZERODIV, "float division by zero (candidate documents have no tokens)");
+  std::sort(order.begin(), order.end(), [&](int32_t a, int32_t b) { return fkh[a] < fkh[b]; });
+  double sum = 0.0;
+  for (int32_t t : order) sum = sum + bm25_idf(n_cand, dfh[t]);
+  *eps = 0.25 * (sum / (double)order.size());
+  return CM_OK;
 }
 
 }  // namespace
@@ -1564,8 +1733,9 @@ int cm_bm25_search_dev(cm_bm25 *h, const int32_t *q_terms_dev, const int32_t *q_
                        total_terms, h->idf.as<double>(), h->vocab, w.q_idf);
     CM_HIP(hipGetLastError());
   }
-  return bm25_launch_core(h, q_terms_dev, q_off_dev, nq, total_terms, k, nullptr, h->avgdl, w, score_dev, row_dev,
-                          st);
+  hipLaunchKernelGGL(bm25_set_f64_kernel, dim3(1), dim3(64), 0, st, h->avgdl, w.avgdl);
+  CM_HIP(hipGetLastError());
+  return bm25_launch_core(h, q_terms_dev, q_off_dev, nq, total_terms, k, nullptr, w, score_dev, row_dev, st);
 }
 
 int cm_bm25_search(cm_bm25 *h, const int32_t *q_terms, const int32_t *q_off, int32_t nq, int32_t k,
@@ -1573,7 +1743,7 @@ int cm_bm25_search(cm_bm25 *h, const int32_t *q_terms, const int32_t *q_off, int
   if (!h) CM_FAIL(CM_EINVAL, "null handle");
   if (nq <= 0) return CM_OK;
   if (!q_off || !out_score || !out_row) CM_FAIL(CM_EINVAL, "NULL argument");
-  if (k <= 0 || k > kMaxTopK) CM_FAIL(CM_EINVAL, "k must be in [1, " + std::to_string(kMaxTopK) + "]");
+  if (k <= 0) CM_FAIL(CM_EINVAL, "k must be >= 1");
   const int32_t total = q_off[nq];
   if (total < 0 || (total > 0 && !q_terms)) CM_FAIL(CM_EINVAL, "bad q_off");
   for (int i = 0; i < nq; ++i)
@@ -1631,7 +1801,7 @@ int cm_bm25_search(cm_bm25 *h, const int32_t *q_terms, const int32_t *q_off, int
       if ((rc = h->qbuf.ensure(nu * 4)) || (rc = h->obuf.ensure(nu * 8))) return rc;
       CM_HIP(hipMemcpyAsync(h->qbuf.ptr, uterms.data(), nu * 4, hipMemcpyHostToDevice, h->stream));
       hipLaunchKernelGGL(bm25_term_df_kernel, dim3((unsigned)nu), dim3(256), 0, h->stream, h->qbuf.as<int32_t>(),
-                         (int)nu, h->term_off.as<int64_t>(), h->post_doc.as<int32_t>(), h->post_pos.as<uint32_t>(),
+                         (int)nu, h->vocab, h->term_off.as<int64_t>(), h->post_doc.as<int32_t>(), h->post_pos.as<uint32_t>(),
                          h->live.as<uint32_t>(), allow_dev, h->obuf.as<int64_t>(), (uint64_t *)nullptr);
       CM_HIP(hipGetLastError());
       CM_HIP(hipMemcpyAsync(udf.data(), h->obuf.ptr, nu * 8, hipMemcpyDeviceToHost, h->stream));
@@ -1640,29 +1810,7 @@ int cm_bm25_search(cm_bm25 *h, const int32_t *q_terms, const int32_t *q_off, int
         if (udf[u] > 0 && bm25_idf(n_cand, udf[u]) < 0) need_eps = true;
     }
     double eps = 0.0;
-    if (need_eps) {
-      // average idf over the whole candidate vocabulary in first-occurrence order
-      const int32_t V = h->vocab;
-      if ((rc = h->obuf.ensure((size_t)V * 16))) return rc;
-      int64_t *dfv = h->obuf.as<int64_t>();
-      uint64_t *fkv = reinterpret_cast<uint64_t *>(h->obuf.as<char>() + (size_t)V * 8);
-      hipLaunchKernelGGL(bm25_term_df_kernel, dim3((unsigned)V), dim3(256), 0, h->stream, (const int32_t *)nullptr,
-                         (int)V, h->term_off.as<int64_t>(), h->post_doc.as<int32_t>(), h->post_pos.as<uint32_t>(),
-                         h->live.as<uint32_t>(), allow_dev, dfv, fkv);
-      CM_HIP(hipGetLastError());
-      std::vector<int64_t> dfh((size_t)V);
-      std::vector<uint64_t> fkh((size_t)V);
-      CM_HIP(hipMemcpyAsync(dfh.data(), dfv, (size_t)V * 8, hipMemcpyDeviceToHost, h->stream));
-      CM_HIP(hipMemcpyAsync(fkh.data(), fkv, (size_t)V * 8, hipMemcpyDeviceToHost, h->stream));
-      CM_HIP(hipStreamSynchronize(h->stream));
-      std::vector<int32_t> order;
-      for (int32_t t = 0; t < V; ++t)
-        if (dfh[t] > 0) order.push_back(t);
-      std::sort(order.begin(), order.end(), [&](int32_t a, int32_t b) { return fkh[a] < fkh[b]; });
-      double s = 0.0;
-      for (int32_t t : order) s = s + bm25_idf(n_cand, dfh[t]);
-      eps = 0.25 * (s / (double)order.size());
-    }
+    if (need_eps && (rc = filtered_eps(h, allow_dev, n_cand, &eps))) return rc;
     for (int32_t i = 0; i < total; ++i) {
       const int32_t t = q_terms[i];
       if (t < 0 || t >= h->vocab) continue;
@@ -1672,6 +1820,16 @@ int cm_bm25_search(cm_bm25 *h, const int32_t *q_terms, const int32_t *q_off, int
       const double v = bm25_idf(n_cand, d);
       q_idf[i] = v < 0 ? eps : v;
     }
+  }
+  if (k > kMaxTopK) {  // beyond the fused top-k lists: full scores + one sort per query
+    rc = bm25_search_full(h, q_terms, q_off, nq, k, q_idf.data(), avgdl, allow_dev, n_cand, out_score, out_row);
+    if (rc) return rc;
+    if (out_n) {
+      const int32_t nv = (int32_t)std::min<int64_t>(k, n_cand);
+      for (int i = 0; i < nq; ++i) out_n[i] = nv;
+    }
+    h->last_rescored = -1;
+    return CM_OK;
   }
   // device search
   const int64_t wsb = cm_bm25_search_workspace(h, nq, total, k);
@@ -1686,7 +1844,9 @@ int cm_bm25_search(cm_bm25 *h, const int32_t *q_terms, const int32_t *q_off, int
   if (total > 0) CM_HIP(hipMemcpyAsync(w.q_idf, q_idf.data(), (size_t)total * 8, hipMemcpyHostToDevice, h->stream));
   double *d_score = h->obuf.as<double>();
   int64_t *d_row = reinterpret_cast<int64_t *>(d_score + (size_t)nq * k);
-  rc = bm25_launch_core(h, d_terms, d_off, nq, total, k, allow_dev, avgdl, w, d_score, d_row, h->stream);
+  hipLaunchKernelGGL(bm25_set_f64_kernel, dim3(1), dim3(64), 0, h->stream, avgdl, w.avgdl);
+  CM_HIP(hipGetLastError());
+  rc = bm25_launch_core(h, d_terms, d_off, nq, total, k, allow_dev, w, d_score, d_row, h->stream);
   if (rc) return rc;
   h->last_rescored = h->path == 1 ? -1 : count_rescored(h, nq, w, h->stream);
   CM_HIP(hipMemcpyAsync(out_score, d_score, (size_t)nq * k * 8, hipMemcpyDeviceToHost, h->stream));
@@ -1697,6 +1857,120 @@ int cm_bm25_search(cm_bm25 *h, const int32_t *q_terms, const int32_t *q_off, int
     for (int i = 0; i < nq; ++i) out_n[i] = nv;
   }
   return CM_OK;
+}
+
+int cm_bm25_prepare_filtered(cm_bm25 *h, int64_t max_docs) {
+  if (!h) CM_FAIL(CM_EINVAL, "null handle");
+  if (max_docs < 0 || max_docs >= (int64_t)1 << 40) CM_FAIL(CM_EINVAL, "bad max_docs");
+  const int64_t n = std::max(max_docs, h->ndocs);
+  if (n <= h->log_n) return CM_OK;
+  DeviceGuard dg(h->dev);
+  std::vector<double> L((size_t)n + 1);
+  for (int64_t x = 0; x <= n; ++x) L[(size_t)x] = std::log((double)x + 0.5);  // glibc, as bm25_idf
+  int rc = h->logtab.ensure(L.size() * 8);
+  if (rc) return rc;
+  CM_HIP(hipMemcpyAsync(h->logtab.ptr, L.data(), L.size() * 8, hipMemcpyHostToDevice, h->stream));
+  CM_HIP(hipStreamSynchronize(h->stream));
+  h->log_n = n;
+  return CM_OK;
+}
+
+int cm_bm25_filter_stats_dev(cm_bm25 *h, const uint32_t *allow_dev, const int32_t *q_terms_dev, int32_t n_terms,
+                             int64_t *stats_dev, int64_t *df_dev, void *stream) {
+  if (!h || !allow_dev || !stats_dev || (n_terms > 0 && (!q_terms_dev || !df_dev))) CM_FAIL(CM_EINVAL, "NULL argument");
+  if (n_terms < 0) CM_FAIL(CM_EINVAL, "n_terms must be >= 0");
+  DeviceGuard dg(h->dev);
+  hipStream_t st = (hipStream_t)stream;
+  const int64_t nw = std::max<int64_t>(1, ceil_div(h->ndocs, 32));
+  CM_HIP(hipMemsetAsync(stats_dev, 0, 16, st));
+  if (h->ndocs > 0) {
+    hipLaunchKernelGGL(bm25_filtered_stats_kernel, dim3((unsigned)std::min<int64_t>(1024, ceil_div(nw, 256))),
+                       dim3(256), 0, st, h->dl.as<int32_t>(), h->live.as<uint32_t>(), allow_dev, h->ndocs,
+                       reinterpret_cast<unsigned long long *>(stats_dev));
+    CM_HIP(hipGetLastError());
+  }
+  if (n_terms > 0) {
+    if (h->npost == 0) {
+      CM_HIP(hipMemsetAsync(df_dev, 0, (size_t)n_terms * 8, st));
+    } else {
+      hipLaunchKernelGGL(bm25_term_df_kernel, dim3((unsigned)n_terms), dim3(256), 0, st, q_terms_dev, (int)n_terms,
+                         h->vocab, h->term_off.as<int64_t>(), h->post_doc.as<int32_t>(), h->post_pos.as<uint32_t>(),
+                         h->live.as<uint32_t>(), allow_dev, df_dev, (uint64_t *)nullptr);
+      CM_HIP(hipGetLastError());
+    }
+  }
+  return CM_OK;
+}
+
+int cm_bm25_filter_term_stats_dev(cm_bm25 *h, const uint32_t *allow_dev, int64_t *df_dev, uint64_t *first_dev,
+                                  void *stream) {
+  if (!h || !allow_dev || !df_dev || !first_dev) CM_FAIL(CM_EINVAL, "NULL argument");
+  if (h->vocab <= 0) return CM_OK;
+  DeviceGuard dg(h->dev);
+  hipLaunchKernelGGL(bm25_term_df_kernel, dim3((unsigned)h->vocab), dim3(256), 0, (hipStream_t)stream,
+                     (const int32_t *)nullptr, (int)h->vocab, h->vocab, h->term_off.as<int64_t>(),
+                     h->post_doc.as<int32_t>(), h->post_pos.as<uint32_t>(), h->live.as<uint32_t>(), allow_dev, df_dev,
+                     first_dev);
+  CM_HIP(hipGetLastError());
+  return CM_OK;
+}
+
+int cm_bm25_filter_eps(cm_bm25 *h, const uint32_t *allow_bits, double *eps_out) {
+  if (!h || !allow_bits || !eps_out) CM_FAIL(CM_EINVAL, "NULL argument");
+  DeviceGuard dg(h->dev);
+  int rc;
+  const int64_t nw = std::max<int64_t>(1, ceil_div(h->ndocs, 32));
+  if ((rc = h->allow_buf.ensure((size_t)nw * 4)) || (rc = h->tmp.ensure(16))) return rc;
+  CM_HIP(hipMemcpyAsync(h->allow_buf.ptr, allow_bits, (size_t)nw * 4, hipMemcpyDefault, h->stream));
+  CM_HIP(hipMemsetAsync(h->tmp.ptr, 0, 16, h->stream));
+  hipLaunchKernelGGL(bm25_filtered_stats_kernel, dim3((unsigned)std::min<int64_t>(1024, ceil_div(nw, 256))), dim3(256),
+                     0, h->stream, h->dl.as<int32_t>(), h->live.as<uint32_t>(), h->allow_buf.as<uint32_t>(), h->ndocs,
+                     h->tmp.as<unsigned long long>());
+  CM_HIP(hipGetLastError());
+  unsigned long long st2[2];
+  CM_HIP(hipMemcpyAsync(st2, h->tmp.ptr, 16, hipMemcpyDeviceToHost, h->stream));
+  CM_HIP(hipStreamSynchronize(h->stream));
+  if (st2[0] == 0) {
+    *eps_out = 0.0;
+    return CM_OK;
+  }
+  return filtered_eps(h, h->allow_buf.as<uint32_t>(), (int64_t)st2[0], eps_out);
+}
+
+int cm_bm25_search_stats_dev(cm_bm25 *h, const int32_t *q_terms_dev, const int32_t *q_off_dev, int32_t nq,
+                             int32_t total_terms, int32_t k, const uint32_t *allow_dev, const int64_t *stats_dev,
+                             const int64_t *df_dev, const double *eps_dev, double *score_dev, int64_t *row_dev,
+                             int32_t *status_dev, void *workspace_dev, int64_t workspace_bytes, void *stream) {
+  if (!h) CM_FAIL(CM_EINVAL, "null handle");
+  if (nq <= 0) return CM_OK;
+  if (k <= 0 || k > kMaxTopK) CM_FAIL(CM_EINVAL, "k must be in [1, " + std::to_string(kMaxTopK) + "]");
+  if (!stats_dev || !status_dev || (total_terms > 0 && !df_dev)) CM_FAIL(CM_EINVAL, "NULL argument");
+  if (h->ndocs == 0) CM_FAIL(CM_EINVAL, "empty BM25 index");
+  if (h->log_n < 0) CM_FAIL(CM_EINVAL, "cm_bm25_prepare_filtered was not called for this index");
+  DeviceGuard dg(h->dev);
+  hipStream_t st = (hipStream_t)stream;
+  BmWs w = bm_ws_layout(h, nq, total_terms, k, workspace_dev);
+  if (!workspace_dev || (int64_t)w.total > workspace_bytes) CM_FAIL(CM_EINVAL, "bm25 workspace too small");
+  CM_HIP(hipMemsetAsync(status_dev, 0, 4, st));
+  hipLaunchKernelGGL(bm25_stats_idf_kernel, dim3((unsigned)std::max<int64_t>(1, ceil_div(total_terms, 256))), dim3(256),
+                     0, st, q_terms_dev, total_terms, h->vocab, stats_dev, df_dev, h->logtab.as<double>(), h->log_n,
+                     eps_dev, w.q_idf, w.avgdl, status_dev);
+  CM_HIP(hipGetLastError());
+  return bm25_launch_core(h, q_terms_dev, q_off_dev, nq, total_terms, k, allow_dev, w, score_dev, row_dev, st);
+}
+
+int cm_bm25_search_filtered_dev(cm_bm25 *h, const int32_t *q_terms_dev, const int32_t *q_off_dev, int32_t nq,
+                                int32_t total_terms, int32_t k, const uint32_t *allow_dev, const double *eps_dev,
+                                double *score_dev, int64_t *row_dev, int32_t *status_dev, void *workspace_dev,
+                                int64_t workspace_bytes, void *stream) {
+  if (!h || !allow_dev) CM_FAIL(CM_EINVAL, "NULL argument");
+  if (nq <= 0) return CM_OK;
+  BmWs w = bm_ws_layout(h, nq, total_terms, k, workspace_dev);
+  if (!workspace_dev || (int64_t)w.total > workspace_bytes) CM_FAIL(CM_EINVAL, "bm25 workspace too small");
+  int rc = cm_bm25_filter_stats_dev(h, allow_dev, q_terms_dev, total_terms, w.stats, w.df, stream);
+  if (rc) return rc;
+  return cm_bm25_search_stats_dev(h, q_terms_dev, q_off_dev, nq, total_terms, k, allow_dev, w.stats, w.df, eps_dev,
+                                  score_dev, row_dev, status_dev, workspace_dev, workspace_bytes, stream);
 }
 
 }  // extern "C"

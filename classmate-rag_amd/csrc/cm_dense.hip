@@ -19,6 +19,8 @@
 // per-range lists (sorted) with a tournament.
 #include "cm_common.h"
 
+#include <hipcub/hipcub.hpp>
+
 #include <algorithm>
 #include <mutex>
 #include <vector>
@@ -94,10 +96,16 @@ __global__ void __launch_bounds__(kThreads, 2)
   const DenseLds L = dense_lds_layout(QB, KMAX, ld);
   // qmask (K1c/K1s fallback): only queries with qmask[q] != 0 are searched; a workgroup whose
   // query group has none exits before touching the corpus (block-uniform: no barrier skipped)
-  if (qmask) {
+  if (qmask) {  // (a dynamic-LDS word: __syncthreads_or would add static LDS past the 160 KiB budget)
+    uint32_t *flag = reinterpret_cast<uint32_t *>(lds + L.cnt);
+    if (threadIdx.x == 0) flag[0] = 0u;
+    __syncthreads();
     const int qq = (int)(blockIdx.x / n_cblocks) * QB + (int)threadIdx.x;
-    const int act = (threadIdx.x < QB && qq < nq) ? qmask[qq] : 0;
-    if (!__syncthreads_or(act)) return;
+    if (threadIdx.x < QB && qq < nq && qmask[qq]) flag[0] = 1u;
+    __syncthreads();
+    const uint32_t any = flag[0];
+    __syncthreads();  // every thread has read the word before the init below reuses it
+    if (!any) return;
   }
   f32x4 *qfrag = reinterpret_cast<f32x4 *>(lds + L.qfrag);
   float *invq = reinterpret_cast<float *>(lds + L.invq);
@@ -381,19 +389,28 @@ __device__ inline float coarse_err(const float *qnorm, int qi, const float *row_
 #define K1C_RING 8
 #endif
 constexpr int kRRing = K1C_RING;  // LDS ring slots (8 KB each): kRRing - 1 chunks in flight per CU
+// LDS-resident query chunks of the whole-pass K1c at ld 768 (the rest stay in registers); the ring
+// and these share the 160 KiB: (kRRing + 4 kK1cNql) x 8 KiB
+#ifndef K1C_NQL
+#define K1C_NQL 3
+#endif
+constexpr int kK1cNql = K1C_NQL;
 constexpr int kRRows = 64;      // rows per compute tile / chunk
 constexpr int kCBufCap = 64;    // candidate slots per (range, query)
 
 // Per-tile candidate epilogue shared by K1c and K1s.  acc[rt][qt][r] is the coarse product of
-// row rt*16 + 4g + r of the tile with query qt*16 + j (lane (g, j)); tmask its 64 live & allow
-// bits.  MINONLY: running minimum coarse distance per query.  Otherwise every row with coarse
-// distance <= sd[qt] is appended to the query's buffer dst(qt) (slots by ballot + popcount among
-// the 4 lanes g = 0..3 sharing query j; the count lives in lane j's register, no LDS atomics).
-template <int QT, bool MINONLY, typename Dst>
-__device__ __attribute__((always_inline)) inline void coarse_epilogue(const f32x4 (&acc)[4][QT], uint64_t tmask,
+// row rt*16 + 4g + r of the tile with query qt*16 + j (lane (g, j)); live16 the lane's 16 live &
+// allow bits (bit 4 rt + r).  MINONLY: running minimum coarse distance per query.  Otherwise every
+// row with coarse distance <= sd[qt] is appended to its query's buffer dst0 + qt * 16 * kCBufCap:
+// a per-lane 16-bit hit mask, an exclusive prefix of the hit counts over the 4 lanes (g = 0..3)
+// that share query j, then each lane writes its own hits (usually none); the running count lives
+// in lane j's register (no LDS atomics: those would wait behind the ring's DMAs).  A q-tile with
+// no row under any of its queries' seeds costs one max-reduction and a ballot.
+template <int QT, bool MINONLY>
+__device__ __attribute__((always_inline)) inline void coarse_epilogue(const f32x4 (&acc)[4][QT], uint32_t live16,
                                                                       int64_t row0, const float (&sd)[QT],
                                                                       float (&best)[QT], uint32_t (&qcnt)[QT],
-                                                                      Dst dst) {
+                                                                      uint64_t *dst0) {
   const int lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15;
 #pragma unroll
   for (int qt = 0; qt < QT; ++qt) {
@@ -403,7 +420,7 @@ __device__ __attribute__((always_inline)) inline void coarse_epilogue(const f32x
       for (int rt = 0; rt < 4; ++rt)
 #pragma unroll
         for (int r = 0; r < 4; ++r)
-          if ((tmask >> (rt * 16 + 4 * g + r)) & 1u) m = fminf(m, 1.0f - acc[rt][qt][r]);
+          if ((live16 >> (rt * 4 + r)) & 1u) m = fminf(m, 1.0f - acc[rt][qt][r]);
       best[qt] = fminf(best[qt], m);
     } else {
       float mx = -__builtin_inff();
@@ -412,27 +429,40 @@ __device__ __attribute__((always_inline)) inline void coarse_epilogue(const f32x
 #pragma unroll
         for (int r = 0; r < 4; ++r) mx = fmaxf(mx, acc[rt][qt][r]);
       if (__ballot(1.0f - mx <= sd[qt]) == 0) continue;  // no row of the tile under any seed
-      const uint64_t samej = 0x0001000100010001ull << j;
-      uint64_t *d = dst(qt);
+      uint32_t hm = 0;
 #pragma unroll
-      for (int rt = 0; rt < 4; ++rt) {
-        __builtin_amdgcn_sched_barrier(0);
+      for (int rt = 0; rt < 4; ++rt)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int rr = rt * 16 + 4 * g + r;
-          const float dist = 1.0f - acc[rt][qt][r];
-          const bool pred = ((tmask >> rr) & 1u) && dist <= sd[qt];
-          const uint64_t m = __ballot(pred);
-          if (m == 0) continue;
-          const uint32_t base = __shfl(qcnt[qt], j);
-          const uint32_t slot = base + (uint32_t)__popcll(m & samej & ((1ull << lane) - 1ull));
-          if (pred && slot < (uint32_t)kCBufCap)
-            d[slot] = ((uint64_t)f32_order(dist) << 32) | (uint64_t)(uint32_t)(row0 + rr);
-          if (g == 0) qcnt[qt] += (uint32_t)__popcll(m & samej);
-        }
+        for (int r = 0; r < 4; ++r) hm |= (1.0f - acc[rt][qt][r] <= sd[qt] ? 1u : 0u) << (rt * 4 + r);
+      hm &= live16;
+      const uint32_t cnt = (uint32_t)__popc(hm);
+      uint32_t incl = cnt;  // inclusive scan over g of the lanes j, j + 16, j + 32, j + 48
+      uint32_t t = (uint32_t)__shfl_up((int)incl, 16);
+      if (g >= 1) incl += t;
+      t = (uint32_t)__shfl_up((int)incl, 32);
+      if (g >= 2) incl += t;
+      const uint32_t tot = (uint32_t)__shfl((int)incl, 48 + j);
+      uint32_t slot = (uint32_t)__shfl((int)qcnt[qt], j) + incl - cnt;
+      uint64_t *d = dst0 + (int64_t)qt * 16 * kCBufCap;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {  // static register indices; a wave-uniform skip per position
+        const bool hit = (hm >> i) & 1u;
+        if (__ballot(hit) == 0) continue;
+        if (hit && slot < (uint32_t)kCBufCap)
+          d[slot] = ((uint64_t)f32_order(1.0f - acc[i >> 2][qt][i & 3]) << 32) |
+                    (uint64_t)(uint32_t)(row0 + (i >> 2) * 16 + 4 * g + (i & 3));
+        slot += hit ? 1u : 0u;
       }
+      if (g == 0) qcnt[qt] += tot;
     }
   }
+}
+// The lane's 16 bits of a tile's 64-bit live & allow mask: bit 4 rt + r = tile row rt*16 + 4g + r.
+__device__ inline uint32_t lane_live16(uint64_t tmask, int g) {
+  uint32_t v = 0;
+#pragma unroll
+  for (int rt = 0; rt < 4; ++rt) v |= (uint32_t)((tmask >> (rt * 16 + 4 * g)) & 0xfu) << (rt * 4);
+  return v;
 }
 
 // ---------------------------------------------------------------------------
@@ -449,14 +479,20 @@ __device__ __attribute__((always_inline)) inline void coarse_epilogue(const f32x
 //   main pass: every live+allowed row with coarse distance <= seed[q] is appended to the
 //     (range, query) candidate buffer out_keys[pass][wg][q][kCBufCap];
 //     out_cnt[pass][wg][q] = appended count (> kCBufCap: the buffer overflowed).
-template <int NQL>
+template <int NQL, int RING = kRRing>
 struct K1rLds {
   static constexpr int ring = 0;
-  static constexpr int qf = ring + kRRing * 8192;          // [NQL][W waves][32/W frags][64 lanes] x 16 B
+  static constexpr int qf = ring + RING * 8192;            // [NQL][W waves][32/W frags][64 lanes] x 16 B
   static constexpr int total = qf + NQL * 4 * 8 * 1024;
 };
 
-template <int KC, int NQL, bool MINONLY, int W>
+//   QPASS = 128 (the paired form, K1c2): a workgroup holds half of the pass's queries, all in
+//     registers (no LDS-resident query chunks), so the whole 160 KiB LDS is the DMA ring (20 slots,
+//     >= 18 chunks = 144 KiB in flight per CU, deep enough to cover the loaded HBM latency); the
+//     two workgroups of a (pass, range) are blocks b and b + 8 -- one XCD under round-robin
+//     placement -- so the second reader of every chunk finds it in (or on its way into) that XCD's L2
+//     and the corpus still crosses HBM about once.  Placement is a speed assumption only.
+template <int KC, int NQL, bool MINONLY, int W, int RING = kRRing, int QPASS = kBQPass>
 __global__ void __launch_bounds__(64 * W, 1)
     dense_coarse_scan_kernel(const _Float16 *__restrict__ Xh, const uint32_t *__restrict__ live,
                              const uint32_t *__restrict__ allow, int64_t n_words, const _Float16 *__restrict__ Qh,
@@ -465,24 +501,36 @@ __global__ void __launch_bounds__(64 * W, 1)
                              float *__restrict__ out_min, int dbg) {
   constexpr int ld = 64 * KC;
   constexpr int KR = KC - NQL;  // register-resident query chunks
-  using LL = K1rLds<NQL>;
-  constexpr int QT = 16 / W;        // 16-query tiles per wave
-  constexpr int NF = 2 * QT;        // query fragments per wave and chunk
-  constexpr int PCS = 8 / W;        // 1 KB DMA pieces per wave and chunk
+  using LL = K1rLds<NQL, RING>;
+  constexpr int QT = QPASS / (16 * W);  // 16-query tiles per wave
+  constexpr int NF = 2 * QT;            // query fragments per wave and chunk
+  constexpr int PCS = 8 / W;            // 1 KB DMA pieces per wave and chunk
+  constexpr int H = kBQPass / QPASS;    // workgroups per (pass, range)
+#ifndef CM_ABLATION
+  dbg = 0;  // product build: the ablation branches fold away (exact lgkmcnt / vmcnt counting)
+#endif
   static_assert(W == 4 || W == 8, "K1c: 4 or 8 waves");
+  static_assert(H == 1 || H == 2, "K1c: full or half passes");
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4;
   const int j = lane & 15;
-  const int wg = blockIdx.x % n_wg;
-  const int qp = blockIdx.x / n_wg;
+  int lr = blockIdx.x, half = 0;  // linear (pass, range) index and query half
+  if (H == 2) {                   // blocks b, b + 8 -> same (pass, range), halves 0 / 1
+    const int grp = blockIdx.x >> 3;
+    half = grp & 1;
+    lr = (grp >> 1) * 8 + (blockIdx.x & 7);
+  }
+  const int wg = lr % n_wg;
+  const int qp = lr / n_wg;
+  if (H == 2 && qp * kBQPass >= nq) return;  // grid padding of the paired mapping (whole workgroup)
   const int64_t r_begin = (int64_t)wg * rows_per_wg;
   const int64_t r_end = min(r_begin + rows_per_wg, rows_end);
   const int ntiles = r_begin < r_end ? (int)((r_end - r_begin) / kRRows) : 0;
   const int total = ntiles * KC;
-  const int qc0 = wave * 16 * QT;
+  const int qc0 = half * QPASS + wave * 16 * QT;  // wave's first query within the pass
   const int qg0 = qp * kBQPass + qc0;
 
   // resident query fragments (B operand): lane (g, j) of q-tile qt, chunk c, half sb holds
@@ -523,7 +571,7 @@ __global__ void __launch_bounds__(64 * W, 1)
     const int gl = min(gc, total - 1);  // clamped: one control path past the end
     const int t = gl / KC, c = gl - t * KC;
     const int64_t tile = (r_begin >> 6) + t;
-    unsigned char *slot = lds + LL::ring + (gc % kRRing) * 8192;
+    unsigned char *slot = lds + LL::ring + (gc % RING) * 8192;
 #pragma unroll
     for (int i = 0; i < PCS; ++i) {
       const int o = W * i + wave;
@@ -545,10 +593,8 @@ __global__ void __launch_bounds__(64 * W, 1)
     // tile's chunks instead of a scalar load waited for here)
     const uint32_t b0 = (uint32_t)__builtin_amdgcn_readlane((int)tile_words, 0);
     const uint32_t b1 = (uint32_t)__builtin_amdgcn_readlane((int)tile_words, 1);
-    const uint64_t tmask = ((uint64_t)b1 << 32) | b0;
-    coarse_epilogue<QT, MINONLY>(acc, tmask, row0, sd, best, qcnt, [&](int qt) {
-      return out_keys + (((int64_t)qp * n_wg + wg) * kBQPass + qc0 + qt * 16 + j) * kCBufCap;
-    });
+    coarse_epilogue<QT, MINONLY>(acc, lane_live16(((uint64_t)b1 << 32) | b0, g), row0, sd, best, qcnt,
+                                 out_keys + (((int64_t)qp * n_wg + wg) * kBQPass + qc0 + j) * kCBufCap);
 #pragma unroll
     for (int rt = 0; rt < 4; ++rt)
 #pragma unroll
@@ -559,18 +605,18 @@ __global__ void __launch_bounds__(64 * W, 1)
     // Software-pipelined chunk loop.  Chunk gc's 32 MFMAs run in two halves (row tiles 0-1,
     // 2-3); between them the wave waits for chunk gc+1's DMA pieces, the barrier publishes
     // chunk gc+1 and retires every read of chunk gc's slot (each wave drains its LDS reads
-    // first), chunk gc + kRRing is issued into that slot and the row fragments 0-1 of chunk gc+1
+    // first), chunk gc + RING is issued into that slot and the row fragments 0-1 of chunk gc+1
     // are read into the registers half 1 has just consumed; fragments 2-3 follow half 2.  Every
     // barrier, DMA issue and LDS read thus sits behind >= 16 MFMAs instead of in front of them.
     auto frag = [&](int gc, int rt, int sb) -> f16x8 {
-      const unsigned char *slot = lds + LL::ring + (gc % kRRing) * 8192;
+      const unsigned char *slot = lds + LL::ring + (gc % RING) * 8192;
       return *reinterpret_cast<const f16x8 *>(slot + (rt * 2 + sb) * 1024 + lane * 16);
     };
 #pragma unroll
-    for (int p = 0; p < kRRing - 1; ++p) issue(p);
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PCS * (kRRing - 2)) : "memory");
+    for (int p = 0; p < RING - 1; ++p) issue(p);
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PCS * (RING - 2)) : "memory");
     __builtin_amdgcn_s_barrier();
-    issue(kRRing - 1);
+    issue(RING - 1);
     f16x8 xf[4][2];
 #pragma unroll
     for (int rt = 0; rt < 4; ++rt) {
@@ -606,11 +652,11 @@ __global__ void __launch_bounds__(64 * W, 1)
             acc[rt][qt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xf[rt][1], qv(qt, 1), acc[rt][qt], 0, 0, 0);
         }
         __builtin_amdgcn_sched_barrier(0);
-        // chunk gc+1 landed (this wave's pieces: the PCS (kRRing - 2) younger DMAs may stay in
+        // chunk gc+1 landed (this wave's pieces: the PCS (RING - 2) younger DMAs may stay in
         // flight); own LDS reads of slot gc done; the barrier makes both true for every wave
-        asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(PCS * (kRRing - 2)) : "memory");
+        asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(PCS * (RING - 2)) : "memory");
         if (!(dbg & 512)) __builtin_amdgcn_s_barrier();  // bit 9: ablation only (races)
-        if (!(dbg & 1024)) issue(gc + kRRing);             // bit 10: ablation only (stale data)
+        if (!(dbg & 1024)) issue(gc + RING);             // bit 10: ablation only (stale data)
 #pragma unroll
         for (int rt = 0; rt < ((dbg & 2048) ? 0 : 2); ++rt) {  // bit 11: ablation only (stale fragments)
           xf[rt][0] = frag(gc + 1, rt, 0);
@@ -752,9 +798,8 @@ __global__ void __launch_bounds__(256, 1)
       const int64_t row0 = r_begin + (int64_t)t * kRRows;
       const uint32_t b0 = (uint32_t)__builtin_amdgcn_readlane((int)tile_words, 0);
       const uint32_t b1 = (uint32_t)__builtin_amdgcn_readlane((int)tile_words, 1);
-      coarse_epilogue<QT, MINONLY>(acc, ((uint64_t)b1 << 32) | b0, row0, sd, best, qcnt, [&](int qt) {
-        return out_keys + ((int64_t)vg * qs + qt * 16 + j) * kCBufCap;
-      });
+      coarse_epilogue<QT, MINONLY>(acc, lane_live16(((uint64_t)b1 << 32) | b0, g), row0, sd, best, qcnt,
+                                   out_keys + ((int64_t)vg * qs + j) * kCBufCap);
 #pragma unroll
       for (int rt = 0; rt < 4; ++rt)
 #pragma unroll
@@ -1108,6 +1153,42 @@ __global__ void dense_gather_kernel(const float *__restrict__ C, int ld, int dim
   for (int c = threadIdx.x; c < dim; c += blockDim.x) o[c] = (r >= 0 && r < size) ? C[r * ld + c] : 0.f;
 }
 
+// k > kMaxTopK (a Chroma n_results beyond the fused top-k lists, vector_chroma.py:225-229): the
+// exact distance of every live + allowed row to one query, with the re-rank kernel's formula
+// d = 1 - (c.q) / ((||c|| + 1e-30)(||q|| + 1e-30)) in fp64, as a sortable (f32 distance, row) key
+// (~0 for rows that cannot be returned).  One wave per 4 rows, lanes across the dims (coalesced
+// 1 KB per load instruction), fp64 butterfly reduction.
+__global__ void __launch_bounds__(256) dense_all_keys_kernel(const float *__restrict__ C, int ld,
+                                                             const uint32_t *__restrict__ live,
+                                                             const uint32_t *__restrict__ allow, int64_t size,
+                                                             const float *__restrict__ qp, double qnorm,
+                                                             uint64_t *__restrict__ keys) {
+  const int lane = threadIdx.x & 63;
+  const int64_t r0 = (((int64_t)blockIdx.x * 4) + (threadIdx.x >> 6)) * 4;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int64_t r = r0 + u;
+    if (r >= size) return;  // wave-uniform
+    const float *cr = C + r * ld;
+    double dq = 0.0, dc = 0.0;
+    for (int c = lane * 4; c < ld; c += 256) {
+      const float4 x = *reinterpret_cast<const float4 *>(cr + c);
+      const float4 y = *reinterpret_cast<const float4 *>(qp + c);
+      dq += (double)x.x * y.x + (double)x.y * y.y + (double)x.z * y.z + (double)x.w * y.w;
+      dc += (double)x.x * x.x + (double)x.y * x.y + (double)x.z * x.z + (double)x.w * x.w;
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+      dq += __shfl_xor(dq, o);
+      dc += __shfl_xor(dc, o);
+    }
+    if (lane == 0) {
+      const uint32_t w = live[r >> 5] & (allow ? allow[r >> 5] : 0xffffffffu);
+      const float dist = (float)(1.0 - dq / ((sqrt(dc) + 1e-30) * (qnorm + 1e-30)));
+      keys[r] = ((w >> (r & 31)) & 1u) ? (((uint64_t)f32_order(dist) << 32) | (uint64_t)(uint32_t)r) : kEmptyKey;
+    }
+  }
+}
+
 __global__ void popcount_kernel(const uint32_t *__restrict__ bits, int64_t n_words,
                                 unsigned long long *__restrict__ out) {
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1321,18 +1402,37 @@ int dense_kind(const cm_dense *h, int nq, int k) {
 // Coarse-scan geometry.  K1c: a pass of kBQPass queries per workgroup, one workgroup per CU and
 // pass; K1s: one pass of kSQ queries, n_wg = "virtual groups" = waves (4 per CU).  The sample
 // pre-pass runs the same kernel over a prefix of 1/64 of the rows (1/16 below 1M rows).
+// K1c form: whole passes (QPASS 256, LDS ring + LDS-resident query chunks; default) or paired
+// half passes (QPASS 128, 20-slot ring, CM_K1C_PAIRED=1).  Measured at 10M x 768, B = 256:
+// 4.5 vs 6.0 ms -- the ring depth is not what limits the scan (4 slots run as fast as 8).
+bool k1c_paired() {
+  static const bool p = [] {
+    const char *e = getenv("CM_K1C_PAIRED");
+    return e && e[0] == '1';
+  }();
+  return p;
+}
+
 struct CoarseCfg {
-  bool stream;
+  bool stream, paired;
   int qs, n_pass, n_wg, n_wg_sample;
   int64_t rows_per_wg, rows_end, rows_per_wg_sample, rows_end_sample;
+  // blocks of a K1c launch over n_wg ranges: the paired form maps blocks b, b + 8 to one (pass,
+  // range) and pads the grid to whole groups of 16
+  unsigned grid(int ranges) const {
+    const int64_t m = (int64_t)n_pass * ranges;
+    return (unsigned)(paired ? round_up(2 * m, 16) : m);
+  }
 };
 CoarseCfg coarse_config(const cm_dense *h, int nq, bool stream) {
   CoarseCfg c{};
   c.stream = stream;
+  c.paired = !stream && k1c_paired();
   c.qs = stream ? kSQ : kBQPass;
   c.n_pass = stream ? 1 : (int)ceil_div(nq, kBQPass);
   c.rows_end = round_up(std::max<int64_t>(h->size, 1), kStepRows);
-  const int64_t groups = stream ? (int64_t)num_cus(h->dev) * 4 : std::max(1, num_cus(h->dev) / c.n_pass);
+  int64_t groups = stream ? (int64_t)num_cus(h->dev) * 4 : std::max(1, num_cus(h->dev) / c.n_pass);
+  if (c.paired) groups = std::max<int64_t>(1, groups / 2);
   auto split = [&](int64_t rows_end, int64_t &per, int &n) {
     const int64_t tiles = rows_end / kRRows;
     per = ceil_div(tiles, std::min<int64_t>(groups, tiles)) * kRRows;
@@ -1387,10 +1487,14 @@ int set_coarse_attrs() {
   static hipError_t err = hipSuccess;
   std::call_once(once, [] {
     const std::pair<const void *, int> fs[] = {
-        {reinterpret_cast<const void *>(&dense_coarse_scan_kernel<12, 3, false, kK1cWaves>), K1rLds<3>::total},
-        {reinterpret_cast<const void *>(&dense_coarse_scan_kernel<12, 3, true, kK1cWaves>), K1rLds<3>::total},
+        {reinterpret_cast<const void *>(&dense_coarse_scan_kernel<12, kK1cNql, false, kK1cWaves>), K1rLds<kK1cNql>::total},
+        {reinterpret_cast<const void *>(&dense_coarse_scan_kernel<12, kK1cNql, true, kK1cWaves>), K1rLds<kK1cNql>::total},
         {reinterpret_cast<const void *>(&dense_coarse_scan_kernel<6, 0, false, kK1cWaves>), K1rLds<0>::total},
         {reinterpret_cast<const void *>(&dense_coarse_scan_kernel<6, 0, true, kK1cWaves>), K1rLds<0>::total},
+        {reinterpret_cast<const void *>(&dense_coarse_scan_kernel<12, 0, false, 4, 20, 128>), K1rLds<0, 20>::total},
+        {reinterpret_cast<const void *>(&dense_coarse_scan_kernel<12, 0, true, 4, 20, 128>), K1rLds<0, 20>::total},
+        {reinterpret_cast<const void *>(&dense_coarse_scan_kernel<6, 0, false, 4, 20, 128>), K1rLds<0, 20>::total},
+        {reinterpret_cast<const void *>(&dense_coarse_scan_kernel<6, 0, true, 4, 20, 128>), K1rLds<0, 20>::total},
         {reinterpret_cast<const void *>(&dense_rerank_kernel), kGatherCap * 12}};
     for (const auto &f : fs) {
       const hipError_t e = hipFuncSetAttribute(f.first, hipFuncAttributeMaxDynamicSharedMemorySize, f.second);
@@ -1428,9 +1532,17 @@ int launch_coarse(cm_dense *h, const float *q_dev, int nq, int k, bool stream, c
   CM_HIP(hipGetLastError());
   CM_HIP(hipMemsetAsync(w.fb_count, 0, 4, st));
   const bool d768 = h->ld == 768;
-  const size_t slds = d768 ? K1rLds<3>::total : K1rLds<0>::total;
+  const size_t slds = c.paired ? K1rLds<0, 20>::total : d768 ? K1rLds<kK1cNql>::total : K1rLds<0>::total;
+  const int k1c_threads = c.paired ? 256 : 64 * kK1cWaves;
   auto k1c = [&](bool minonly) {
-    if (d768) return minonly ? &dense_coarse_scan_kernel<12, 3, true, kK1cWaves> : &dense_coarse_scan_kernel<12, 3, false, kK1cWaves>;
+    if (c.paired) {
+      if (d768)
+        return minonly ? &dense_coarse_scan_kernel<12, 0, true, 4, 20, 128>
+                       : &dense_coarse_scan_kernel<12, 0, false, 4, 20, 128>;
+      return minonly ? &dense_coarse_scan_kernel<6, 0, true, 4, 20, 128>
+                     : &dense_coarse_scan_kernel<6, 0, false, 4, 20, 128>;
+    }
+    if (d768) return minonly ? &dense_coarse_scan_kernel<12, kK1cNql, true, kK1cWaves> : &dense_coarse_scan_kernel<12, kK1cNql, false, kK1cWaves>;
     return minonly ? &dense_coarse_scan_kernel<6, 0, true, kK1cWaves> : &dense_coarse_scan_kernel<6, 0, false, kK1cWaves>;
   };
   // 1. sample pre-pass (per-group minima) -> seed
@@ -1439,7 +1551,7 @@ int launch_coarse(cm_dense *h, const float *q_dev, int nq, int k, bool stream, c
                        h->Xh, h->live, allow, n_words, w.qh, nq, (const float *)nullptr, c.rows_per_wg_sample,
                        c.rows_end_sample, c.n_wg_sample, c.qs, (uint64_t *)nullptr, (uint32_t *)nullptr, w.mins);
   } else {
-    hipLaunchKernelGGL(k1c(true), dim3(c.n_wg_sample * c.n_pass), dim3(64 * kK1cWaves), slds, st, h->Xh, h->live,
+    hipLaunchKernelGGL(k1c(true), dim3(c.grid(c.n_wg_sample)), dim3(k1c_threads), slds, st, h->Xh, h->live,
                        allow, n_words, w.qh, nq, (const float *)nullptr, c.rows_per_wg_sample, c.rows_end_sample,
                        c.n_wg_sample, (uint64_t *)nullptr, (uint32_t *)nullptr, w.mins, 0);
   }
@@ -1454,7 +1566,7 @@ int launch_coarse(cm_dense *h, const float *q_dev, int nq, int k, bool stream, c
                        h->live, allow, n_words, w.qh, nq, (const float *)w.seed, c.rows_per_wg, c.rows_end, c.n_wg,
                        c.qs, w.keys, w.cnt, (float *)nullptr);
   } else {
-    hipLaunchKernelGGL(k1c(false), dim3(c.n_wg * c.n_pass), dim3(64 * kK1cWaves), slds, st, h->Xh, h->live, allow,
+    hipLaunchKernelGGL(k1c(false), dim3(c.grid(c.n_wg)), dim3(k1c_threads), slds, st, h->Xh, h->live, allow,
                        n_words, w.qh, nq, (const float *)w.seed, c.rows_per_wg, c.rows_end, c.n_wg, w.keys, w.cnt,
                        (float *)nullptr, dense_debug_flags());
   }
@@ -1474,6 +1586,65 @@ int launch_coarse(cm_dense *h, const float *q_dev, int nq, int k, bool stream, c
   hipLaunchKernelGGL(dense_merge_kernel, dim3(nq), dim3(256), 0, st, w.k1.cand, kc.n_cblocks, kc.QB, k, nq,
                      (const int32_t *)w.fb_mask, dist_dev, row_dev);
   CM_HIP(hipGetLastError());
+  return CM_OK;
+}
+
+// Host-array search with k > kMaxTopK: every row's exact key, one device radix sort per query, the
+// first k keys (ascending (distance, row), -1 padding past the live + allowed rows).
+int dense_search_full(cm_dense *h, const float *q, int nq, int k, const uint32_t *allow_bits, float *out_dist,
+                      int64_t *out_row, float *out_vec) {
+  const int64_t n = std::max<int64_t>(h->size, 1);
+  int rc;
+  size_t tmp_bytes = 0;
+  CM_HIP(hipcub::DeviceRadixSort::SortKeys(nullptr, tmp_bytes, (const uint64_t *)nullptr, (uint64_t *)nullptr,
+                                           (int)n, 0, 64, h->stream));
+  const size_t keys_off = round_up((int64_t)tmp_bytes, 256);
+  const size_t q_off = keys_off + round_up(n * 16, 256);
+  if ((rc = h->ws.ensure(q_off + (size_t)h->ld * 4))) return rc;
+  char *base = h->ws.as<char>();
+  uint64_t *keys = reinterpret_cast<uint64_t *>(base + keys_off), *sorted = keys + n;
+  float *qp = reinterpret_cast<float *>(base + q_off);
+  const uint32_t *allow_dev = nullptr;
+  const int64_t nw = ceil_div(h->size, 32);
+  if (allow_bits) {
+    if ((rc = h->allow_buf.ensure((size_t)std::max<int64_t>(nw, 1) * 4))) return rc;
+    CM_HIP(hipMemcpyAsync(h->allow_buf.ptr, allow_bits, (size_t)nw * 4, hipMemcpyDefault, h->stream));
+    allow_dev = h->allow_buf.as<uint32_t>();
+  }
+  CM_HIP(hipMemsetAsync(keys, 0xff, (size_t)n * 8, h->stream));  // rows past size (empty store) sort last
+  const int kk = (int)std::min<int64_t>(k, n);
+  std::vector<uint64_t> top((size_t)kk);
+  std::vector<float> qpad((size_t)h->ld, 0.f);
+  for (int i = 0; i < nq; ++i) {
+    double qn = 0.0;
+    for (int c = 0; c < h->dim; ++c) {
+      qpad[c] = q[(int64_t)i * h->dim + c];
+      qn += (double)qpad[c] * qpad[c];
+    }
+    CM_HIP(hipMemcpyAsync(qp, qpad.data(), (size_t)h->ld * 4, hipMemcpyHostToDevice, h->stream));
+    hipLaunchKernelGGL(dense_all_keys_kernel, dim3((unsigned)ceil_div(n, 16)), dim3(256), 0, h->stream, h->C, h->ld,
+                       h->live, allow_dev, h->size, qp, std::sqrt(qn), keys);
+    CM_HIP(hipGetLastError());
+    CM_HIP(hipcub::DeviceRadixSort::SortKeys(base, tmp_bytes, keys, sorted, (int)n, 0, 64, h->stream));
+    CM_HIP(hipMemcpyAsync(top.data(), sorted, (size_t)kk * 8, hipMemcpyDeviceToHost, h->stream));
+    CM_HIP(hipStreamSynchronize(h->stream));
+    for (int j = 0; j < k; ++j) {
+      const uint64_t key = j < kk ? top[j] : kEmptyKey;
+      out_dist[(int64_t)i * k + j] = key == kEmptyKey ? 0.f : f32_unorder((uint32_t)(key >> 32));
+      out_row[(int64_t)i * k + j] = key == kEmptyKey ? -1 : (int64_t)(uint32_t)key;
+    }
+  }
+  if (out_vec) {  // stored fp32 rows of the results (include_embeddings)
+    const size_t nr = (size_t)nq * k;
+    if ((rc = h->rows_buf.ensure(nr * 8)) || (rc = h->out_buf.ensure(nr * h->dim * 4))) return rc;
+    CM_HIP(hipMemcpyAsync(h->rows_buf.ptr, out_row, nr * 8, hipMemcpyHostToDevice, h->stream));
+    hipLaunchKernelGGL(dense_gather_kernel, dim3((unsigned)nr), dim3(256), 0, h->stream, h->C, h->ld, h->dim,
+                       h->rows_buf.as<int64_t>(), (int64_t)nr, h->size, h->out_buf.as<float>());
+    CM_HIP(hipGetLastError());
+    CM_HIP(hipMemcpyAsync(out_vec, h->out_buf.ptr, nr * h->dim * 4, hipMemcpyDeviceToHost, h->stream));
+    CM_HIP(hipStreamSynchronize(h->stream));
+  }
+  h->last_fallbacks = 0;
   return CM_OK;
 }
 
@@ -1757,8 +1928,9 @@ int cm_dense_search(cm_dense *h, const float *q, int32_t nq, int32_t k, const ui
   if (!h) CM_FAIL(CM_EINVAL, "null handle");
   if (nq <= 0) return CM_OK;
   if (!q || !out_dist || !out_row) CM_FAIL(CM_EINVAL, "NULL argument");
-  if (k <= 0 || k > kMaxTopK) CM_FAIL(CM_EINVAL, "k must be in [1, " + std::to_string(kMaxTopK) + "]");
+  if (k <= 0) CM_FAIL(CM_EINVAL, "k must be >= 1");
   DeviceGuard dg(h->dev);
+  if (k > kMaxTopK) return dense_search_full(h, q, nq, k, allow_bits, out_dist, out_row, out_vec);
   const int64_t wsb = cm_dense_search_workspace(h, nq, k);
   int rc;
   if ((rc = h->ws.ensure((size_t)wsb))) return rc;
@@ -1799,3 +1971,4 @@ int cm_dense_search(cm_dense *h, const float *q, int32_t nq, int32_t k, const ui
 }
 
 }  // extern "C"
+

@@ -49,7 +49,8 @@ extern "C" {
 const char *cm_last_error(void);
 int cm_version(void);
 int cm_device_count(int *n);
-/* largest k the fused top-k kernels accept (dense and BM25). */
+/* largest k the fused top-k kernels accept (dense and BM25 _dev entries); the
+ * host-array searches accept any k >= 1 (beyond it: full order + device sort). */
 int cm_max_topk(void);
 
 /* Dense cosine k-NN ---------------------------------------------------
@@ -199,6 +200,44 @@ int64_t cm_bm25_search_workspace(cm_bm25 *h, int32_t nq, int32_t total_terms, in
 int cm_bm25_search_dev(cm_bm25 *h, const int32_t *q_terms_dev, const int32_t *q_off_dev, int32_t nq,
                        int32_t total_terms, int32_t k, double *score_dev, int64_t *row_dev,
                        void *workspace_dev, int64_t workspace_bytes, void *stream);
+
+/* Filtered search on the device (quirk Q2: rank_bm25 statistics over the
+ * candidate set, rag/retrieval/bm25.py:184-191), graph-capturable.
+ *   cm_bm25_prepare_filtered: host call, once per index (before capture):
+ *     uploads L[x] = log(x + 0.5) for x <= max(max_docs, num_docs) (glibc,
+ *     CPython's math.log), so the device forms idf = L[Nc - df] - L[df] with
+ *     rank_bm25's exact bits.  max_docs = the global corpus size on a shard.
+ *   cm_bm25_filter_stats_dev: stats_dev = {Nc, sum of candidate lengths}
+ *     (int64[2]), df_dev[i] = candidate df of q_terms_dev[i] (int64).  A
+ *     sharded index all-reduces (sums) both before searching.
+ *   cm_bm25_filter_term_stats_dev: the same for every term (df int64[V]) plus
+ *     each term's first candidate (row << 32 | position) key (uint64[V],
+ *     ~0 = none): a shard's share of the epsilon floor's statistics.
+ *   cm_bm25_filter_eps: host call; rank_bm25's epsilon (0.25 x the mean idf
+ *     of the candidate vocabulary in first-occurrence order) for one filter;
+ *     allow_bits host or device words.
+ *   cm_bm25_search_stats_dev: cm_bm25_search_dev over the allowed documents
+ *     with the given candidate statistics; eps_dev (nullable) is the epsilon
+ *     used when an idf is negative.  status_dev (int32, written on stream):
+ *     bit 0 an idf was negative and eps_dev was NULL/NaN (compute eps with
+ *     cm_bm25_filter_eps and search again), bit 1 candidates without tokens
+ *     (the reference's ZeroDivisionError), bit 2 Nc beyond the prepared table.
+ *   cm_bm25_search_filtered_dev: filter_stats_dev + search_stats_dev on one
+ *     index (workspace: cm_bm25_search_workspace).                          */
+int cm_bm25_prepare_filtered(cm_bm25 *h, int64_t max_docs);
+int cm_bm25_filter_stats_dev(cm_bm25 *h, const uint32_t *allow_dev, const int32_t *q_terms_dev, int32_t n_terms,
+                             int64_t *stats_dev, int64_t *df_dev, void *stream);
+int cm_bm25_filter_term_stats_dev(cm_bm25 *h, const uint32_t *allow_dev, int64_t *df_dev, uint64_t *first_dev,
+                                  void *stream);
+int cm_bm25_filter_eps(cm_bm25 *h, const uint32_t *allow_bits, double *eps_out);
+int cm_bm25_search_stats_dev(cm_bm25 *h, const int32_t *q_terms_dev, const int32_t *q_off_dev, int32_t nq,
+                             int32_t total_terms, int32_t k, const uint32_t *allow_dev, const int64_t *stats_dev,
+                             const int64_t *df_dev, const double *eps_dev, double *score_dev, int64_t *row_dev,
+                             int32_t *status_dev, void *workspace_dev, int64_t workspace_bytes, void *stream);
+int cm_bm25_search_filtered_dev(cm_bm25 *h, const int32_t *q_terms_dev, const int32_t *q_off_dev, int32_t nq,
+                                int32_t total_terms, int32_t k, const uint32_t *allow_dev, const double *eps_dev,
+                                double *score_dev, int64_t *row_dev, int32_t *status_dev, void *workspace_dev,
+                                int64_t workspace_bytes, void *stream);
 
 /* Where-filters on the device ---------------------------
  * A where clause compiled on the host (classmate_hip/retrieval/filters.py,

@@ -274,3 +274,35 @@ def test_vector_store_save_after_trailing_deletes(corpus, tmp_path):
     assert GpuVectorStore(persist_dir=tmp_path).count() == 0
     fourth.upsert(ids=["new"], documents=["x"], metadatas=[{}], embeddings=emb[:1])
     assert [r["id"] for r in GpuVectorStore(persist_dir=tmp_path).query(query_embeddings=emb[0], top_k=3)] == ["new"]
+
+
+@pytest.mark.parametrize("top_k", [300, 999, 5000, -7])
+def test_top_k_beyond_fused_lists(stores, corpus, top_k):
+    """top_k above cm_max_topk() (256): the reference sorts every candidate (bm25.py:199) and passes
+    any n_results to Chroma (vector_chroma.py:225-229); the device full-order path returns the
+    same lists (BM25 bit-exact incl. zero-score padding; dense within 1e-4, exact-oracle order)."""
+    from oracle import ref_semantics as orc
+    vs, bm, _ = stores
+    obm = orc.BM25Oracle()
+    obm.upsert_many(corpus["ids"], corpus["texts"], corpus["metas"])
+    for q in corpus["qtexts"][:3]:
+        got = [[r["id"], r["score"]] for r in bm.search(query=q, top_k=top_k)]
+        want = [[w["id"], w["score"]] for w in obm.search(q, None, top_k=top_k)]
+        assert got == want
+    got = [[r["id"], r["score"]] for r in bm.search(query=corpus["qtexts"][0], where=FILTERS["course_only"],
+                                                     top_k=top_k)]
+    assert got == [[w["id"], w["score"]] for w in obm.search(corpus["qtexts"][0], FILTERS["course_only"],
+                                                             top_k=top_k)]
+    if top_k > 0:
+        ovs = orc.ExactVectorStore(corpus["ids"], corpus["texts"], corpus["metas"], corpus["emb"])
+        for qv in corpus["qvecs"][:3]:
+            got = vs.query(query_embeddings=qv, top_k=top_k, include_embeddings=True)
+            want = ovs.query(query_embeddings=qv, top_k=top_k)
+            assert len(got) == len(want) == min(top_k, len(corpus["ids"]))
+            np.testing.assert_allclose([r["distance"] for r in got], [w["distance"] for w in want], atol=TOL)
+            gd = np.array([w["distance"] for w in want])
+            for j, (g, w) in enumerate(zip(got, want)):   # order exact wherever the oracle separates it
+                if (j == 0 or gd[j] - gd[j - 1] > 1e-5) and (j == len(gd) - 1 or gd[j + 1] - gd[j] > 1e-5):
+                    assert g["id"] == w["id"]
+            idx = {i: n for n, i in enumerate(corpus["ids"])}
+            assert all(np.array_equal(r["embedding"], corpus["emb"][idx[r["id"]]]) for r in got[:50])

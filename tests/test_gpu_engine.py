@@ -151,11 +151,14 @@ def test_dense_coarse_certificate(eng, path):
     dist, rows = idx.search(q, 24)
     _check_dense(dist, rows, emb, q, 24)
     assert idx.last_fallbacks() == 0
-    # 600 near-duplicates of one vector (cosine gaps ~1e-8, far inside the 2E band)
+    # near-duplicates of one vector (cosine gaps ~1e-8, far inside the 2E band): 600 overflow
+    # K1c's 64-slot (range, query) buffers; K1s's 1024 small groups hold them, so it gets a
+    # cluster wider than the re-rank band cap (1024 rows) instead
+    nd = 600 if path == 3 else 1500
     base = rng.standard_normal(dim).astype(np.float32)
-    dup = base + 1e-4 * rng.standard_normal((600, dim)).astype(np.float32)
+    dup = base + 1e-4 * rng.standard_normal((nd, dim)).astype(np.float32)
     emb2 = np.concatenate([emb, dup])
-    idx.upsert(dup, np.arange(n, n + 600))
+    idx.upsert(dup, np.arange(n, n + nd))
     q2 = np.concatenate([q[:8], base + 0.01 * rng.standard_normal((8, dim)).astype(np.float32)])
     dist, rows = idx.search(q2, 24)
     _check_dense(dist, rows, emb2, q2, 24)
@@ -581,3 +584,63 @@ def test_rrf_merge_lds_and_global_paths_agree(eng):
     for a, b in zip(small, large):
         assert np.array_equal(np.asarray(a), np.asarray(b))
     assert int(np.asarray(small[-1]).max()) > 0
+
+
+def _dev_queries(qs):
+    import torch
+    off = np.zeros(len(qs) + 1, np.int32)
+    off[1:] = np.cumsum([len(q) for q in qs])
+    flat = np.concatenate([np.asarray(q, np.int32) for q in qs]) if off[-1] else np.zeros(1, np.int32)
+    return torch.from_numpy(flat).cuda(), torch.from_numpy(off).cuda()
+
+
+@pytest.mark.parametrize("path", BM25_PATHS)
+def test_bm25_filtered_device_entry_matches_host(eng, path):
+    """cm_bm25_search_filtered_dev (candidate statistics, idf from the glibc log table, epsilon
+    recovery) == the host-array filtered search == the oracle over the filtered subset, bit for
+    bit; includes filters whose candidates make a query term's idf negative (epsilon floor)."""
+    import torch
+    rng = np.random.default_rng(3)
+    words = [f"w{chr(97 + i)}{chr(97 + j)}" for i in range(20) for j in range(20)]
+    texts = []
+    for d in range(3000):
+        n = int(rng.integers(0, 30))
+        ws = [words[int(x)] for x in rng.integers(0, len(words), n)]
+        if rng.random() < 0.8:
+            ws.append("common")
+        texts.append(" ".join(ws))
+    toks = [orc.tokenize(t, "en") for t in texts]
+    b, vocab = _build_bm25(eng, toks, path)
+    b.prepare_filtered()
+    ids = [f"d{i}" for i in range(len(texts))]
+    queries = ["common", "common common wbc", "wbc wbc wbc", "zzzz", "wab wcd common wab", "wab"]
+    qs = [[vocab.get(t, -1) for t in orc.tokenize(q, "en")] for q in queries]
+    qt, qo = _dev_queries(qs)
+    masks = {"first40": np.arange(len(texts)) < 40, "every3": np.arange(len(texts)) % 3 == 0,
+             "all": np.ones(len(texts), bool), "none": np.zeros(len(texts), bool)}
+    for name, mask in masks.items():
+        words_ = _bits(mask)
+        allow = torch.from_numpy(words_.view(np.int32)).cuda()
+        for k in (1, 12, 64):
+            s_h, r_h, n_h = b.search(qs, k, words_)
+            s_d, r_d = b.search_filtered(qt, qo, k, allow)
+            s_d, r_d = s_d.cpu().numpy(), r_d.cpu().numpy()
+            for i in range(len(qs)):
+                n = int(n_h[i])
+                assert r_d[i][:n].tolist() == r_h[i][:n].tolist(), (name, k, i)
+                assert s_d[i][:n].tolist() == s_h[i][:n].tolist(), (name, k, i)
+                assert (r_d[i][n:] == -1).all()
+        sub = [i for i in range(len(texts)) if mask[i]]
+        if sub:
+            ora = orc.BM25Oracle()
+            ora.upsert_many([ids[i] for i in sub], [texts[i] for i in sub], [{"language": "en"}] * len(sub))
+            s_d, r_d = b.search_filtered(qt, qo, 12, allow)
+            for i, q in enumerate(queries):
+                want = ora.search(q, None, top_k=12)
+                got = [[ids[r], s] for r, s in zip(r_d[i].tolist(), s_d[i].tolist()) if r >= 0]
+                assert got == [[w["id"], w["score"]] for w in want], (name, q)
+    # the status word reports the missing epsilon instead of guessing it
+    mask = np.arange(len(texts)) < 40
+    allow = torch.from_numpy(_bits(mask).view(np.int32)).cuda()
+    _, _, st = b.search_filtered_dev(qt, qo, 10, allow)
+    assert int(st.item()) & b.FILT_EPS_MISSING

@@ -33,6 +33,13 @@ def _dense_data(nd):
     return emb, q
 
 
+def _filter_mask(nd):
+    """Every third document plus a dense prefix: the candidates of term 0 exceed half of them
+    (negative idf -> the epsilon floor's global exchange)."""
+    r = np.arange(nd)
+    return (r % 3 == 0) | (r < 150)
+
+
 def _worker(rank, port, out_q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(WS))
     dist.init_process_group("gloo", rank=rank, world_size=WS)
@@ -57,6 +64,20 @@ def _worker(rank, port, out_q):
             rg = np.where(rw >= 0, rw + row0, rw)
             S, R = P.merge_bm25_topk(torch.from_numpy(sc), torch.from_numpy(rg), k)
             res[f"bm25_{k}"] = (S.numpy(), R.numpy())
+        # filtered (quirk Q2): candidate statistics all-reduced, device idf, all-gather merge
+        mask = _filter_mask(nd)[row0:row0 + n]
+        words = np.zeros((n + 31) // 32, np.uint32)
+        idx = np.nonzero(mask)[0]
+        np.bitwise_or.at(words, idx >> 5, (np.uint32(1) << (idx & 31).astype(np.uint32)))
+        allow = torch.from_numpy(words.view(np.int32)).cuda()
+        bm.prepare_filtered(nd)
+        off_q = np.zeros(len(queries) + 1, np.int32)
+        off_q[1:] = np.cumsum([len(x) for x in queries])
+        qt = torch.from_numpy(np.concatenate([np.asarray(x, np.int32) for x in queries])).cuda()
+        qo = torch.from_numpy(off_q).cuda()
+        for k in (1, 10, 64):
+            S, R = P.bm25_search_filtered_sharded(bm, qt, qo, k, allow, row0)
+            res[f"filt_{k}"] = (S.cpu().numpy(), R.cpu().numpy())
         emb, q = _dense_data(nd)
         dn = engine.DenseIndex(DIM, device=0, capacity=n)
         dn.upsert(emb[row0:row0 + n], np.arange(n, dtype=np.int64))
@@ -108,3 +129,24 @@ def test_sharded_hip_dense_equals_single_index(results):
         D, R = res["dense"]
         assert np.array_equal(R, r)
         np.testing.assert_array_equal(D, d)
+
+
+@pytest.mark.parametrize("k", [1, 10, 64])
+def test_sharded_hip_bm25_filtered_equals_unsharded_oracle(results, k):
+    """Filtered BM25 across two shards (candidate statistics all-reduced, epsilon floor from the
+    global first-occurrence order) == rank_bm25 over the filtered documents, bit for bit."""
+    toks, off, vocab, queries = _corpus()
+    nd = off.shape[0] - 1
+    keep = np.nonzero(_filter_mask(nd))[0]
+    sub_toks = np.concatenate([toks[off[d]:off[d + 1]] for d in keep])
+    sub_off = np.zeros(keep.shape[0] + 1, np.int64)
+    sub_off[1:] = np.cumsum(off[keep + 1] - off[keep])
+    csr = corc.build_csr(sub_toks, sub_off, vocab)
+    idf, eps = corc.bm25_idf(csr["df"], csr["first_key"], keep.shape[0])
+    assert (idf == eps).any()                        # the epsilon floor is exercised
+    sc, rw = corc.bm25_topk(csr, idf, float(sub_off[-1]) / keep.shape[0], queries, k)
+    rw = np.where(rw >= 0, keep[np.maximum(rw, 0)], -1)
+    for r in results:
+        S, R = r[f"filt_{k}"]
+        assert np.array_equal(R, rw)
+        assert np.array_equal(S, sc)

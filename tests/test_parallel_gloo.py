@@ -41,6 +41,44 @@ def _corpus(seed=3, nd=6000, vocab=700):
     return toks, off, vocab, queries
 
 
+def _filter_mask(nd):
+    r = np.arange(nd)
+    return (r % 3 == 0) | (r < 150)
+
+
+def _masked_csr(toks, off, vocab, mask):
+    """CSR of a shard whose non-candidate documents are emptied: candidate df and first
+    (local row, position) keys with the shard's own row numbering."""
+    lens = np.where(mask, off[1:] - off[:-1], 0)
+    keep = np.repeat(mask, off[1:] - off[:-1])
+    moff = np.zeros(mask.shape[0] + 1, np.int64)
+    moff[1:] = np.cumsum(lens)
+    return corc.build_csr(toks[keep], moff, vocab)
+
+
+def _filtered_shard_search(P, toks, off, vocab, queries, row0, n, k):
+    import math
+    mask = _filter_mask(off.shape[0] - 1)[row0:row0 + n]
+    loc_off = off[row0:row0 + n + 1] - off[row0]
+    loc_toks = toks[off[row0]:off[row0 + n]]
+    mc = _masked_csr(loc_toks, loc_off, vocab, mask)
+    flat = np.concatenate([np.asarray(q, np.int64) for q in queries])
+    stats = torch.tensor([int(mask.sum()), int(mc["dl"].astype(np.int64).sum())], dtype=torch.int64)
+    df = torch.from_numpy(np.where(flat >= 0, mc["df"][np.maximum(flat, 0)], 0).astype(np.int64))
+    P.allreduce_filtered_stats(stats, df)
+    nc, sl = int(stats[0]), int(stats[1])
+    eps = P.filtered_eps_global(mc["df"], mc["first_key"], row0, nc)
+    idf = np.zeros(vocab, np.float64)                       # per term: global filtered idf
+    for t, d in zip(flat.tolist(), df.numpy().tolist()):
+        if t >= 0 and d > 0:
+            v = math.log(nc - d + 0.5) - math.log(d + 0.5)
+            idf[t] = eps if v < 0 else v
+    csr = corc.build_csr(loc_toks, loc_off, vocab)
+    sc, rw = corc.bm25_topk(csr, idf, sl / nc, queries, k, allow=mask)
+    S, R = P.merge_bm25_topk(torch.from_numpy(sc), torch.from_numpy(np.where(rw >= 0, rw + row0, rw)), k)
+    return S.numpy(), R.numpy()
+
+
 def _worker(rank, port, out_q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(WS))
     dist.init_process_group("gloo", rank=rank, world_size=WS)
@@ -78,6 +116,10 @@ def _worker(rank, port, out_q):
         local = torch.from_numpy(emb)[rows.clamp(0, nd - 1)] * own.unsqueeze(-1)
         res["pool"] = P.assemble_pool_vectors(rows, local, row0, n).numpy()
         res["max"] = P.max_over_ranks(float(rank) + 0.5)
+        # filtered BM25 (quirk Q2): candidate statistics all-reduced, epsilon floor from the
+        # global first-occurrence order -- the exchange bm25_search_filtered_sharded runs
+        for k in (1, 10, 64):
+            res[f"filt_{k}"] = _filtered_shard_search(P, toks, off, vocab, queries, row0, n, k)
         out_q.put(res)
     finally:
         dist.destroy_process_group()
@@ -145,3 +187,24 @@ def test_pool_assembly_and_max(results):
     for r in results:
         np.testing.assert_array_equal(r["pool"][0], want)
         assert r["max"] == 1.5
+
+
+@pytest.mark.parametrize("k", [1, 10, 64])
+def test_filtered_bm25_exchange_equals_unsharded_oracle(results, k):
+    """Sharded filtered BM25: the all-reduced candidate statistics and the global epsilon floor
+    give rank_bm25 over the filtered documents bit for bit (rag/retrieval/bm25.py:184-191)."""
+    toks, off, vocab, queries = _corpus()
+    nd = off.shape[0] - 1
+    keep = np.nonzero(_filter_mask(nd))[0]
+    sub_toks = np.concatenate([toks[off[d]:off[d + 1]] for d in keep])
+    sub_off = np.zeros(keep.shape[0] + 1, np.int64)
+    sub_off[1:] = np.cumsum(off[keep + 1] - off[keep])
+    csr = corc.build_csr(sub_toks, sub_off, vocab)
+    idf, eps = corc.bm25_idf(csr["df"], csr["first_key"], keep.shape[0])
+    assert (idf == eps).any()                           # the epsilon floor is exercised
+    sc, rw = corc.bm25_topk(csr, idf, float(sub_off[-1]) / keep.shape[0], queries, k)
+    rw = np.where(rw >= 0, keep[np.maximum(rw, 0)], -1)
+    for r in results:
+        S, R = r[f"filt_{k}"]
+        assert np.array_equal(R, rw)
+        assert np.array_equal(S, sc)
