@@ -394,6 +394,18 @@ constexpr int kRRing = K1C_RING;  // LDS ring slots (8 KB each): kRRing - 1 chun
 #ifndef K1C_NQL
 #define K1C_NQL 3
 #endif
+// cache-policy bits of K1c's corpus DMA (2 = nt: streamed once)
+#ifndef K1C_AUX
+#define K1C_AUX 2
+#endif
+// query chunks whose resident fragments are pinned to AGPRs (see the K1c prologue)
+#ifndef K1C_QAGPR
+#define K1C_QAGPR 8
+#endif
+// 1: the interleaved K1c chunk schedule (one non-MFMA step per MFMA); 0: the two-block schedule
+#ifndef K1C_SCHED
+#define K1C_SCHED 1
+#endif
 constexpr int kK1cNql = K1C_NQL;
 constexpr int kRRows = 64;      // rows per compute tile / chunk
 constexpr int kCBufCap = 64;    // candidate slots per (range, query)
@@ -506,10 +518,13 @@ __global__ void __launch_bounds__(64 * W, 1)
   constexpr int NF = 2 * QT;            // query fragments per wave and chunk
   constexpr int PCS = 8 / W;            // 1 KB DMA pieces per wave and chunk
   constexpr int H = kBQPass / QPASS;    // workgroups per (pass, range)
-#ifndef CM_ABLATION
+#if defined(K1C_DBG)
+  dbg = K1C_DBG;  // compile-time timing ablation (tools/build_dense_variant.sh), folds like the product
+#elif !defined(CM_ABLATION)
   dbg = 0;  // product build: the ablation branches fold away (exact lgkmcnt / vmcnt counting)
 #endif
   static_assert(W == 4 || W == 8, "K1c: 4 or 8 waves");
+  static_assert(LL::total <= 160 * 1024, "K1c: LDS ring + query chunks + mask exceed 160 KiB");
   static_assert(H == 1 || H == 2, "K1c: full or half passes");
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   const int tid = threadIdx.x;
@@ -544,7 +559,14 @@ __global__ void __launch_bounds__(64 * W, 1)
 #pragma unroll
     for (int qt = 0; qt < QT; ++qt)
 #pragma unroll
-      for (int sb = 0; sb < 2; ++sb) qres[c][qt][sb] = *qsrc(c, qt, sb);
+      for (int sb = 0; sb < 2; ++sb) {
+        qres[c][qt][sb] = *qsrc(c, qt, sb);
+        // pin the first K1C_QAGPR chunks' fragments to AGPRs (the 256 of them hold 8 chunks): the
+        // MFMA reads its B operand from an AGPR directly, where a VGPR value the allocator parked
+        // in an AGPR is copied back before every use (16 v_accvgpr_read per chunk).  With the
+        // accumulators in VGPRs (-mllvm -amdgpu-mfma-vgpr-form, Makefile) nothing is copied.
+        if (c < K1C_QAGPR) asm volatile("" : "+a"(qres[c][qt][sb]));
+      }
 #pragma unroll
   for (int c = 0; c < NQL; ++c)
 #pragma unroll
@@ -561,23 +583,29 @@ __global__ void __launch_bounds__(64 * W, 1)
     const int qq = qg0 + qt * 16 + j;
     sd[qt] = MINONLY ? 0.f : (qq < nq ? seed[qq] : -__builtin_inff());  // padded queries accept nothing
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // vmcnt(0) through the builtin (gfx9 encoding: vmcnt 0, expcnt 7, lgkmcnt 15), not inline asm: the
+  // compiler's wait tracker must see the prologue's query loads retired, or it re-waits for them
+  // with a vmcnt(0) inside the chunk loop -- draining the DMA ring once per tile
+  __builtin_amdgcn_s_waitcnt(0x0F70);
   __syncthreads();  // LDS query fragments ready; no DMA in flight yet
 
   // glds of chunk gc: wave-instruction i moves fragment block o = W i + wave (1 KB, lane-linear)
   const __attribute__((address_space(1))) unsigned char *Xb =
       (const __attribute__((address_space(1))) unsigned char *)Xh;
+  // the workgroup's chunks are contiguous in the plane: chunk gc = block run (cb + gc) * 8
+  const int64_t cb = (r_begin >> 6) * KC;
+  auto issue_piece = [&](int gc, int i) __attribute__((always_inline)) {
+    int gl = min(gc, total - 1);  // clamped: one control path past the end
+    if (dbg & 8192) gl &= 15;     // bit 13: ablation only (L2-resident source: LDS traffic without HBM)
+    const int o = W * i + wave;
+    __builtin_amdgcn_global_load_lds(Xb + (((cb + gl) * 8 + o) << 10) + lane * 16,
+                                     (__attribute__((address_space(3))) void *)(lds + LL::ring + (gc % RING) * 8192 +
+                                                                                o * 1024),
+                                     16, 0, K1C_AUX);
+  };
   auto issue = [&](int gc) __attribute__((always_inline)) {
-    const int gl = min(gc, total - 1);  // clamped: one control path past the end
-    const int t = gl / KC, c = gl - t * KC;
-    const int64_t tile = (r_begin >> 6) + t;
-    unsigned char *slot = lds + LL::ring + (gc % RING) * 8192;
 #pragma unroll
-    for (int i = 0; i < PCS; ++i) {
-      const int o = W * i + wave;
-      __builtin_amdgcn_global_load_lds(Xb + (((tile * KC + c) * 8 + o) << 10) + lane * 16,
-                                       (__attribute__((address_space(3))) void *)(slot + o * 1024), 16, 0, 0);
-    }
+    for (int i = 0; i < PCS; ++i) issue_piece(gc, i);
   };
   f32x4 acc[4][QT];
 #pragma unroll
@@ -585,14 +613,33 @@ __global__ void __launch_bounds__(64 * W, 1)
 #pragma unroll
     for (int qt = 0; qt < QT; ++qt) acc[rt][qt] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  uint32_t tile_words = 0;  // lanes 0, 1: live & allow words of the current tile
+  // The live and allow words of a window of 32 tiles (64 words: one per lane) are loaded into
+  // two VGPRs when the window starts and read out per tile with a uniform readlane.  The compiler
+  // cannot count a VGPR load among the LDS DMAs (it would wait vmcnt(0) at every use), so the
+  // window load waits vmcnt(0) itself, where the compiler sees it: the DMA ring drains once per 32
+  // tiles instead of once per tile.
+  const uint32_t *allw = allow ? allow : live;
+  uint32_t lwin = 0u, awin = 0u;
+  auto load_window = [&](int t) __attribute__((always_inline)) {
+    const int64_t wi = ((r_begin + (int64_t)t * kRRows) >> 5) + lane;
+    const int64_t wc = wi < n_words ? wi : n_words - 1;  // n_words >= 1 whenever a tile is scanned
+    lwin = live[wc];
+    awin = allw[wc];
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0), visible to the compiler's wait tracking
+  };
   auto epilogue = [&](int t) __attribute__((always_inline)) {
     const int64_t row0 = r_begin + (int64_t)t * kRRows;
-    // lane (g, j) holds rows rt*16 + 4g + r: bit (16 rt + 4 g + r) of the 64-bit tile mask, whose
-    // two words lanes 0 and 1 loaded when the tile started (a vector load that lands during the
-    // tile's chunks instead of a scalar load waited for here)
-    const uint32_t b0 = (uint32_t)__builtin_amdgcn_readlane((int)tile_words, 0);
-    const uint32_t b1 = (uint32_t)__builtin_amdgcn_readlane((int)tile_words, 1);
+    const int64_t w0 = row0 >> 5;
+    // lane (g, j) holds rows rt*16 + 4g + r: bit (16 rt + 4 g + r) of the 64-bit tile mask
+#ifdef K1C_NOMASK
+    const uint32_t b0 = 0xffffffffu, b1 = 0xffffffffu;  // timing ablation only: every row live
+#else
+    const int wl = 2 * (t & 31);
+    const uint32_t m0 = (uint32_t)__builtin_amdgcn_readlane((int)(lwin & awin), wl);
+    const uint32_t m1 = (uint32_t)__builtin_amdgcn_readlane((int)(lwin & awin), wl + 1);
+    const uint32_t b0 = w0 < n_words ? m0 : 0u;
+    const uint32_t b1 = w0 + 1 < n_words ? m1 : 0u;
+#endif
     coarse_epilogue<QT, MINONLY>(acc, lane_live16(((uint64_t)b1 << 32) | b0, g), row0, sd, best, qcnt,
                                  out_keys + (((int64_t)qp * n_wg + wg) * kBQPass + qc0 + j) * kCBufCap);
 #pragma unroll
@@ -619,7 +666,7 @@ __global__ void __launch_bounds__(64 * W, 1)
     issue(RING - 1);
     f16x8 xf[4][2];
 #pragma unroll
-    for (int rt = 0; rt < 4; ++rt) {
+    for (int rt = 0; rt < (K1C_SCHED ? 2 : 4); ++rt) {  // interleaved schedule: chunk 0 reads its own 2-3
       xf[rt][0] = frag(0, rt, 0);
       xf[rt][1] = frag(0, rt, 1);
     }
@@ -633,14 +680,69 @@ __global__ void __launch_bounds__(64 * W, 1)
                                                         lane * 16);
     }
     for (int t = 0; t < ntiles; ++t) {
-      {
-        const int64_t wi = ((r_begin + (int64_t)t * kRRows) >> 5) + (lane & 1);  // lane-split: VMEM, not SMEM
-        tile_words = wi < n_words ? (live[wi] & (allow ? allow[wi] : 0xffffffffu)) : 0u;
-      }
+      if ((t & 31) == 0) load_window(t);
 #pragma unroll
       for (int c = 0; c < KC; ++c) {
         const int gc = t * KC + c;
+#if defined(K1C_QV) && K1C_QV == 1  // timing ablations only: one resident chunk's fragments for all
+        auto qv = [&](int qt, int sb) -> f16x8 { return qres[0][qt][sb]; };
+#elif defined(K1C_QV) && K1C_QV == 2  // ... register fragments only (no LDS-resident chunks)
+        auto qv = [&](int qt, int sb) -> f16x8 { return qres[KR > 0 ? c % KR : 0][qt][sb]; };
+#else
         auto qv = [&](int qt, int sb) -> f16x8 { return c < KR ? qres[c < KR ? c : 0][qt][sb] : ql[qt][sb]; };
+#endif
+        const int cn = (c + 1) % KC;  // next chunk's query fragments come from LDS when cn >= KR
+#if K1C_SCHED
+        // Interleaved chunk schedule.  With one wave per SIMD nothing hides a non-MFMA instruction
+        // but the MFMA issued just before it, so the chunk's LDS reads, counted wait, barrier and
+        // DMA pieces are threaded one per MFMA through its 2 x MH MFMAs (sched_barrier-fenced):
+        //   half 1 (row tiles 0-1): read row fragments 2-3 of chunk gc (slot certified by the
+        //     previous chunk's barrier), then wait for chunk gc+1 (own pieces; PCS (RING - 2) younger
+        //     stay in flight) and for the own reads of slot gc, barrier (chunk gc+1 visible, every
+        //     read of slot gc retired), DMA chunk gc + RING into slot gc;
+        //   half 2 (row tiles 2-3): read row fragments 0-1 of chunk gc+1; the next chunk's LDS
+        //     query fragments follow the last MFMA of their q-tile group.
+        // MFMA order within a half: q-tile group, k-half, row tile, q-tile (an accumulator recurs
+        // every 2 QA MFMAs), so a q-tile group's fragments are free half-way through the half.
+        {
+          constexpr int QA = QT / 2, MH = 8 * QA;
+          auto mf = [&](int h, int m) __attribute__((always_inline)) {
+            const int qa = m % QA, rt = 2 * h + (m / QA) % 2, sb = (m / (2 * QA)) % 2, qt = (m / (4 * QA)) * QA + qa;
+            if (dbg & 4096) return;  // bit 12: ablation only (no MFMA: the memory side alone)
+            acc[rt][qt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xf[rt][sb], qv(qt, sb), acc[rt][qt], 0, 0, 0);
+          };
+          auto read_ql = [&](int grp) __attribute__((always_inline)) {
+#pragma unroll
+            for (int qa = 0; qa < QA; ++qa)
+#pragma unroll
+              for (int sb = 0; sb < 2; ++sb)
+                ql[grp * QA + qa][sb] = *reinterpret_cast<const f16x8 *>(
+                    lds + LL::qf + (((cn - KR) * W + wave) * NF + (grp * QA + qa) * 2 + sb) * 1024 + lane * 16);
+          };
+#pragma unroll
+          for (int m = 0; m < MH; ++m) {
+            mf(0, m);
+            __builtin_amdgcn_sched_barrier(0);
+            if (m < 4 && !(dbg & 2048)) xf[2 + m / 2][m % 2] = frag(gc, 2 + m / 2, m % 2);  // bit 11: ablation
+            if (m == MH - PCS - 2) {
+              asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(PCS * (RING - 2)) : "memory");
+              if (!(dbg & 512)) __builtin_amdgcn_s_barrier();  // bit 9: ablation only (races)
+            }
+            if (m >= MH - PCS - 1 && m < MH - 1 && !(dbg & 1024))  // bit 10: ablation only (stale data)
+              issue_piece(gc + RING, m - (MH - PCS - 1));
+            __builtin_amdgcn_sched_barrier(0);
+          }
+#pragma unroll
+          for (int m = 0; m < MH; ++m) {
+            mf(1, m);
+            __builtin_amdgcn_sched_barrier(0);
+            if (m < 4 && !(dbg & 2048)) xf[m / 2][m % 2] = frag(gc + 1, m / 2, m % 2);
+            if (cn >= KR && m == MH / 2 - 1) read_ql(0);
+            if (cn >= KR && m == MH - 1) read_ql(1);
+            __builtin_amdgcn_sched_barrier(0);
+          }
+        }
+#else
         // half 1: row tiles 0, 1
 #pragma unroll
         for (int rt = 0; rt < 2; ++rt) {
@@ -679,7 +781,6 @@ __global__ void __launch_bounds__(64 * W, 1)
           xf[rt][0] = frag(gc + 1, rt, 0);
           xf[rt][1] = frag(gc + 1, rt, 1);
         }
-        const int cn = (c + 1) % KC;  // next chunk's query fragments, when LDS-resident
         if (cn >= KR) {
 #pragma unroll
           for (int qt = 0; qt < QT; ++qt)
@@ -689,8 +790,21 @@ __global__ void __launch_bounds__(64 * W, 1)
                   lds + LL::qf + (((cn - KR) * W + wave) * NF + qt * 2 + sb) * 1024 + lane * 16);
         }
         __builtin_amdgcn_sched_barrier(0);
+#endif
       }
+#ifdef K1C_EPI0  // timing ablation only: keep the MFMAs alive with a trivial epilogue
+      {
+        float z = 0.f;
+#pragma unroll
+        for (int rt = 0; rt < 4; ++rt)
+#pragma unroll
+          for (int qt = 0; qt < QT; ++qt) z += acc[rt][qt][0];
+        best[0] = fminf(best[0], z);
+        qcnt[0] += z == 12345.f ? 1u : 0u;  // observable: out_cnt / out_min
+      }
+#else
       if (!(dbg & 128)) epilogue(t);
+#endif
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // clamped tail DMAs land before the LDS is released
   }
@@ -774,10 +888,14 @@ __global__ void __launch_bounds__(256, 1)
 #pragma unroll
     for (int p = 0; p < R - 1; ++p) load(xb[p], p);
     for (int t = 0; t < ntiles; ++t) {
-      uint32_t tile_words;
+      uint32_t lw, aw;  // branch-free loads, combined at the epilogue (see K1c)
+      bool w_ok;
       {
         const int64_t wi = ((r_begin + (int64_t)t * kRRows) >> 5) + (lane & 1);
-        tile_words = wi < n_words ? (live[wi] & (allow ? allow[wi] : 0xffffffffu)) : 0u;
+        w_ok = wi < n_words;
+        const int64_t wc = w_ok ? wi : n_words - 1;
+        lw = __builtin_nontemporal_load(live + wc);
+        aw = __builtin_nontemporal_load((allow ? allow : live) + wc);
       }
 #pragma unroll
       for (int c = 0; c < KC; ++c) {
@@ -796,6 +914,7 @@ __global__ void __launch_bounds__(256, 1)
         __builtin_amdgcn_sched_barrier(0);
       }
       const int64_t row0 = r_begin + (int64_t)t * kRRows;
+      const uint32_t tile_words = w_ok ? (lw & aw) : 0u;
       const uint32_t b0 = (uint32_t)__builtin_amdgcn_readlane((int)tile_words, 0);
       const uint32_t b1 = (uint32_t)__builtin_amdgcn_readlane((int)tile_words, 1);
       coarse_epilogue<QT, MINONLY>(acc, lane_live16(((uint64_t)b1 << 32) | b0, g), row0, sd, best, qcnt,
