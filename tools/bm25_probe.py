@@ -44,6 +44,7 @@ for path in [int(x) for x in a.paths.split(",")]:
     out = b.search_dev(q_terms, q_off, 10, workspace=ws)
     torch.cuda.synchronize()
     ts = []
+    b.timing(True)
     for _ in range(a.reps):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
@@ -51,6 +52,8 @@ for path in [int(x) for x in a.paths.split(",")]:
         e1.record()
         torch.cuda.synchronize()
         ts.append(e0.elapsed_time(e1))
+    kt = b.timing_drain()
+    b.timing(False)
     res = (out[0].cpu(), out[1].cpu())
     same = "" if ref is None else f" identical_to_path{ref[2]}={bool(torch.equal(ref[0], res[0]) and torch.equal(ref[1], res[1]))}"
     if ref is None:
@@ -58,5 +61,5 @@ for path in [int(x) for x in a.paths.split(",")]:
     nr = (a.docs + 1023) // 1024
     resc = b.workspace_rescored(a.batch, q_terms.numel(), 10, ws)
     print(f"docs={a.docs} B={a.batch} head_terms={b.num_head_terms} path={path} dbg={os.environ.get('CM_BM25_DEBUG', '0')} "
-          f"search_ms={sorted(ts)[len(ts) // 2]:.3f} rescored={resc}/{a.batch * nr}{same} "
+          f"search_ms={sorted(ts)[len(ts) // 2]:.3f} kernel_ms={sorted(kt)[len(kt) // 2]:.3f} rescored={resc}/{a.batch * nr}{same} "
           f"all={['%.2f' % t for t in ts]}", flush=True)
