@@ -50,7 +50,7 @@ def parse_args():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--mode", choices=["hybrid", "dense", "ingest"], default="hybrid")
+    ap.add_argument("--mode", choices=["hybrid", "dense", "ingest", "e2e"], default="hybrid")
     ap.add_argument("--docs-per-gpu", type=int, default=10_000_000)
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--k", type=int, default=10)
@@ -72,6 +72,8 @@ def parse_args():
     ap.add_argument("--bm25-priority", type=int, default=0, help="HIP stream priority of the BM25 stream (-1 = high)")
     ap.add_argument("--bm25-after-e5", action="store_true", help="launch BM25 after the E5 encode (overlap with dense)")
     ap.add_argument("--seq-len", type=int, default=256, help="ingest mode: tokens per chunk")
+    ap.add_argument("--e2e-words", type=int, default=40, help="e2e mode: words per synthetic chunk")
+    ap.add_argument("--e2e-latency-queries", type=int, default=32, help="e2e mode: single-query retrieve() calls timed")
     ap.add_argument("--cpu-baseline", type=int, default=1)
     ap.add_argument("--cpu-queries", type=int, default=64)
     ap.add_argument("--seed", type=int, default=1)
@@ -153,6 +155,8 @@ def main():
         log(f"note: --gpus {args.gpus} but WORLD_SIZE={ws}; using {ws}")
     if args.mode == "ingest":
         return run_ingest(args, rank, ws, dev)
+    if args.mode == "e2e":
+        return run_e2e(args, rank, ws, dev)
 
     B, K, P, D = args.batch, args.k, args.pool, args.dim
     if args.mode == "dense":   # C2: plain cosine top-k (no MMR pool)
@@ -530,12 +534,112 @@ def cpu_baseline_and_recall(args, dense, bm25, res, q_terms, q_dev):
 
 
 # ---------------------------------------------------------------------------
+def run_e2e(args, rank, ws, dev):
+    """The drop-in API end to end: HybridRetriever.retrieve_batch over query STRINGS
+    -> lists of result dicts, through GpuVectorStore / BM25Store / E5MultilingualEmbedder exactly as
+    the reference's callers use them (rag/retrieval/fusion.py HybridRetriever.retrieve).  Corpus:
+    --docs-per-gpu synthetic chunks of --e2e-words Zipf words (letters-only ids, as the BM25 tokenizer
+    keeps letters only), metadata {course, week, language},
+    random unit embeddings upserted with the texts (the passage encode is ingest mode's metric);
+    queries are word samples of corpus chunks encoded by the random-init E5 (fp32, the drop-in
+    default) with the offline hash tokenizer.  value = retrieve_batch queries/s (B per call);
+    also single-query retrieve() latency p50 / p99."""
+    import numpy as np
+    import torch
+    from classmate_hip.embeddings import E5MultilingualEmbedder
+    from classmate_hip.retrieval.bm25 import BM25Store
+    from classmate_hip.retrieval.fusion import HybridRetriever
+    from classmate_hip.retrieval.vector_store import GpuVectorStore
+    if ws != 1:
+        sys.exit("bench.py --mode e2e: single process (the drop-in API is one store per process)")
+    N, B, K, D = args.docs_per_gpu, args.batch, args.k, args.dim
+    rng = np.random.default_rng(args.seed)
+    t_setup = time.perf_counter()
+    V = 1 << 16
+    p = 1.0 / np.arange(1, V + 1) ** args.zipf
+    cdf = np.cumsum(p)
+    cdf /= cdf[-1]
+    words = np.minimum(np.searchsorted(cdf, rng.random(N * args.e2e_words)), V - 1).reshape(N, args.e2e_words)
+    alpha = np.array(list("abcdefghijklmnopqrstuvwxyz"))
+    vocab = ["zq" + "".join(alpha[(w // 26 ** i) % 26] for i in range(4)) for w in range(V)]  # letters only
+    texts = [" ".join(vocab[w] for w in row) for row in words]
+    ids = [f"c{i}" for i in range(N)]
+    metas = [{"course": f"C{i % 16}", "week": int(i % 12), "language": "en"} for i in range(N)]
+    log(f"e2e corpus: {N} chunks x {args.e2e_words} words ({time.perf_counter() - t_setup:.1f}s)")
+    g = torch.Generator(device="cuda").manual_seed(args.seed * 1000)
+    emb = torch.randn(N, D, device=dev, generator=g)
+    emb /= emb.norm(dim=1, keepdim=True)
+    emb = emb.cpu().numpy()
+    vs = GpuVectorStore(persist_dir=None, device=dev.index)
+    step = 1 << 18
+    for i in range(0, N, step):
+        vs.upsert(ids=ids[i:i + step], documents=texts[i:i + step], metadatas=metas[i:i + step],
+                  embeddings=emb[i:i + step])
+    del emb
+    bm = BM25Store(index_dir=None, device=dev.index)
+    bm.upsert_many(ids=ids, texts=texts, metadatas=metas)
+    embedder = E5MultilingualEmbedder.random_init(seed=0, device=str(dev), num_layers=args.e5_layers)
+    retr = HybridRetriever(vector_store=vs, bm25_store=bm, embedder=embedder)
+    qsrc = rng.integers(0, N, B * (args.steps + args.warmup + 1))
+    qs = [" ".join(texts[i].split()[j:j + 6]) for i, j in zip(qsrc, rng.integers(0, args.e2e_words - 6, qsrc.size))]
+    retr.retrieve_batch(questions=qs[:B], top_k=K)     # builds the BM25 index, first graph/kernels
+    torch.cuda.synchronize()
+    log(f"e2e stores ready: {vs.count()} vectors, {len(bm._id_list)} BM25 docs ({time.perf_counter() - t_setup:.1f}s)")
+    for w in range(args.warmup):
+        retr.retrieve_batch(questions=qs[(w + 1) * B:(w + 2) * B], top_k=K)
+    torch.cuda.synchronize()
+    prof = None
+    if os.environ.get("CM_E2E_PROFILE"):              # host-side profile of the timed calls
+        import cProfile
+        prof = cProfile.Profile()
+        prof.enable()
+    t0 = time.perf_counter()
+    n_res = 0
+    for st in range(args.steps):
+        o = (args.warmup + 1 + st) * B
+        res = retr.retrieve_batch(questions=qs[o:o + B], top_k=K)
+        n_res += sum(len(r) for r in res)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if prof is not None:
+        import pstats
+        prof.disable()
+        pstats.Stats(prof, stream=sys.stderr).sort_stats("cumulative").print_stats(40)
+    for i in range(3):                                 # batch-1 shapes: first-call setup
+        retr.retrieve(question=qs[-1 - i], top_k=K)
+    lat = []
+    for i in range(args.e2e_latency_queries):
+        t1 = time.perf_counter()
+        retr.retrieve(question=qs[i], top_k=K)
+        lat.append((time.perf_counter() - t1) * 1e3)
+    lat.sort()
+    qps = B * args.steps / elapsed
+    log(f"{args.steps} retrieve_batch calls in {elapsed:.3f}s -> {qps:.1f} q/s; retrieve() p50 "
+        f"{lat[len(lat) // 2]:.2f} ms, p99 {lat[min(len(lat) - 1, int(len(lat) * 0.99))]:.2f} ms")
+    out = {
+        "metric": f"drop-in HybridRetriever.retrieve_batch queries/sec (strings -> result dicts), {N} chunks",
+        "value": qps, "unit": "queries/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "fp32 E5 + f16/f64 dense + f64 BM25",
+        "data": "synthetic (seeded): Zipf-word chunks, random unit embeddings, random-init E5-base weights",
+        "config": {"workload": "drop-in retrieve_batch (E5 query encode + cosine pool 24 + MMR 8 + BM25 8 + RRF)",
+                   "chunks": N, "words_per_chunk": args.e2e_words, "global_batch": B, "top_k": K, "dim": D},
+        "retrieve_latency_ms": {"p50": lat[len(lat) // 2], "p99": lat[min(len(lat) - 1, int(len(lat) * 0.99))],
+                                "n": len(lat)},
+        "results_returned": n_res, "setup_s": time.perf_counter() - t_setup,
+    }
+    line = json.dumps(out)
+    print(line, flush=True)
+    if args.out:
+        Path(args.out).write_text(line + "\n")
+
+
 def run_ingest(args, rank, ws, dev):
-    """configs[2]: E5-base batch encode (bf16 forward + HIP mean-pool/L2), chunks/s."""
+    """configs[2]: E5-base batch encode (forward in --e5-dtype + HIP mean-pool/L2), chunks/s."""
     import torch
     from classmate_hip import parallel
     from classmate_hip.embeddings import E5MultilingualEmbedder
-    emb = E5MultilingualEmbedder.random_init(seed=0, device=str(dev), num_layers=args.e5_layers)
+    emb = E5MultilingualEmbedder.random_init(seed=0, device=str(dev), num_layers=args.e5_layers, dtype=args.e5_dtype)
     B, S = args.batch, args.seq_len
     g = torch.Generator(device="cuda").manual_seed(args.seed + rank)
     ids = torch.randint(5, 250002, (B, S), device=dev, generator=g)
@@ -560,12 +664,15 @@ def run_ingest(args, rank, ws, dev):
     res = {"metric": "E5-base ingest encode chunks/sec (forward + HIP mean-pool/L2)", "value": val,
            "unit": "chunks/s", "n_gpus": ws, "steps": args.steps, "warmup": args.warmup,
            "ms_per_step": el / args.steps * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-           "dtype": "bf16", "data": "synthetic token ids, random-init E5-base weights",
+           "dtype": {"bfloat16": "bf16", "float32": "fp32"}[args.e5_dtype],
+           "data": "synthetic token ids, random-init E5-base weights",
            "config": {"workload": "E5-base encode", "global_batch": B * ws, "seq_len": S,
                       "parallelism": f"replicas x{ws}"},
            "achieved_tflops": val * flops_seq / 1e12}
     if rank == 0:
         print(json.dumps(res), flush=True)
+        if args.out:
+            Path(args.out).write_text(json.dumps(res) + "\n")
 
 
 if __name__ == "__main__":

@@ -35,12 +35,29 @@ def _tokenize(text: str, lang_hint: Optional[str] = None) -> List[str]:
     return [t for t in (m.group(0).lower() for m in _TOKEN_RE.finditer(text or "")) if t not in sw and len(t) > 1]
 
 
+_LANGDETECT = None  # (DetectorFactory, detect) once imported; False when the package is absent
+
+
+def _langdetect():
+    global _LANGDETECT
+    if _LANGDETECT is None:
+        try:
+            from langdetect import DetectorFactory, detect
+            _LANGDETECT = (DetectorFactory, detect)
+        except Exception:  # absent: every text is 'en' (the reference's except branch)
+            _LANGDETECT = False
+    return _LANGDETECT
+
+
 def detect_lang_tag(text: str) -> str:
-    """rag/utils/lang_detect.py:16-24: langdetect (seed 42) restricted to en/it, 'en' otherwise."""
+    """rag/utils/lang_detect.py:16-24: langdetect (seed 42) restricted to en/it, 'en' otherwise.
+    The import is attempted once per process (a failed import per call cost ~60 us per query)."""
+    ld = _langdetect()
+    if not ld:
+        return "en"
     try:
-        from langdetect import DetectorFactory, detect
-        DetectorFactory.seed = 42
-        lang = detect(text or "")
+        ld[0].seed = 42
+        lang = ld[1](text or "")
         return lang if lang in ("en", "it") else "en"
     except Exception:
         return "en"

@@ -234,8 +234,8 @@ class GpuVectorStore:
             item = {"id": self._ids[r], "document": self._docs[r] if include_documents else None,
                     "metadata": self._meta.metas[r],
                     "distance": float(dist[i, j])}
-            if include_embeddings:
-                item["embedding"] = np.array(vecs[i, j], dtype="float32")
+            if include_embeddings:   # a row view of this call's own (B, k, D) fp32 buffer
+                item["embedding"] = vecs[i, j]
             out.append(item)
         return out
 

@@ -217,8 +217,9 @@ def test_e5_graph_replay_matches_eager():
     g_mask.copy_(mask)
     graph.replay()
     torch.cuda.synchronize()
-    want = emb.encode_token_ids(ids, mask)
+    want = emb._encode_hf(ids, mask)
     torch.testing.assert_close(g_out, want, atol=2e-3, rtol=0)
+    torch.testing.assert_close(emb.encode_token_ids(ids, mask), want, atol=2e-3, rtol=0)
     assert torch.allclose(g_out.norm(dim=1), torch.ones(B, device="cuda"), atol=1e-5)
     # unpadded batches: the maskless graph equals the eager encode
     mask.fill_(1)

@@ -523,7 +523,13 @@ def test_e5_lean_forward_fp32_matches_hf():
     u_ids.copy_(ids)
     graph.replay()
     torch.cuda.synchronize()
-    torch.testing.assert_close(u_out, emb.encode_token_ids(ids, mask), atol=2e-5, rtol=0)
+    torch.testing.assert_close(u_out, emb._encode_hf(ids, mask), atol=2e-5, rtol=0)
+    torch.testing.assert_close(emb.encode_token_ids(ids, mask), emb._encode_hf(ids, mask), atol=2e-5, rtol=0)
+    mask[2, 11:] = 0                                   # ragged rows: lean padded path == HF
+    mask[5, 3:] = 0
+    ids[2, 11:] = 1
+    ids[5, 3:] = 1
+    torch.testing.assert_close(emb.encode_token_ids(ids, mask), emb._encode_hf(ids, mask), atol=2e-5, rtol=0)
 
 
 @pytest.mark.parametrize("S", [1, 7, 16, 24, 32, 33, 64])
