@@ -11,6 +11,7 @@ from pathlib import Path
 
 REPO = Path(__file__).resolve().parents[1]
 sys.path[:0] = [str(REPO), str(REPO / "classmate-rag_amd")]
+import numpy as np  # noqa: E402
 import torch  # noqa: E402
 from bench import gen_tokens, sample_query_terms  # noqa: E402
 from classmate_hip import engine  # noqa: E402
@@ -60,6 +61,22 @@ for path in [int(x) for x in a.paths.split(",")]:
         ref = (res[0], res[1], path)
     nr = (a.docs + 1023) // 1024
     resc = b.workspace_rescored(a.batch, q_terms.numel(), 10, ws)
+    if path == 2 and os.environ.get("BM25_ITEMS"):
+        # K2b work: mirror bm_ws_layout (cm_bm25.hip) to read the planned items (diagnostic only)
+        ru = lambda x: (x + 255) // 256 * 256
+        nq, tt, k = a.batch, q_terms.numel(), 10
+        off = ru(nq * 8) + ru(128 * 16 * 8) + ru(tt * 8) + ru(tt * (nr + 1) * 8) + ru(nq * nr * k * 8) + ru(nq * nr * k * 4)
+        off_need = off
+        off += ru(((nq + 3) // 4) * nr)
+        off_items = off
+        off += ru(nq * nr * 8)
+        n_items = int(ws[off:off + 4].view(torch.int32).item())
+        items = ws[off_items:off_items + 8 * n_items].view(torch.int64).cpu().numpy()
+        masks = (items & 0xffff).astype(np.uint64)
+        nblk = int(sum(bin(int(m)).count("1") for m in masks))
+        need = ws[off_need:off_need + ((nq + 3) // 4) * nr].cpu().numpy()
+        print(f"K2b items={n_items} blocks={nblk} ({nblk * 64} docs scored); K2 need pairs="
+              f"{int(sum(bin(int(x)).count('1') for x in need))}", flush=True)
     print(f"docs={a.docs} B={a.batch} head_terms={b.num_head_terms} path={path} dbg={os.environ.get('CM_BM25_DEBUG', '0')} "
           f"search_ms={sorted(ts)[len(ts) // 2]:.3f} kernel_ms={sorted(kt)[len(kt) // 2]:.3f} rescored={resc}/{a.batch * nr}{same} "
           f"all={['%.2f' % t for t in ts]}", flush=True)
