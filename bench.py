@@ -71,6 +71,8 @@ def parse_args():
     ap.add_argument("--serial", action="store_true", help="run BM25 on the main stream (no overlap with E5 + dense)")
     ap.add_argument("--bm25-priority", type=int, default=0, help="HIP stream priority of the BM25 stream (-1 = high)")
     ap.add_argument("--bm25-after-e5", action="store_true", help="launch BM25 after the E5 encode (overlap with dense)")
+    ap.add_argument("--bm25-cus", default="", help="run the BM25 stream on a CU subset: 'first:N', 'stride:S' "
+                    "(every S-th CU) or '' (all CUs)")
     ap.add_argument("--seq-len", type=int, default=256, help="ingest mode: tokens per chunk")
     ap.add_argument("--e2e-words", type=int, default=40, help="e2e mode: words per synthetic chunk")
     ap.add_argument("--e2e-latency-queries", type=int, default=32, help="e2e mode: single-query retrieve() calls timed")
@@ -231,6 +233,12 @@ def main():
     main = torch.cuda.current_stream(dev)
     side = (torch.cuda.Stream(device=dev, priority=args.bm25_priority)
             if (bm25 is not None and not args.serial) else main)
+    if bm25 is not None and not args.serial and args.bm25_cus:
+        n_cu = torch.cuda.get_device_properties(dev).multi_processor_count
+        how, val = args.bm25_cus.split(":")
+        cus = range(int(val)) if how == "first" else range(0, n_cu, int(val))
+        side = engine.cu_masked_stream(local, list(cus))
+        log(f"BM25 stream on {len(list(cus))} of {n_cu} CUs ({args.bm25_cus})")
 
     def run_bm25(e):
         # BM25 needs only the query term ids: it runs on its own stream, overlapping the E5

@@ -51,6 +51,8 @@ SIGNATURES = {
     "cm_last_error": (c_char_p,),
     "cm_version": (c_int,),
     "cm_device_count": (c_int, P(c_int)),
+    "cm_stream_create_cu_masked": (c_int, c_int, P(C.c_uint32), c_int, P(c_vp)),
+    "cm_stream_destroy": (c_int, c_vp),
     "cm_max_topk": (c_int,),
     "cm_dense_create": (c_int, c_int, c_i32, c_i64, P(c_vp)),
     "cm_dense_destroy": (None, c_vp),

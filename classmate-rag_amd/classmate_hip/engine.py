@@ -45,6 +45,34 @@ def _c(a, dtype):
     return np.ascontiguousarray(a, dtype=dtype)
 
 
+def cu_masked_stream(device: int, cus):
+    """A torch.cuda.ExternalStream whose kernels run only on the CU indices in ``cus``
+    (``cm_stream_create_cu_masked``); the HIP stream lives as long as the returned object."""
+    n_cu = torch.cuda.get_device_properties(device).multi_processor_count
+    words = np.zeros((n_cu + 31) // 32, np.uint32)
+    for c in cus:
+        if not 0 <= c < n_cu:
+            raise ValueError(f"CU index {c} outside 0..{n_cu - 1}")
+        words[c // 32] |= np.uint32(1 << (c % 32))
+    ptr = C.c_void_p()
+    L.check(L.fn["cm_stream_create_cu_masked"](device, words.ctypes.data_as(C.POINTER(C.c_uint32)), words.size,
+                                                C.byref(ptr)), "cm_stream_create_cu_masked")
+    st = torch.cuda.ExternalStream(ptr.value, device=torch.device("cuda", device))
+    st._cm_keep = (words, _StreamOwner(ptr.value))
+    return st
+
+
+class _StreamOwner:
+    def __init__(self, ptr):
+        self.ptr = ptr
+
+    def __del__(self):
+        try:
+            L.fn["cm_stream_destroy"](C.c_void_p(self.ptr))
+        except Exception:
+            pass
+
+
 class DenseIndex:
     """HBM-resident fp32 corpus + exact cosine top-k (replaces Chroma's HNSW)."""
 

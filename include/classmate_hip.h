@@ -49,6 +49,12 @@ extern "C" {
 const char *cm_last_error(void);
 int cm_version(void);
 int cm_device_count(int *n);
+/* A HIP stream restricted to the CUs whose bits are set in cu_mask (n_words
+ * 32-bit words; bit i = CU i of the device's enumeration) -- for running a
+ * latency-bound stage beside a bandwidth-bound one (bench.py --bm25-cus).
+ * Not a reference interface: an engine-side scheduling helper. */
+int cm_stream_create_cu_masked(int device, const uint32_t *cu_mask, int n_words, void **out_stream);
+int cm_stream_destroy(void *stream);
 /* largest k the fused top-k kernels accept (dense and BM25 _dev entries); the
  * host-array searches accept any k >= 1 (beyond it: full order + device sort). */
 int cm_max_topk(void);
