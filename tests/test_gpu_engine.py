@@ -437,6 +437,42 @@ def test_bm25_many_ranges_vs_c_oracle(eng, policy, path):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("df_frac", [0.02, 0.035, 0.06])
+def test_bm25_tail_pass_super_range_halving(eng, df_frac):
+    """K2a gathers 4 consecutive ranges per iteration and halves the span when their candidate
+    postings overflow its LDS lists (320 per query group): query groups whose only candidate
+    generators are designated head terms of ~2-6 % df land on 4-, 2- and 1-range spans (and on
+    the K2 re-score when one range overflows).  Bit-identical to the full scan and the C oracle."""
+    from oracle import corc
+    rng = np.random.default_rng(33)
+    nd, vocab = 60_000, 3000
+    lens = np.maximum(rng.poisson(20, nd), 1)
+    off = np.zeros(nd + 1, np.int64)
+    off[1:] = np.cumsum(lens)
+    toks = rng.integers(10, vocab, int(off[-1])).astype(np.int32)       # rare background terms
+    for t in range(4):                                                    # terms 0..3: ~df_frac each
+        docs = np.nonzero(rng.random(nd) < df_frac * (1 + 0.3 * t))[0]
+        toks[off[docs] + rng.integers(0, lens[docs])] = t
+    b = eng.BM25Index()
+    b.build(toks, off, vocab)
+    b.set_head_policy(0.01, 8 << 30)                                      # terms 0..3 get head tiles
+    queries = [[0], [1], [0, 1], [2], [3, 0], [1, 2, 3], [0, 1, 2, 3], [2, 3],
+               [int(toks[off[5]]), 0], [1, int(toks[off[9]])], [3], [0, 0, 2]]
+    k = 10
+    csr = corc.build_csr(toks, off, vocab)
+    idf, _ = corc.bm25_idf(csr["df"], csr["first_key"], nd)
+    o_sc, o_rw = corc.bm25_topk(csr, idf, float(lens.sum()) / nd, queries, k)
+    b.set_path(1)
+    s1, r1, _ = b.search(queries, k)
+    b.set_path(2)
+    s2, r2, _ = b.search(queries, k)
+    assert np.array_equal(r1, r2) and np.array_equal(s1, s2)
+    for i in range(len(queries)):
+        assert r2[i][:k].tolist() == o_rw[i].tolist(), i
+        assert s2[i][:k].tolist() == o_sc[i].tolist(), i
+
+
+@pytest.mark.gpu
 def test_bm25_pruned_skips_ranges_and_matches_full_scan(eng):
     """Bench-shaped workload (Zipf corpus, 8-term queries drawn from documents, head tiles on):
     the pruned search re-scores only a fraction of the (query, range) pairs and returns the
