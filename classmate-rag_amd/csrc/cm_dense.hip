@@ -398,6 +398,11 @@ constexpr int kRRing = K1C_RING;  // LDS ring slots (8 KB each): kRRing - 1 chun
 #ifndef K1C_AUX
 #define K1C_AUX 2
 #endif
+// 1: K1s streams the plane with non-temporal loads (read once): 10M x 768, B = 16 2.48 -> 2.22 ms
+// (6.9 TB/s, 0.87 of the 8 TB/s peak)
+#ifndef K1S_NT
+#define K1S_NT 1
+#endif
 // query chunks whose resident fragments are pinned to AGPRs (see the K1c prologue)
 #ifndef K1C_QAGPR
 #define K1C_QAGPR 8
@@ -880,10 +885,9 @@ __global__ void __launch_bounds__(256, 1)
     f16x8 xb[R][8];
     auto load = [&](f16x8 (&b)[8], int gc) __attribute__((always_inline)) {
       const int gl = min(gc, total - 1);  // clamped: one control path past the end
-      const int t = gl / KC, c = gl - t * KC;
-      const f16x8 *p = Xv + ((tile0 + t) * KC + c) * 512 + lane;
+      const f16x8 *p = Xv + (tile0 * KC + gl) * 512 + lane;  // the wave's chunks are contiguous
 #pragma unroll
-      for (int i = 0; i < 8; ++i) b[i] = p[i * 64];
+      for (int i = 0; i < 8; ++i) b[i] = K1S_NT ? __builtin_nontemporal_load(p + i * 64) : p[i * 64];
     };
 #pragma unroll
     for (int p = 0; p < R - 1; ++p) load(xb[p], p);
