@@ -446,31 +446,30 @@ __device__ __attribute__((always_inline)) inline void coarse_epilogue(const f32x
 #pragma unroll
         for (int r = 0; r < 4; ++r) mx = fmaxf(mx, acc[rt][qt][r]);
       if (__ballot(1.0f - mx <= sd[qt]) == 0) continue;  // no row of the tile under any seed
-      uint32_t hm = 0;
-#pragma unroll
-      for (int rt = 0; rt < 4; ++rt)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) hm |= (1.0f - acc[rt][qt][r] <= sd[qt] ? 1u : 0u) << (rt * 4 + r);
-      hm &= live16;
-      const uint32_t cnt = (uint32_t)__popc(hm);
-      uint32_t incl = cnt;  // inclusive scan over g of the lanes j, j + 16, j + 32, j + 48
-      uint32_t t = (uint32_t)__shfl_up((int)incl, 16);
-      if (g >= 1) incl += t;
-      t = (uint32_t)__shfl_up((int)incl, 32);
-      if (g >= 2) incl += t;
-      const uint32_t tot = (uint32_t)__shfl((int)incl, 48 + j);
-      uint32_t slot = (uint32_t)__shfl((int)qcnt[qt], j) + incl - cnt;
+#ifdef K1C_NOHIT
+      if (sd[qt] < 1e30f) continue;  // timing ablation only: never append
+#endif
+      // Append every live row under the seed, position by position (static register indices):
+      // one ballot per position tells which of the 64 lanes hit; the slot of a hit is the query's
+      // running count plus the hits of the same query's lower lanes (g' < g) at this position --
+      // popcounts of the ballot under per-lane masks, so no cross-lane shuffles (LDS round trips)
+      // are needed.  All 4 lanes of query j keep identical copies of its count.
+      const uint64_t m_all = 0x0001000100010001ull << j;           // lanes (g', j), g' = 0..3
+      const uint64_t m_low = m_all & ((1ull << (16 * g)) - 1ull);  // lanes (g' < g, j)
+      uint32_t run = qcnt[qt];
       uint64_t *d = dst0 + (int64_t)qt * 16 * kCBufCap;
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {  // static register indices; a wave-uniform skip per position
-        const bool hit = (hm >> i) & 1u;
-        if (__ballot(hit) == 0) continue;
+      for (int i = 0; i < 16; ++i) {
+        const bool hit = (1.0f - acc[i >> 2][qt][i & 3] <= sd[qt]) && ((live16 >> i) & 1u);
+        const uint64_t B = __ballot(hit);
+        if (B == 0) continue;  // wave-uniform
+        const uint32_t slot = run + (uint32_t)__popcll(B & m_low);
         if (hit && slot < (uint32_t)kCBufCap)
           d[slot] = ((uint64_t)f32_order(1.0f - acc[i >> 2][qt][i & 3]) << 32) |
                     (uint64_t)(uint32_t)(row0 + (i >> 2) * 16 + 4 * g + (i & 3));
-        slot += hit ? 1u : 0u;
+        run += (uint32_t)__popcll(B & m_all);
       }
-      if (g == 0) qcnt[qt] += tot;
+      qcnt[qt] = run;
     }
   }
 }
@@ -580,7 +579,7 @@ __global__ void __launch_bounds__(64 * W, 1)
           *qsrc(KR + c, f >> 1, f & 1);
   // per-lane seeds of the lane's QT queries (qt*16 + j)
   float sd[QT], best[QT];
-  uint32_t qcnt[QT];  // lanes g == 0: candidates appended for query qt*16 + j
+  uint32_t qcnt[QT];  // candidates appended for query qt*16 + j (same value in its 4 lanes)
 #pragma unroll
   for (int qt = 0; qt < QT; ++qt) {
     best[qt] = __builtin_inff();
@@ -729,12 +728,13 @@ __global__ void __launch_bounds__(64 * W, 1)
             mf(0, m);
             __builtin_amdgcn_sched_barrier(0);
             if (m < 4 && !(dbg & 2048)) xf[2 + m / 2][m % 2] = frag(gc, 2 + m / 2, m % 2);  // bit 11: ablation
-            if (m == MH - PCS - 2) {
+            const int w0 = MH - PCS - 2;
+            if (m == w0) {
               asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(PCS * (RING - 2)) : "memory");
               if (!(dbg & 512)) __builtin_amdgcn_s_barrier();  // bit 9: ablation only (races)
             }
-            if (m >= MH - PCS - 1 && m < MH - 1 && !(dbg & 1024))  // bit 10: ablation only (stale data)
-              issue_piece(gc + RING, m - (MH - PCS - 1));
+            if (m > w0 && m <= w0 + PCS && !(dbg & 1024))  // bit 10: ablation only (stale data)
+              issue_piece(gc + RING, m - w0 - 1);
             __builtin_amdgcn_sched_barrier(0);
           }
 #pragma unroll
