@@ -946,6 +946,8 @@ struct cm_bm25 {
   int64_t log_n = -1;
   DevBuf head_maxtf, range_mindl;  // pruned search: per-(head, range) max tf, per-range min length
   DevBuf blk_maxtf, blk_mindl;     // the same per 64-doc block
+  DevBuf blk_maxr;                 // per (head, 64-doc block): ceil-quantised max ratio tf.2.5/(tf + K_d)
+  double maxr_avgdl = 0.0;         // ... at this avgdl: a valid bound for every search avgdl <= it
   int32_t path = 0;                // 0 auto (pruned), 1 full K2 scan, 2 pruned
   int32_t last_rescored = 0;       // (query, range) pairs K2 re-scored in the last host search
   int32_t nhead = 0;
@@ -1087,6 +1089,16 @@ int build_head_tiles(cm_bm25 *h, const std::vector<int32_t> &df) {
     hipLaunchKernelGGL(bm25_blk_max_kernel, dim3((unsigned)ceil_div((int64_t)h->nhead * nblk, 256)), dim3(256), 0,
                        h->stream, h->headtf.as<uint8_t>(), h->npad, nblk, h->nhead, h->blk_maxtf.as<uint8_t>());
     CM_HIP(hipGetLastError());
+    // the ratio bound per (head, block) at 1.05 x the current avgdl (the ratio grows with avgdl, so
+    // it also bounds searches whose avgdl is somewhat larger: other shards' global statistics)
+    h->maxr_avgdl = h->avgdl > 0.0 ? h->avgdl * 1.05 : 0.0;
+    if (h->maxr_avgdl > 0.0) {
+      if ((rc = h->blk_maxr.ensure((size_t)h->nhead * nblk))) return rc;
+      hipLaunchKernelGGL(bm25_blk_maxratio_kernel, dim3((unsigned)ceil_div((int64_t)h->nhead * nblk, 256)),
+                         dim3(256), 0, h->stream, h->headtf.as<uint8_t>(), h->npad, h->dl.as<int32_t>(), h->ndocs,
+                         nblk, h->nhead, h->maxr_avgdl, h->blk_maxr.as<uint8_t>());
+      CM_HIP(hipGetLastError());
+    }
   }
   CM_HIP(hipStreamSynchronize(h->stream));
   return CM_OK;
@@ -1208,7 +1220,9 @@ int bm25_launch_core(cm_bm25 *h, const int32_t *q_terms_dev, const int32_t *q_of
     CM_HIP(hipMemsetAsync(w.item_count, 0, 4, st));
     hipLaunchKernelGGL(bm25_plan_kernel, dim3((unsigned)ceil_div(nqg * nr, 256)), dim3(256), 0, st, q_terms_dev,
                        q_off_dev, nq, h->vocab, w.q_idf, head_id, h->head_maxtf.as<uint8_t>(),
-                       h->range_mindl.as<int32_t>(), h->blk_maxtf.as<uint8_t>(), h->blk_mindl.as<int32_t>(), nr,
+                       h->range_mindl.as<int32_t>(), h->blk_maxtf.as<uint8_t>(), h->blk_mindl.as<int32_t>(),
+                       (h->nhead && h->maxr_avgdl > 0.0) ? h->blk_maxr.as<uint8_t>() : (const uint8_t *)nullptr,
+                       h->maxr_avgdl, nr,
                        (int64_t)nr * (kRange / 64), avgdl, k, score_dev, row_dev, w.need, w.items, w.item_count,
                        w.qcand);
     CM_HIP(hipGetLastError());
@@ -1252,7 +1266,7 @@ int32_t count_rescored(cm_bm25 *h, int nq, const BmWs &w, hipStream_t st) {
 void bm25_free(cm_bm25 *h) {
   for (DevBuf *b : {&h->term_off, &h->post_doc, &h->post_tf, &h->post_pos, &h->dl, &h->live, &h->idf, &h->ws,
                     &h->qbuf, &h->obuf, &h->allow_buf, &h->tmp, &h->headtf, &h->head_id, &h->head_maxtf,
-                    &h->range_mindl, &h->blk_maxtf, &h->blk_mindl})
+                    &h->range_mindl, &h->blk_maxtf, &h->blk_mindl, &h->blk_maxr})
     b->release();
 }
 

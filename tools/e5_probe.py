@@ -7,7 +7,8 @@ import torch  # noqa: E402
 from classmate_hip.embeddings import E5MultilingualEmbedder  # noqa: E402
 
 B, S = 256, 24
-emb = E5MultilingualEmbedder.random_init(seed=0, device="cuda")
+import os  # noqa: E402
+emb = E5MultilingualEmbedder.random_init(seed=0, device="cuda", dtype=os.environ.get("E5_DTYPE", "bfloat16"))
 g = torch.Generator(device="cuda").manual_seed(13)
 ids = torch.randint(5, 250002, (B, S), device="cuda", generator=g)
 mask = torch.ones_like(ids)
