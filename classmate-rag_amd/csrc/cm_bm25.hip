@@ -147,7 +147,8 @@ __global__ void bm25_bounds_kernel(const int32_t *__restrict__ q_terms, int n_te
   int64_t *out = bounds + (int64_t)i * (nr + 1);
   const int r0 = g * kBoundsGroup;
   const int r1 = min(r0 + kBoundsGroup, nr + 1);
-  if (t < 0 || t >= vocab || !qcand[i]) {  // unknown or dense-tile term: no postings walk
+  if (t >= 0 && t < vocab && !qcand[i]) return;  // dense-tile term: no reader looks at its bounds
+  if (t < 0 || t >= vocab) {  // unknown term: empty lists (K2 reads them)
     for (int r = r0; r < r1; ++r) out[r] = 0;
     return;
   }
