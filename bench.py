@@ -438,16 +438,19 @@ def _bm25_roofline(bm25, q_terms, N, ms, traffic):
     """K2a (the pruned search's tail pass, its largest kernel) per launch, algorithmic bytes:
     every walked posting read once (4 B doc + 2 B tf) and, per posting, the candidate's doc
     length (4 B) and one tf byte per head term of its query.  Walked terms = non-head terms, or
-    the rarest head term of a query that has none (bm25_qcand_kernel); head terms = df > N/64
-    (the default tile policy).  K2a is latency/issue-bound, so this fraction is low by nature."""
+    the rarest head term of a query that has none (bm25_qcand_kernel); head terms = the tiles (the
+    num_head_terms highest-df terms, df > N/128 within 8 GiB by default)
+    K2a is latency/issue-bound, so this fraction is low by nature."""
     import numpy as np
     df, _ = bm25.term_stats()
+    nh = bm25.num_head_terms                       # the tiles: the nh highest-df terms
+    head_df = np.sort(df)[::-1][nh - 1] if nh > 0 else np.iinfo(np.int64).max
     qt = q_terms.view(-1, 8).cpu().numpy() if q_terms.numel() % 8 == 0 else q_terms.view(1, -1).cpu().numpy()
     bytes_ = 0.0
     for row in qt:
         row = row[(row >= 0) & (row < df.shape[0])]
         d = df[row].astype(np.float64)
-        head = d > N / 64.0
+        head = d >= head_df
         walked = d[~head] if (~head).any() else (np.array([d[head].min()]) if head.any() else d[:0])
         n_post = float(walked.sum())
         bytes_ += n_post * (6.0 + 4.0 + float(head.sum()))

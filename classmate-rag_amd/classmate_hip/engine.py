@@ -288,7 +288,7 @@ class BM25Index:
         out["dl"] = out["dl"][:n]
         return out
 
-    def set_head_policy(self, min_df_frac: float = 1.0 / 64, max_bytes: int = 8 << 30):
+    def set_head_policy(self, min_df_frac: float = 1.0 / 128, max_bytes: int = 8 << 30):
         """Dense tf tiles for high-df terms (same results; max_bytes=0 disables)."""
         L.check(L.fn["cm_bm25_set_head_policy"](self._h, float(min_df_frac), int(max_bytes)), "cm_bm25_set_head_policy")
 

@@ -20,7 +20,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--docs", type=int, default=10_000_000)
 ap.add_argument("--batch", type=int, default=256)
 ap.add_argument("--reps", type=int, default=5)
-ap.add_argument("--head-frac", type=float, default=1.0 / 64)
+ap.add_argument("--head-frac", type=float, default=1.0 / 128)
 ap.add_argument("--head-bytes", type=int, default=8 << 30)
 ap.add_argument("--paths", default="1,2", help="search strategies to time (1 full K2 scan, 2 pruned)")
 a = ap.parse_args()
