@@ -23,6 +23,7 @@ ap.add_argument("--reps", type=int, default=5)
 ap.add_argument("--head-frac", type=float, default=1.0 / 128)
 ap.add_argument("--head-bytes", type=int, default=8 << 30)
 ap.add_argument("--paths", default="1,2", help="search strategies to time (1 full K2 scan, 2 pruned)")
+ap.add_argument("--dbg", default="", help="comma list of CM_BM25_DEBUG values to sweep (ablation builds only)")
 a = ap.parse_args()
 tok, off = gen_tokens(a.docs, 1 << 20, 1.07, 120.0, seed=1500)
 b = engine.BM25Index()
@@ -39,7 +40,12 @@ print(f"workload: mean head terms/query {head.sum(1).mean():.2f}, mean head df s
       f"mean tail df sum/query {(qdf * ~head).sum(1).mean():.4g}, distinct head terms in batch "
       f"{len(set(qh[head].tolist()))}, head tiles {b.num_head_terms}", flush=True)
 ref = None
-for path in [int(x) for x in a.paths.split(",")]:
+runs = [(int(p), None) for p in a.paths.split(",")]
+if a.dbg:
+    runs = [(int(a.paths.split(",")[-1]), d) for d in a.dbg.split(",")]
+for path, dbgv in runs:
+    if dbgv is not None:
+        os.environ["CM_BM25_DEBUG"] = dbgv
     b.set_path(path)
     ws = torch.empty(b.workspace_bytes(a.batch, q_terms.numel(), 10), dtype=torch.uint8, device="cuda")
     out = b.search_dev(q_terms, q_off, 10, workspace=ws)
