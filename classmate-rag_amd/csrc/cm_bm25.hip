@@ -40,6 +40,14 @@ constexpr int kBmThreads = 256;              // 4 waves = 4 queries per K2 workg
 constexpr int kBoundsGroup = 8;              // ranges per bounds thread (gallop between them)
 constexpr int kMergeThreads = 1024;
 constexpr int kMergePer = 16;                // lists per merge thread -> <= 16384 ranges (16.7M docs)
+constexpr int kTermLanesQd = 16;             // K2b descriptor slots per query (== kTermLanes)
+
+// Candidate lists, one per (query, range), k slots each: slot 0 of every list of query q lies
+// contiguous at [q * nr + r] (the merge's first read of all lists is coalesced), slots 1..k-1 of
+// a list contiguous after the heads, at nl + (q * nr + r) * (k - 1) + j - 1 (nl = nq * nr lists).
+__device__ inline int64_t lslot(int64_t list, int64_t nl, int k, int j) {
+  return j == 0 ? list : nl + list * (int64_t)(k - 1) + (j - 1);
+}
 
 struct PairKey {  // (k, r) lexicographic; smaller is better
   uint64_t k;
@@ -107,9 +115,16 @@ __device__ inline int64_t lower_bound_doc(const int32_t *__restrict__ post_doc, 
 // generators): every known non-head term, and — when designate is set and a query has no such
 // term — every occurrence of its rarest head term (lowest df, then first in query order), so
 // that the pruned search has tail candidates, hence a threshold, for all-head queries too.
+// qd_* (when qd_code is set): K2b's per-query term descriptors, so a planned item needs one
+// dependent load level instead of q_off -> q_terms -> head_id: qd_code[q][j] = (head id + 1,
+// 0 = not a head) | walked << 30 for the first kTermLanes terms (0 past the end), qd_idf the
+// term's idf (0 past the end), qd_tb[q] = q_off[q], qd_len[q] = the query's term count.
 __global__ void bm25_qcand_kernel(const int32_t *__restrict__ q_terms, const int32_t *__restrict__ q_off, int nq,
                                   int32_t vocab, const int32_t *__restrict__ head_id,
-                                  const int64_t *__restrict__ term_off, int designate, uint8_t *__restrict__ qcand) {
+                                  const int64_t *__restrict__ term_off, int designate, uint8_t *__restrict__ qcand,
+                                  const double *__restrict__ q_idf, int32_t *__restrict__ qd_code,
+                                  double *__restrict__ qd_idf, int32_t *__restrict__ qd_tb,
+                                  int32_t *__restrict__ qd_len) {
   const int q = blockIdx.x * blockDim.x + threadIdx.x;
   if (q >= nq) return;
   const int tb = q_off[q], te = q_off[q + 1];
@@ -133,6 +148,24 @@ __global__ void bm25_qcand_kernel(const int32_t *__restrict__ q_terms, const int
   if (designate && !any && best_t >= 0)
     for (int i = tb; i < te; ++i)
       if (q_terms[i] == best_t) qcand[i] = 1;
+  if (!qd_code) return;
+  qd_tb[q] = tb;
+  qd_len[q] = te - tb;
+  for (int j = 0; j < kTermLanesQd; ++j) {
+    const int i = tb + j;
+    int32_t c = 0;
+    double f = 0.0;
+    if (i < te) {
+      const int32_t t = q_terms[i];
+      if (t >= 0 && t < vocab) {
+        c = (head_id ? head_id[t] : -1) + 1;
+        if (qcand[i]) c |= 1 << 30;
+      }
+      f = q_idf[i];
+    }
+    qd_code[(int64_t)q * kTermLanesQd + j] = c;
+    qd_idf[(int64_t)q * kTermLanesQd + j] = f;
+  }
 }
 
 __global__ void bm25_bounds_kernel(const int32_t *__restrict__ q_terms, int n_terms, int32_t vocab, int nr,
@@ -208,6 +241,7 @@ constexpr int kLutW = 128;
 constexpr int kLutTF = 16;
 constexpr int kQPerWave = 4;    // queries per wave; lanes 16q..16q+15 hold query q's first 16 term descriptors
 constexpr int kTermLanes = 64 / kQPerWave;
+static_assert(kTermLanesQd == kTermLanes, "K2b descriptors cover a wave's term lanes");
 #ifndef K2_WAVES_PER_EU
 #define K2_WAVES_PER_EU 2
 #endif
@@ -600,7 +634,7 @@ __global__ void __launch_bounds__(kBmThreads) __attribute__((amdgpu_waves_per_eu
         wave_min_pair(mk, mr);
         if (mr == 0xffffffffu || mk > T) break;  // nothing left that can enter the global top-k
         if (lane == 0) {
-          const int64_t o = ((int64_t)qi * nr + r) * k + i;
+          const int64_t o = lslot((int64_t)qi * nr + r, (int64_t)nq * nr, k, i);
           cand_key[o] = mk;
           cand_row[o] = mr;
         }
@@ -620,7 +654,7 @@ __global__ void __launch_bounds__(kBmThreads) __attribute__((amdgpu_waves_per_eu
         }
       }
       for (int j = i + lane; j < k; j += 64) {
-        const int64_t o = ((int64_t)qi * nr + r) * k + j;
+        const int64_t o = lslot((int64_t)qi * nr + r, (int64_t)nq * nr, k, j);
         cand_key[o] = kEmptyKey;
         cand_row[o] = 0xffffffffu;
       }
@@ -670,7 +704,7 @@ __global__ void bm25_head_sat_kernel(const int32_t *__restrict__ cand, int ncand
   if (__any(any) && (threadIdx.x & 63) == 0) atomicOr(sat + c, 1);
 }
 
-// Tournament merge of nr sorted per-range lists per query.
+// Tournament merge of nr sorted per-range lists per query (one workgroup per query, gridDim.x = nq).
 __global__ void __launch_bounds__(kMergeThreads) bm25_merge_kernel(const uint64_t *__restrict__ cand_key,
                                                                    const uint32_t *__restrict__ cand_row, int nr,
                                                                    int k, double *__restrict__ out_score,
@@ -681,7 +715,8 @@ __global__ void __launch_bounds__(kMergeThreads) bm25_merge_kernel(const uint64_
   int head[kMergePer];
   uint64_t hk[kMergePer];
   uint32_t hr[kMergePer];
-  const int64_t base = (int64_t)qi * nr * k;
+  const int64_t base = (int64_t)qi * nr;  // list id of (qi, range 0)
+  const int64_t nl = (int64_t)gridDim.x * nr;
 #pragma unroll
   for (int s = 0; s < kMergePer; ++s) {
     const int l = threadIdx.x + kMergeThreads * s;
@@ -689,8 +724,8 @@ __global__ void __launch_bounds__(kMergeThreads) bm25_merge_kernel(const uint64_
     hk[s] = kEmptyKey;
     hr[s] = 0xffffffffu;
     if (l < nr) {
-      hk[s] = cand_key[base + (int64_t)l * k];
-      hr[s] = cand_row[base + (int64_t)l * k];
+      hk[s] = cand_key[base + l];
+      hr[s] = cand_row[base + l];
     }
   }
   for (int i = 0; i < k; ++i) {
@@ -720,8 +755,8 @@ __global__ void __launch_bounds__(kMergeThreads) bm25_merge_kernel(const uint64_
         const int l = threadIdx.x + kMergeThreads * s;
         head[s] += 1;
         if (head[s] < k) {
-          hk[s] = cand_key[base + (int64_t)l * k + head[s]];
-          hr[s] = cand_row[base + (int64_t)l * k + head[s]];
+          hk[s] = cand_key[lslot(base + l, nl, k, head[s])];
+          hr[s] = cand_row[lslot(base + l, nl, k, head[s])];
         } else {
           hk[s] = kEmptyKey;
           hr[s] = 0xffffffffu;
@@ -1132,6 +1167,10 @@ struct BmWs {
   uint8_t *need;  // [query groups][ranges] re-score bits (pruned search)
   uint64_t *items;  // K2b work items (pruned search)
   uint8_t *qcand;   // per query term: postings walked
+  int32_t *qd_code;  // [nq][kTermLanes] K2b term descriptors (bm25_qcand_kernel)
+  double *qd_idf;
+  int32_t *qd_tb;
+  int32_t *qd_len;
   uint32_t *item_count;
   double *avgdl;    // the search's avgdl (unfiltered, host-computed or device-computed statistics)
   int64_t *stats;   // filtered entry: {Nc, sum of candidate lengths}
@@ -1170,6 +1209,14 @@ BmWs bm_ws_layout(const cm_bm25 *h, int nq, int total_terms, int k, void *base) 
   off += 256;
   w.df = reinterpret_cast<int64_t *>(p + off);
   off += round_up((int64_t)std::max(total_terms, 1) * 8, 256);
+  w.qd_code = reinterpret_cast<int32_t *>(p + off);
+  off += round_up((int64_t)std::max(nq, 1) * kTermLanes * 4, 256);
+  w.qd_idf = reinterpret_cast<double *>(p + off);
+  off += round_up((int64_t)std::max(nq, 1) * kTermLanes * 8, 256);
+  w.qd_tb = reinterpret_cast<int32_t *>(p + off);
+  off += round_up((int64_t)std::max(nq, 1) * 4, 256);
+  w.qd_len = reinterpret_cast<int32_t *>(p + off);
+  off += round_up((int64_t)std::max(nq, 1) * 4, 256);
   w.total = off;
   return w;
 }
@@ -1186,7 +1233,8 @@ int bm25_launch_core(cm_bm25 *h, const int32_t *q_terms_dev, const int32_t *q_of
   if (nb > 0) {
     hipLaunchKernelGGL(bm25_qcand_kernel, dim3((unsigned)ceil_div(nq, 256)), dim3(256), 0, st, q_terms_dev, q_off_dev,
                        nq, h->vocab, h->nhead ? h->head_id.as<int32_t>() : (const int32_t *)nullptr,
-                       h->term_off.as<int64_t>(), (int)prune, w.qcand);
+                       h->term_off.as<int64_t>(), (int)prune, w.qcand, w.q_idf, prune ? w.qd_code : nullptr,
+                       w.qd_idf, w.qd_tb, w.qd_len);
     CM_HIP(hipGetLastError());
     hipLaunchKernelGGL(bm25_bounds_kernel, dim3((unsigned)ceil_div(nb, 256)), dim3(256), 0, st, q_terms_dev,
                        total_terms, h->vocab, nr, h->term_off.as<int64_t>(), h->post_doc.as<int32_t>(), w.qcand,
@@ -1220,19 +1268,18 @@ int bm25_launch_core(cm_bm25 *h, const int32_t *q_terms_dev, const int32_t *q_of
                        score_dev, row_dev);
     CM_HIP(hipGetLastError());
     CM_HIP(hipMemsetAsync(w.item_count, 0, 4, st));
-    hipLaunchKernelGGL(bm25_plan_kernel, dim3((unsigned)ceil_div(nqg * nr, 256)), dim3(256), 0, st, q_terms_dev,
-                       q_off_dev, nq, h->vocab, w.q_idf, head_id, h->head_maxtf.as<uint8_t>(),
+    hipLaunchKernelGGL(bm25_plan_kernel, dim3((unsigned)ceil_div(nqg * nr, 256)), dim3(256), 0, st, w.qd_code,
+                       w.qd_idf, w.qd_len, nq, (int)(head_id != nullptr), h->head_maxtf.as<uint8_t>(),
                        h->range_mindl.as<int32_t>(), h->blk_maxtf.as<uint8_t>(), h->blk_mindl.as<int32_t>(),
                        (h->nhead && h->maxr_avgdl > 0.0) ? h->blk_maxr.as<uint8_t>() : (const uint8_t *)nullptr,
-                       h->maxr_avgdl, nr,
-                       (int64_t)nr * (kRange / 64), avgdl, k, score_dev, row_dev, w.need, w.items, w.item_count,
-                       w.qcand);
+                       h->maxr_avgdl, nr, (int64_t)nr * (kRange / 64), avgdl, k, score_dev, row_dev, w.need, w.items,
+                       w.item_count);
     CM_HIP(hipGetLastError());
     // K2b: head-only documents of the planned blocks, merged into the tail pass's lists
-    hipLaunchKernelGGL(bm25_block_kernel, dim3(2048), dim3(256), 0, st, w.items, w.item_count, q_terms_dev,
-                       q_off_dev, h->vocab, w.q_idf, w.bounds, nr, h->post_doc.as<int32_t>(), head_id,
-                       h->headtf.as<uint8_t>(), h->npad, h->dl.as<int32_t>(), h->live.as<uint32_t>(), allow_dev,
-                       h->ndocs, avgdl, k, score_dev, w.cand_key, w.cand_row, w.qcand);
+    hipLaunchKernelGGL(bm25_block_kernel, dim3(2048), dim3(256), 0, st, w.items, w.item_count, w.qd_code,
+                       w.qd_idf, w.qd_tb, w.bounds, nr, h->post_doc.as<int32_t>(), h->headtf.as<uint8_t>(), h->npad,
+                       h->dl.as<int32_t>(), h->live.as<uint32_t>(), allow_dev, h->ndocs, avgdl, k, score_dev, nq,
+                       w.cand_key, w.cand_row);
     CM_HIP(hipGetLastError());
   }
   hipLaunchKernelGGL(bm25_range_kernel<uint16_t>, dim3((unsigned)nblk), dim3(kBmThreads), 0, st, q_terms_dev,
