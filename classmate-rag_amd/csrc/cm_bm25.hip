@@ -1221,6 +1221,9 @@ BmWs bm_ws_layout(const cm_bm25 *h, int nq, int total_terms, int k, void *base) 
   return w;
 }
 
+#ifndef K2B_GRID
+#define K2B_GRID 2048  // K2b workgroups (grid-stride over the planned items)
+#endif
 // Launch K2 + merge given q_idf and *avgdl already in the workspace.
 int bm25_launch_core(cm_bm25 *h, const int32_t *q_terms_dev, const int32_t *q_off_dev, int nq, int total_terms, int k,
                      const uint32_t *allow_dev, const BmWs &w, double *score_dev, int64_t *row_dev, hipStream_t st) {
@@ -1276,7 +1279,7 @@ int bm25_launch_core(cm_bm25 *h, const int32_t *q_terms_dev, const int32_t *q_of
                        w.item_count);
     CM_HIP(hipGetLastError());
     // K2b: head-only documents of the planned blocks, merged into the tail pass's lists
-    hipLaunchKernelGGL(bm25_block_kernel, dim3(2048), dim3(256), 0, st, w.items, w.item_count, w.qd_code,
+    hipLaunchKernelGGL(bm25_block_kernel, dim3(K2B_GRID), dim3(256), 0, st, w.items, w.item_count, w.qd_code,
                        w.qd_idf, w.qd_tb, w.bounds, nr, h->post_doc.as<int32_t>(), h->headtf.as<uint8_t>(), h->npad,
                        h->dl.as<int32_t>(), h->live.as<uint32_t>(), allow_dev, h->ndocs, avgdl, k, score_dev, nq,
                        w.cand_key, w.cand_row);
