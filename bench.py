@@ -431,6 +431,11 @@ def _dense_roofline(kind, N, D, B, ms, traffic):
     r.update(traffic=traffic, kernel=DENSE_KINDS[kind], avg_launch_ms=ms,
              algorithmic_per_launch=dict(bytes=bytes_, flops=flops, rows=N, queries=B, dim=D),
              fp32_equivalent_GBps=N * D * 4 / (ms * 1e-3) / 1e9)
+    # the other side of the same launch: at B = 256 the f16 scan's intensity (B flop/B = 256) sits
+    # just under the nominal ridge (2.5 PF / 8 TB/s = 312), and under the chip's power limit the
+    # MFMA clock drops, so the MFMA side is reported beside the HBM fraction
+    r["mfma_side"] = dict(achieved=flops / (ms * 1e-3) / 1e12, peak=peak, unit="TFLOP/s",
+                          frac=flops / (ms * 1e-3) / 1e12 / peak)
     return r
 
 
