@@ -518,6 +518,55 @@ def test_bm25_pruned_skips_ranges_and_matches_full_scan(eng):
     assert all(int(r) % 3 == 0 for r in f2[1].ravel() if r >= 0)
 
 
+@pytest.mark.gpu
+def test_bm25_pruned_ties_at_threshold(eng):
+    """The pruned search's fp32 pre-bounds (planner, K2a, K2b: a candidate is dropped only when an
+    inflated fp32 upper bound of its score is below the query's threshold T) must keep every
+    document whose exact score equals T.  300 identical copies of a tail + head template and 300
+    of a head-only template, spread over ~120 ranges, put hundreds of exact ties at the k-th
+    score (broken by row).  Both paths equal the C oracle bit for bit for k = 1, 10, 64."""
+    from oracle import corc
+    rng = np.random.default_rng(44)
+    nd, vocab = 120_000, 6000
+    lens = np.maximum(rng.poisson(25, nd), 1)
+    docs_a = rng.choice(nd, 300, replace=False)
+    docs_b = rng.choice(np.setdiff1d(np.arange(nd), docs_a), 300, replace=False)
+    lens[docs_a] = 8
+    lens[docs_b] = 8
+    off = np.zeros(nd + 1, np.int64)
+    off[1:] = np.cumsum(lens)
+    p = 1.0 / np.arange(1, vocab + 1) ** 1.05
+    toks = rng.choice(vocab, size=int(off[-1]), p=p / p.sum()).astype(np.int32)
+    tmpl_a = np.array([0, 1, 1, 2, 5000, 5001, 3, 0], np.int32)  # heads 0..3 + two rare terms
+    tmpl_b = np.array([0, 1, 2, 2, 3, 0, 1, 4], np.int32)        # head terms only
+    for d in docs_a:
+        toks[off[d]:off[d] + 8] = tmpl_a
+    for d in docs_b:
+        toks[off[d]:off[d] + 8] = tmpl_b
+    b = eng.BM25Index()
+    b.build(toks, off, vocab)
+    b.set_head_policy(1.0 / 128, 8 << 30)
+    assert b.num_head_terms >= 5
+    queries = [[0, 1, 2, 3, 5000, 5001], [0, 1, 2, 3, 4], [5000, 0, 1], [2, 2, 0, 4, 1],
+               [5001, 3], [0, 1, 2, 3, 4, 5000], [4, 0]]
+    csr = corc.build_csr(toks, off, vocab)
+    idf, _ = corc.bm25_idf(csr["df"], csr["first_key"], nd)
+    avgdl = float(lens.sum()) / nd
+    for k in (1, 10, 64):
+        o_sc, o_rw = corc.bm25_topk(csr, idf, avgdl, queries, k)
+        b.set_path(1)
+        s1, r1, _ = b.search(queries, k)
+        b.set_path(2)
+        s2, r2, _ = b.search(queries, k)
+        assert np.array_equal(r1, r2) and np.array_equal(s1, s2), k
+        for i in range(len(queries)):
+            assert r2[i][:k].tolist() == o_rw[i].tolist(), (k, i)
+            assert s2[i][:k].tolist() == o_sc[i].tolist(), (k, i)
+    # the tail + head template query really is tie-bound: its top 64 share one score
+    o_sc, _ = corc.bm25_topk(csr, idf, avgdl, queries[:1], 64)
+    assert len(set(o_sc[0].tolist())) == 1
+
+
 @pytest.mark.parametrize("D", [768, 1024, 20, 2048])
 def test_add_layernorm_matches_torch(eng, D):
     """cm_add_layernorm == F.layer_norm(x + r) (torch fp32 reference of the same op)."""
