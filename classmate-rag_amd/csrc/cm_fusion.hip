@@ -101,7 +101,8 @@ __global__ void __launch_bounds__(kMmrThreads) mmr_kernel(const float *__restric
 constexpr int kMmrLdsPool = 32;
 constexpr int kMmrLdsDim = 1024;
 
-__global__ void __launch_bounds__(kMmrThreads) mmr_lds_kernel(const float *__restrict__ q, const float *__restrict__ cands,
+constexpr int kMmrLdsThreads = 1024;  // 16 waves: the (n+1) n similarity pairs (600 at 24) in one pass
+__global__ void __launch_bounds__(kMmrLdsThreads) mmr_lds_kernel(const float *__restrict__ q, const float *__restrict__ cands,
                                                               const int32_t *__restrict__ n_valid, int pool, int dim,
                                                               int k, float lam32, float oml32,
                                                               int32_t *__restrict__ out_order) {
@@ -112,17 +113,32 @@ __global__ void __launch_bounds__(kMmrThreads) mmr_lds_kernel(const float *__res
   const int qi = blockIdx.x;
   const int n = min(n_valid ? n_valid[qi] : pool, pool);
   const int kk = min(k, n);
-  for (int i = threadIdx.x; i < k; i += kMmrThreads) out_order[(int64_t)qi * k + i] = -1;
+  for (int i = threadIdx.x; i < k; i += kMmrLdsThreads) out_order[(int64_t)qi * k + i] = -1;
   if (n <= 0) return;  // uniform
   const float *cv = cands + (int64_t)qi * pool * dim;
   const float *qv = q + (int64_t)qi * dim;
-  for (int t = threadIdx.x; t < (n + 1) * dim; t += kMmrThreads) {
-    const int r = t / dim, d = t - r * dim;
-    rows[r * ld + d] = r < n ? cv[(int64_t)r * dim + d] : qv[d];
+  if ((dim & 3) == 0 && ((reinterpret_cast<uintptr_t>(cands) | reinterpret_cast<uintptr_t>(q)) & 15) == 0) {
+    // 16-B global loads (every row 16-B aligned), scalar LDS stores (odd pitch)
+    const int d4 = dim >> 2;
+    for (int t = threadIdx.x; t < (n + 1) * d4; t += kMmrLdsThreads) {
+      const int r = t / d4, d = (t - r * d4) * 4;
+      const float4 v = *reinterpret_cast<const float4 *>((r < n ? cv + (int64_t)r * dim : qv) + d);
+      float *o = rows + r * ld + d;
+      o[0] = v.x;
+      o[1] = v.y;
+      o[2] = v.z;
+      o[3] = v.w;
+    }
+  } else {
+    for (int t = threadIdx.x; t < (n + 1) * dim; t += kMmrLdsThreads) {
+      const int r = t / dim, d = t - r * dim;
+      rows[r * ld + d] = r < n ? cv[(int64_t)r * dim + d] : qv[d];
+    }
   }
   __syncthreads();
-  // pairs (i, j), i <= n (row n = the query), j < n, j <= i or i == n
-  for (int p = threadIdx.x; p < (n + 1) * n; p += kMmrThreads) {
+  // pairs (i, j), i <= n (row n = the query), j < n, j <= i or i == n; each dot in dimension
+  // order with an fp64 accumulator (unchanged arithmetic: one pair per thread)
+  for (int p = threadIdx.x; p < (n + 1) * n; p += kMmrLdsThreads) {
     const int i = p / n, j = p - i * n;
     if (i < n && j > i) continue;
     const float *a = rows + i * ld;
@@ -354,7 +370,7 @@ int cm_mmr_dev(const float *q_dev, const float *cands_dev, const int32_t *n_vali
                             hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)(((kMmrLdsPool + 1) * (kMmrLdsDim + 1) + (kMmrLdsPool + 1) * kMmrLdsPool) * 4));
     CM_HIP(attr);
-    hipLaunchKernelGGL(mmr_lds_kernel, dim3(nq), dim3(kMmrThreads), lds, (hipStream_t)stream, q_dev, cands_dev,
+    hipLaunchKernelGGL(mmr_lds_kernel, dim3(nq), dim3(kMmrLdsThreads), lds, (hipStream_t)stream, q_dev, cands_dev,
                        n_valid_dev, pool, dim, k, lam32, oml32, order_dev);
     CM_HIP(hipGetLastError());
     return CM_OK;
