@@ -77,7 +77,7 @@ def parse_args():
     ap.add_argument("--e2e-words", type=int, default=40, help="e2e mode: words per synthetic chunk")
     ap.add_argument("--e2e-latency-queries", type=int, default=32, help="e2e mode: single-query retrieve() calls timed")
     ap.add_argument("--cpu-baseline", type=int, default=1)
-    ap.add_argument("--cpu-queries", type=int, default=64)
+    ap.add_argument("--cpu-queries", type=int, default=128)
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--out", default=None, help="also write the JSON line to this file")
     return ap.parse_args()
