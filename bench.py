@@ -225,6 +225,8 @@ def main():
     dout = (torch.empty((B, P), dtype=torch.float32, device=dev), torch.empty((B, P), dtype=torch.int64, device=dev))
     vbuf = torch.empty((B * P, D), dtype=torch.float32, device=dev)
     obuf = torch.empty((B, K), dtype=torch.int32, device=dev)
+    pbuf = (torch.empty((B, K), dtype=torch.int64, device=dev), torch.empty((B, K), dtype=torch.float32, device=dev),
+            torch.empty((B,), dtype=torch.int32, device=dev), torch.empty((B,), dtype=torch.int32, device=dev))
     if bm25 is not None:
         bws = torch.empty(bm25.workspace_bytes(B, q_terms.numel(), K), dtype=torch.uint8, device=dev)
         bout = (torch.empty((B, K), dtype=torch.float64, device=dev), torch.empty((B, K), dtype=torch.int64, device=dev))
@@ -286,10 +288,6 @@ def main():
             rg = r
             vecs = dense.gather_dev(r.reshape(-1), out=vbuf).view(B, P, D)
         order = engine.mmr_dev(q, vecs, K, 0.5, out=obuf)
-        o = order.long().clamp(min=0)
-        vk = torch.gather(rg, 1, o)
-        vd = torch.gather(d, 1, o)
-        vn = (order >= 0).sum(1, dtype=torch.int32)
         main.wait_stream(side)
         if record:
             ev.append(e)
@@ -298,8 +296,9 @@ def main():
             bs, brg = parallel.merge_bm25_topk(bs, brg, K)
         else:
             brg = br
-        bn = (brg >= 0).sum(1, dtype=torch.int32)
-        return engine.rrf_merge_dev(vk.contiguous(), vd.contiguous(), vn, brg.contiguous(), bs.contiguous(), bn,
+        # MMR-ordered vector list + list counts in one device pass, then the fused merge
+        vk, vd, vn, bn = engine.rrf_pool_prep_dev(rg.contiguous(), d.contiguous(), order, brg.contiguous(), out=pbuf)
+        return engine.rrf_merge_dev(vk, vd, vn, brg.contiguous(), bs.contiguous(), bn,
                                     w_vec=1.0, w_bm25=1.0, rrf_k=60, top_k=K)
 
     for _ in range(args.warmup):

@@ -109,6 +109,8 @@ SIGNATURES = {
     "cm_rrf_fuse": (c_int, c_vp, c_vp, c_i32, c_vp, c_i32, c_vp, c_vp, P(c_i32)),
     "cm_rrf_merge": (c_int, c_vp, c_vp, c_vp, c_i32, c_vp, c_vp, c_vp, c_i32, c_i32, c_f64, c_f64, c_i32, c_i32,
                      c_vp, c_vp, c_vp, c_vp, c_vp, c_vp),
+    "cm_rrf_pool_prep_dev": (c_int, c_vp, c_vp, c_i32, c_vp, c_i32, c_vp, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp,
+                             c_vp),
     "cm_rrf_merge_dev": (c_int, c_vp, c_vp, c_vp, c_i32, c_vp, c_vp, c_vp, c_i32, c_i32, c_f64, c_f64, c_i32, c_i32,
                          c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp),
     "cm_filter_eval": (c_int, c_vp, c_i32, c_vp, c_i32, c_vp, c_i32, c_i64, c_vp, c_vp, c_vp),

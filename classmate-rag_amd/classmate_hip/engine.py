@@ -545,6 +545,24 @@ def rrf_merge(vkeys, vdist, vn, bkeys, bscore, bn, *, w_vec: float, w_bm25: floa
     return ok, of, ov, ob, ofl, on
 
 
+def rrf_pool_prep_dev(pool_keys, pool_dist, order, bkeys, out=None):
+    """vkeys/vdist (MMR-ordered pool entries), vn, bn for rrf_merge_dev in one device pass
+    (cm_rrf_pool_prep_dev).  pool_keys int64 (nq, pool), pool_dist float32 (nq, pool), order int32
+    (nq, kv), bkeys int64 (nq, kb); all contiguous on one device."""
+    nq, pool = pool_keys.shape
+    kv, kb = order.shape[1], bkeys.shape[1]
+    dev = pool_keys.device
+    for t, dt in ((pool_keys, torch.int64), (pool_dist, torch.float32), (order, torch.int32), (bkeys, torch.int64)):
+        if t.dtype != dt or not t.is_contiguous() or t.device != dev or t.shape[0] != nq:
+            raise ValueError("rrf_pool_prep_dev: bad input tensor")
+    if out is None:
+        out = (torch.empty((nq, kv), dtype=torch.int64, device=dev), torch.empty((nq, kv), dtype=torch.float32, device=dev),
+               torch.empty((nq,), dtype=torch.int32, device=dev), torch.empty((nq,), dtype=torch.int32, device=dev))
+    L.check(L.fn["cm_rrf_pool_prep_dev"](L.ptr(pool_keys), L.ptr(pool_dist), pool, L.ptr(order), kv, L.ptr(bkeys), kb,
+                                         nq, *[L.ptr(t) for t in out], _stream(dev.index)), "cm_rrf_pool_prep_dev")
+    return out
+
+
 def rrf_merge_dev(vkeys, vdist, vn, bkeys, bscore, bn, *, w_vec, w_bm25, rrf_k, top_k, out=None):
     nq, kv = vkeys.shape
     kb = bkeys.shape[1]

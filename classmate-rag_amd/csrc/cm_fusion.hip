@@ -185,6 +185,30 @@ __global__ void __launch_bounds__(kMmrLdsThreads) mmr_lds_kernel(const float *__
   }
 }
 
+// The vector and BM25 lists of cm_rrf_merge_dev straight from the search outputs (one thread per
+// query): vkeys/vdist[q][i] = the MMR-ordered pool entries (pool_keys/pool_dist[q][order[q][i]]),
+// vn = the selected count (MMR pads its order with -1), bn = the BM25 list's valid count (rows
+// padded with -1) -- the gathers and counts the caller would otherwise run as separate ops.
+__global__ void rrf_pool_prep_kernel(const int64_t *__restrict__ pool_keys, const float *__restrict__ pool_dist,
+                                     int pool, const int32_t *__restrict__ order, int kv,
+                                     const int64_t *__restrict__ bkeys, int kb, int nq, int64_t *__restrict__ vkeys,
+                                     float *__restrict__ vdist, int32_t *__restrict__ vn, int32_t *__restrict__ bn) {
+  const int q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= nq) return;
+  int n = 0;
+  for (int i = 0; i < kv; ++i) {
+    const int32_t o = order[(int64_t)q * kv + i];
+    const bool ok = o >= 0 && o < pool;
+    vkeys[(int64_t)q * kv + i] = ok ? pool_keys[(int64_t)q * pool + o] : -1;
+    vdist[(int64_t)q * kv + i] = ok ? pool_dist[(int64_t)q * pool + o] : 0.f;
+    n += ok ? 1 : 0;
+  }
+  vn[q] = n;
+  int m = 0;
+  for (int i = 0; i < kb; ++i) m += bkeys[(int64_t)q * kb + i] >= 0 ? 1 : 0;
+  bn[q] = m;
+}
+
 // HybridRetriever.retrieve's merge for one query per lane.
 template <bool kLds>
 __global__ void rrf_merge_kernel(const int64_t *__restrict__ vkeys, const float *__restrict__ vdist,
@@ -407,6 +431,19 @@ int cm_mmr(const float *q, const float *cands, const int32_t *n_valid, int32_t n
   if (rc) return rc;
   CM_HIP(hipMemcpyAsync(out_order, dout, nqs * k * 4, hipMemcpyDeviceToHost, s.st));
   CM_HIP(hipStreamSynchronize(s.st));
+  return CM_OK;
+}
+
+int cm_rrf_pool_prep_dev(const int64_t *pool_keys, const float *pool_dist, int32_t pool, const int32_t *order,
+                         int32_t kv, const int64_t *bkeys, int32_t kb, int32_t nq, int64_t *vkeys, float *vdist,
+                         int32_t *vn, int32_t *bn, void *stream) {
+  if (nq <= 0) return CM_OK;
+  if (pool <= 0 || kv < 0 || kb < 0) CM_FAIL(CM_EINVAL, "bad RRF pool sizes");
+  if (!pool_keys || !pool_dist || !order || !bkeys || !vkeys || !vdist || !vn || !bn)
+    CM_FAIL(CM_EINVAL, "NULL argument");
+  hipLaunchKernelGGL(rrf_pool_prep_kernel, dim3((unsigned)ceil_div(nq, 64)), dim3(64), 0, (hipStream_t)stream,
+                     pool_keys, pool_dist, pool, order, kv, bkeys, kb, nq, vkeys, vdist, vn, bn);
+  CM_HIP(hipGetLastError());
   return CM_OK;
 }
 

@@ -292,6 +292,12 @@ int cm_rrf_fuse(const int64_t *keys, const int32_t *off, int32_t nl, const doubl
  * BM25 list (<= kb keys with fp64 score); outputs the top_k items sorted by
  * (fused, -distance or -0.0) descending, stable (vector items first).
  * out_flags bit0 = has vector distance, bit1 = has BM25 score.           */
+/* Inputs of cm_rrf_merge_dev from the device search outputs (fusion.py:132-153's vec_ids /
+ * bm_ids lists): vkeys/vdist[q][i] = pool_keys/pool_dist[q][order[q][i]] for the MMR order
+ * (-1 / 0 past the selected count), vn[q] = selected count, bn[q] = valid BM25 rows (>= 0).  */
+int cm_rrf_pool_prep_dev(const int64_t *pool_keys, const float *pool_dist, int32_t pool, const int32_t *order,
+                         int32_t kv, const int64_t *bkeys, int32_t kb, int32_t nq, int64_t *vkeys, float *vdist,
+                         int32_t *vn, int32_t *bn, void *stream);
 int cm_rrf_merge_dev(const int64_t *vkeys, const float *vdist, const int32_t *vn, int32_t kv,
                      const int64_t *bkeys, const double *bscore, const int32_t *bn, int32_t kb, int32_t nq,
                      double w_vec, double w_bm25, int32_t rrf_k, int32_t top_k, int64_t *out_keys,

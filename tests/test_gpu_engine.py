@@ -636,6 +636,31 @@ def test_short_attention_matches_torch(eng, S):
         eng.short_attention(torch.zeros(2, 65, 3 * H * 64, device="cuda"), H, 0.125)
 
 
+@pytest.mark.gpu
+def test_rrf_pool_prep_matches_torch_glue(eng):
+    """cm_rrf_pool_prep_dev == the torch ops it replaces in the batched step: the MMR-ordered pool
+    keys / distances (gather by order, -1 padding) and the valid counts of both lists."""
+    import torch
+    g = torch.Generator().manual_seed(3)
+    nq, pool, kv, kb = 37, 24, 10, 10
+    keys = torch.randint(0, 1 << 40, (nq, pool), generator=g, dtype=torch.int64)
+    dist = torch.rand((nq, pool), generator=g, dtype=torch.float32)
+    order = torch.stack([torch.randperm(pool, generator=g)[:kv] for _ in range(nq)]).to(torch.int32)
+    nsel = torch.randint(0, kv + 1, (nq,), generator=g)
+    order[torch.arange(kv).unsqueeze(0) >= nsel.unsqueeze(1)] = -1
+    bkeys = torch.randint(0, 1 << 40, (nq, kb), generator=g, dtype=torch.int64)
+    nb = torch.randint(0, kb + 1, (nq,), generator=g)
+    bkeys[torch.arange(kb).unsqueeze(0) >= nb.unsqueeze(1)] = -1
+    dv = [t.cuda() for t in (keys, dist, order, bkeys)]
+    vk, vd, vn, bn = eng.rrf_pool_prep_dev(*dv)
+    o = order.long().clamp(min=0)
+    want_k = torch.where(order >= 0, torch.gather(keys, 1, o), torch.full_like(o, -1))
+    want_d = torch.where(order >= 0, torch.gather(dist, 1, o), torch.zeros_like(dist[:, :kv]))
+    assert torch.equal(vk.cpu(), want_k) and torch.equal(vd.cpu(), want_d)
+    assert torch.equal(vn.cpu(), (order >= 0).sum(1, dtype=torch.int32))
+    assert torch.equal(bn.cpu(), (bkeys >= 0).sum(1, dtype=torch.int32))
+
+
 @pytest.mark.parametrize("pool", [24, 32, 33, 48])
 def test_mmr_small_and_large_pools_match_oracle(eng, pool):
     """Pools <= 32 run the LDS-staged MMR kernel, larger ones the streaming kernel: both give the
