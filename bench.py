@@ -428,8 +428,7 @@ def _dense_roofline(kind, N, D, B, ms, traffic):
         bytes_, flops, peak = N * D * 2 + N / 8 + B * D * 2, 2.0 * N * D * B, PEAK_F16_MFMA_TFLOPS
     r = _roof(bytes_, flops, peak, ms)
     r.update(traffic=traffic, kernel=DENSE_KINDS[kind], avg_launch_ms=ms,
-             algorithmic_per_launch=dict(bytes=bytes_, flops=flops, rows=N, queries=B, dim=D),
-             fp32_equivalent_GBps=N * D * 4 / (ms * 1e-3) / 1e9)
+             algorithmic_per_launch=dict(bytes=bytes_, flops=flops, rows=N, queries=B, dim=D))
     # the other side of the same launch: at B = 256 the f16 scan's intensity (B flop/B = 256) sits
     # just under the nominal ridge (2.5 PF / 8 TB/s = 312), and under the chip's power limit the
     # MFMA clock drops, so the MFMA side is reported beside the HBM fraction
