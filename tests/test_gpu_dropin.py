@@ -229,6 +229,18 @@ def test_e5_graph_replay_matches_eager():
     ugraph.replay()
     torch.cuda.synchronize()
     torch.testing.assert_close(u_out, emb.encode_token_ids(ids, mask), atol=2e-3, rtol=0)
+    # the bench's bf16 graph (same seeded weights, cast) against the fp32 HF forward: not a
+    # self-comparison -- the stated bf16 bound (min cosine >= 0.9999; tests/test_gpu_scale.py holds
+    # the 12-layer B = 32, S = 256 figure)
+    emb_b = E5MultilingualEmbedder.random_init(seed=0, device="cuda", num_layers=2, dtype="bfloat16")
+    b_ids, b_mask, b_out, bgraph = emb_b.capture_graph(B, S, unpadded=True)
+    b_ids.copy_(ids)
+    b_mask.copy_(mask)
+    bgraph.replay()
+    torch.cuda.synchronize()
+    want32 = emb._encode_hf(ids, mask).float()
+    cos = torch.nn.functional.cosine_similarity(b_out.float(), want32, dim=1)
+    assert float(cos.min()) >= 0.9999, float(cos.min())
 
 
 @pytest.mark.parametrize("top_k", [-3, 0, 1, 5])

@@ -177,6 +177,7 @@ def test_dense_device_path_and_gather(eng):
     torch.cuda.synchronize()
     d_h, r_h = idx.search(q, 24)
     assert np.array_equal(r_t.cpu().numpy(), r_h)
+    _check_dense(d_t.cpu().numpy(), r_t.cpu().numpy(), emb, q, 24)  # the device entry vs the fp64 oracle
     g = idx.gather_dev(r_t.reshape(-1)).cpu().numpy().reshape(16, 24, 768)
     assert np.array_equal(g, emb[r_h])
 
