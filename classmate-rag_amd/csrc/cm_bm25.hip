@@ -118,13 +118,14 @@ __device__ inline int64_t lower_bound_doc(const int32_t *__restrict__ post_doc, 
 // qd_* (when qd_code is set): K2b's per-query term descriptors, so a planned item needs one
 // dependent load level instead of q_off -> q_terms -> head_id: qd_code[q][j] = (head id + 1,
 // 0 = not a head) | walked << 30 for the first kTermLanes terms (0 past the end), qd_idf the
-// term's idf (0 past the end), qd_tb[q] = q_off[q], qd_len[q] = the query's term count.
+// term's idf (0 past the end), qd_term the term id (-1 past the end or unknown), qd_tb[q] = q_off[q],
+// qd_len[q] = the query's term count.  K2a reads them too.
 __global__ void bm25_qcand_kernel(const int32_t *__restrict__ q_terms, const int32_t *__restrict__ q_off, int nq,
                                   int32_t vocab, const int32_t *__restrict__ head_id,
                                   const int64_t *__restrict__ term_off, int designate, uint8_t *__restrict__ qcand,
                                   const double *__restrict__ q_idf, int32_t *__restrict__ qd_code,
                                   double *__restrict__ qd_idf, int32_t *__restrict__ qd_tb,
-                                  int32_t *__restrict__ qd_len) {
+                                  int32_t *__restrict__ qd_len, int32_t *__restrict__ qd_term) {
   const int q = blockIdx.x * blockDim.x + threadIdx.x;
   if (q >= nq) return;
   const int tb = q_off[q], te = q_off[q + 1];
@@ -153,10 +154,11 @@ __global__ void bm25_qcand_kernel(const int32_t *__restrict__ q_terms, const int
   qd_len[q] = te - tb;
   for (int j = 0; j < kTermLanesQd; ++j) {
     const int i = tb + j;
-    int32_t c = 0;
+    int32_t c = 0, tt = -1;
     double f = 0.0;
     if (i < te) {
       const int32_t t = q_terms[i];
+      tt = t < vocab ? t : -1;
       if (t >= 0 && t < vocab) {
         c = (head_id ? head_id[t] : -1) + 1;
         if (qcand[i]) c |= 1 << 30;
@@ -165,6 +167,7 @@ __global__ void bm25_qcand_kernel(const int32_t *__restrict__ q_terms, const int
     }
     qd_code[(int64_t)q * kTermLanesQd + j] = c;
     qd_idf[(int64_t)q * kTermLanesQd + j] = f;
+    qd_term[(int64_t)q * kTermLanesQd + j] = tt;
   }
 }
 
@@ -1171,6 +1174,7 @@ struct BmWs {
   double *qd_idf;
   int32_t *qd_tb;
   int32_t *qd_len;
+  int32_t *qd_term;
   uint32_t *item_count;
   double *avgdl;    // the search's avgdl (unfiltered, host-computed or device-computed statistics)
   int64_t *stats;   // filtered entry: {Nc, sum of candidate lengths}
@@ -1217,6 +1221,8 @@ BmWs bm_ws_layout(const cm_bm25 *h, int nq, int total_terms, int k, void *base) 
   off += round_up((int64_t)std::max(nq, 1) * 4, 256);
   w.qd_len = reinterpret_cast<int32_t *>(p + off);
   off += round_up((int64_t)std::max(nq, 1) * 4, 256);
+  w.qd_term = reinterpret_cast<int32_t *>(p + off);
+  off += round_up((int64_t)std::max(nq, 1) * kTermLanes * 4, 256);
   w.total = off;
   return w;
 }
@@ -1236,12 +1242,14 @@ int bm25_launch_core(cm_bm25 *h, const int32_t *q_terms_dev, const int32_t *q_of
   const int ngroups = (nr + 1 + kBoundsGroup - 1) / kBoundsGroup;
   const int64_t nb = (int64_t)total_terms * ngroups;
   const bool prune = h->path != 1 && !(bm25_debug_flags() & 4);
-  if (nb > 0) {
+  if (nq > 0) {  // also for batches without terms: K2a and K2b read the per-query descriptors
     hipLaunchKernelGGL(bm25_qcand_kernel, dim3((unsigned)ceil_div(nq, 256)), dim3(256), 0, st, q_terms_dev, q_off_dev,
                        nq, h->vocab, h->nhead ? h->head_id.as<int32_t>() : (const int32_t *)nullptr,
                        h->term_off.as<int64_t>(), (int)prune, w.qcand, w.q_idf, prune ? w.qd_code : nullptr,
-                       w.qd_idf, w.qd_tb, w.qd_len);
+                       w.qd_idf, w.qd_tb, w.qd_len, w.qd_term);
     CM_HIP(hipGetLastError());
+  }
+  if (nb > 0) {
     hipLaunchKernelGGL(bm25_bounds_kernel, dim3((unsigned)ceil_div(nb, 256)), dim3(256), 0, st, q_terms_dev,
                        total_terms, h->vocab, nr, h->term_off.as<int64_t>(), h->post_doc.as<int32_t>(), w.qcand,
                        w.bounds);
@@ -1270,8 +1278,8 @@ int bm25_launch_core(cm_bm25 *h, const int32_t *q_terms_dev, const int32_t *q_of
     hipLaunchKernelGGL(bm25_tail_kernel<uint16_t>, dim3((unsigned)nblk_a), dim3(kBmThreads), 0, st, q_terms_dev,
                        q_off_dev, nq, h->vocab, w.q_idf, w.bounds, nr, rpw_a, h->post_doc.as<int32_t>(),
                        h->post_tf.as<uint16_t>(), head_id, h->headtf.as<uint8_t>(), h->npad, h->dl.as<int32_t>(),
-                       h->live.as<uint32_t>(), allow_dev, avgdl, k, w.cand_key, w.cand_row, w.thr, w.need, w.qcand,
-                       bm25_debug_flags());
+                       h->live.as<uint32_t>(), allow_dev, avgdl, k, w.cand_key, w.cand_row, w.thr, w.need, w.qd_code,
+                       w.qd_term, w.qd_idf, w.qd_tb, w.qd_len, bm25_debug_flags());
     h->timer.end(st);
     CM_HIP(hipGetLastError());
     hipLaunchKernelGGL(bm25_merge_kernel, dim3(nq), dim3(kMergeThreads), 0, st, w.cand_key, w.cand_row, nr, k,
