@@ -79,6 +79,47 @@ class HashTokenizer:
         return ids, mask
 
 
+def _act_scale(bound: float) -> float:
+    """Power-of-two a_scale for K10 with |x| * a_scale <= 2^15 (< f16 max 65504) given |x| <= bound."""
+    return (2.0 ** 15) / engine._pow2_at_most(bound) / 2.0 if bound > 0 else 1.0
+
+
+def _f16x3_layers(layers, emb_ln, D: int):
+    """Per layer: the four projections as K10 weights (engine.F16x3Weight) + the a_scale of each
+    GEMM input, from rigorous bounds on the activations (no data needed):
+      * LayerNorm output x = z * gamma + beta with sum(z^2) <= D, so |x_i| <= sqrt(D) max|gamma| +
+        max|beta| and ||x||_2 <= sqrt(D) max|gamma| + ||beta||_2 (QKV and FFN-up inputs);
+      * attention output: a convex combination of V rows, |o_i| <= max over tokens |v_i| with
+        v = x Wv^T + bv, |v_i| <= ||x||_2 ||Wv_i||_2 + |bv_i| (O-projection input);
+      * GELU output: |gelu(u)| <= max(|u|, 0.17), u = x Wi^T + bi bounded the same way
+        (FFN-down input).
+    Returns tuples (wqkv, a_qkv, wo, a_o, g1, b1, wi, a_i, w2, a_2, g2, b2)."""
+    import torch
+    sq = math.sqrt(D)
+
+    def ln_bounds(g, b):
+        gm = float(g.abs().max())
+        return sq * gm + float(b.abs().max()), sq * gm + float(b.norm())
+
+    def proj_bound(l2, w, b):
+        return l2 * float(w.norm(dim=1).max()) + float(b.abs().max())
+
+    out = []
+    prev_ln = (emb_ln.weight, emb_ln.bias)
+    with torch.no_grad():
+        for (wqkv, bqkv, wo, bo, g1, b1, wi, bi, w2, b2, g2, bb2) in layers:
+            x_inf, x_l2 = ln_bounds(*prev_ln)
+            o_bound = proj_bound(x_l2, wqkv[2 * D:], bqkv[2 * D:])
+            y_inf, y_l2 = ln_bounds(g1, b1)
+            h_bound = max(proj_bound(y_l2, wi, bi), 0.17)
+            out.append((engine.F16x3Weight(wqkv, bqkv), _act_scale(x_inf),
+                        engine.F16x3Weight(wo, bo), _act_scale(o_bound), g1, b1,
+                        engine.F16x3Weight(wi, bi), _act_scale(y_inf),
+                        engine.F16x3Weight(w2, b2), _act_scale(h_bound), g2, bb2))
+            prev_ln = (g2, bb2)
+    return out
+
+
 class E5MultilingualEmbedder:
     def __init__(self, model_name: str = "intfloat/multilingual-e5-base", device: Optional[str] = None,
                  normalize: bool = True, dtype: Optional[str] = None, _model=None, _tokenizer=None):
@@ -203,6 +244,12 @@ class E5MultilingualEmbedder:
         fused_attn = (os.environ.get("CM_E5_FUSED_ATTN", "1") != "0" and D // H == 64
                       and self.dtype in (torch.bfloat16, torch.float32))
         scale = 1.0 / math.sqrt(D // H)
+        # fp32: the projections run on K10 (split-precision f16 MFMAs, fp32 accuracy) unless
+        # CM_E5_F16X3=0 (then torch's fp32 GEMMs on hipBLASLt)
+        self.f16x3 = (self.dtype == torch.float32 and fused and os.environ.get("CM_E5_F16X3", "1") != "0"
+                      and D % 64 == 0 and cfg.intermediate_size % 64 == 0)
+        if self.f16x3:
+            layers = _f16x3_layers(layers, emb.LayerNorm, D)
         if fused:
             def add_ln(x, r, g, b):
                 return engine.add_layernorm(x, r, g, b, eps)
@@ -210,7 +257,8 @@ class E5MultilingualEmbedder:
             def add_ln(x, r, g, b):
                 return F.layer_norm(x + r, (D,), g, b, eps)
 
-        def fwd(ids, mask=None):
+        def embed(ids, mask):
+            """word + position/type embeddings -> (x0 input of the embedding LayerNorm, residual, keep)."""
             B, S = ids.shape
             keep = None
             if mask is not None and not bool(mask.all()):
@@ -226,20 +274,52 @@ class E5MultilingualEmbedder:
                 pt = emb.position_embeddings(pos) + emb.token_type_embeddings.weight[0]   # (S, D), tiled
                 if not fused:
                     pt = pt[None]
-            x = add_ln(emb.word_embeddings(ids), pt, emb.LayerNorm.weight, emb.LayerNorm.bias)
+            return emb.word_embeddings(ids), pt, keep
+
+        def sdpa(qkv, B, S, keep):
+            qkv = qkv.view(B, S, 3, H, D // H).permute(2, 0, 3, 1, 4)
+            o = F.scaled_dot_product_attention(qkv[0], qkv[1], qkv[2], attn_mask=keep)
+            return o.transpose(1, 2).reshape(B, S, D)
+
+        def fwd_f16x3(ids, mask=None):
+            # K10 path: every GEMM operand is produced directly as split planes (K8 / attention /
+            # the FFN-up epilogue write them), so the projections are pure LDS-DMA + MFMA kernels
+            B, S = ids.shape
+            w0, pt, keep = embed(ids, mask)
+            x, xp = engine.add_layernorm_split(w0, pt, emb.LayerNorm.weight, emb.LayerNorm.bias, eps, layers[0][1])
+            short = fused_attn and S <= 64 and keep is None
+            for li, (wqkv, a_qkv, wo, a_o, g1, b1, wi, a_i, w2, a_2, g2, bb2) in enumerate(layers):
+                qkv = engine.linear_f16x3(xp, wqkv)
+                if short:   # HIP attention reads the QKV output in place and writes the O operand planes
+                    op = engine.short_attention_split(qkv.view(B, S, 3 * D), H, scale, a_o)
+                else:
+                    op = engine.split_rows(sdpa(qkv, B, S, keep), a_o)
+                x, xp = engine.add_layernorm_split(x, engine.linear_f16x3(op, wo), g1, b1, eps, a_i)
+                hp = engine.linear_f16x3(xp, wi, gelu=True, planes_out=a_2)   # GELU + split fused
+                y = engine.linear_f16x3(hp, w2)
+                if li + 1 < len(layers):
+                    x, xp = engine.add_layernorm_split(x, y, g2, bb2, eps, layers[li + 1][1])
+                else:
+                    x = add_ln(x, y, g2, bb2)
+            return x.view(B, S, D)
+
+        def fwd(ids, mask=None):
+            B, S = ids.shape
+            w0, pt, keep = embed(ids, mask)
+            x = add_ln(w0, pt, emb.LayerNorm.weight, emb.LayerNorm.bias)
             short = fused_attn and S <= 64 and keep is None
             for (wqkv, bqkv, wo, bo, g1, b1, wi, bi, w2, b2, g2, bb2) in layers:
                 if short:   # HIP kernel reads the QKV GEMM output in place, writes (B, S, D)
                     o = engine.short_attention(F.linear(x, wqkv, bqkv), H, scale)
                 else:
-                    qkv = F.linear(x, wqkv, bqkv).view(B, S, 3, H, D // H).permute(2, 0, 3, 1, 4)
-                    o = F.scaled_dot_product_attention(qkv[0], qkv[1], qkv[2], attn_mask=keep)
-                    o = o.transpose(1, 2).reshape(B, S, D)
+                    o = sdpa(F.linear(x, wqkv, bqkv), B, S, keep)
                 x = add_ln(x, F.linear(o, wo, bo), g1, b1)
                 h = F.gelu(F.linear(x, wi, bi))
                 x = add_ln(x, F.linear(h, w2, b2), g2, bb2)
             return x
 
+        if self.f16x3:
+            fwd = fwd_f16x3
         self._lean = fwd
         return fwd
 

@@ -636,6 +636,130 @@ def short_attention(qkv, heads: int, scale: float, out=None):
                                        _stream(qkv.device.index)), "cm_short_attention")
     return out
 
+
+# ---------------------------------------------------------------------------
+# K10: fp32-accurate linear layers on the f16 matrix cores (split precision)
+def _pow2_at_most(x: float) -> float:
+    """Largest power of two <= x (x > 0)."""
+    import math
+    m, e = math.frexp(x)          # x = m * 2**e, 0.5 <= m < 1
+    return math.ldexp(1.0, e - 1)
+
+
+class F16x3Weight:
+    """An nn.Linear weight (N, K) fp32 prepared for ``linear_f16x3``: the two f16 halves of
+    W * scale in the fragment-major order the kernel streams (cm_f16x3_split_weights), scale a
+    power of two putting max|W| in [2^14, 2^15).  Keeps the fp32 bias (or None)."""
+
+    def __init__(self, weight, bias=None):
+        if weight.dtype != torch.float32 or weight.dim() != 2 or not weight.is_cuda:
+            raise ValueError("weight must be a 2-D fp32 device tensor")
+        N, K = weight.shape
+        if N % 64 or K % 32:
+            raise ValueError("need N % 64 == 0 and K % 32 == 0")
+        w = weight.detach().contiguous()
+        amax = float(w.abs().max())
+        self.scale = (2.0 ** 14) / _pow2_at_most(amax) if amax > 0 else 1.0
+        self.N, self.K = N, K
+        self.hi = torch.empty((N, K), dtype=torch.float16, device=w.device)
+        self.lo = torch.empty((N, K), dtype=torch.float16, device=w.device)
+        self.bias = bias.detach().float().contiguous() if bias is not None else None
+        if self.bias is not None and self.bias.numel() != N:
+            raise ValueError("bias must have N elements")
+        L.check(L.fn["cm_f16x3_split_weights"](L.ptr(w), N, K, float(self.scale), L.ptr(self.hi), L.ptr(self.lo),
+                                               _stream(w.device.index)), "cm_f16x3_split_weights")
+
+
+class Planes:
+    """An M x K fp32 matrix as K10 split planes: hi/lo f16 tensors of (ceil(M/16)*16, K) in the
+    fragment-major order (include/classmate_hip.h), holding the values times ``scale``."""
+
+    __slots__ = ("hi", "lo", "M", "K", "scale")
+
+    def __init__(self, M: int, K: int, scale: float, device):
+        rows = -(-M // 16) * 16
+        self.hi = torch.empty((rows, K), dtype=torch.float16, device=device)
+        self.lo = torch.empty((rows, K), dtype=torch.float16, device=device)
+        self.M, self.K, self.scale = M, K, float(scale)
+
+
+def split_rows(x, scale: float = 1.0) -> Planes:
+    """fp32 (..., K) device rows -> Planes of x * scale (cm_f16x3_split_rows)."""
+    if x.dtype != torch.float32 or x.shape[-1] % 32:
+        raise ValueError("x must be fp32 with a last dim that is a multiple of 32")
+    x = x.contiguous()
+    K = x.shape[-1]
+    p = Planes(x.numel() // K, K, scale, x.device)
+    L.check(L.fn["cm_f16x3_split_rows"](L.ptr(x), p.M, K, p.scale, L.ptr(p.hi), L.ptr(p.lo), _stream(x.device.index)),
+            "cm_f16x3_split_rows")
+    return p
+
+
+def linear_f16x3(x, w: "F16x3Weight", a_scale: float = 1.0, gelu: bool = False, out=None, planes_out: float = 0.0):
+    """y = x W^T + b (then exact-erf GELU if ``gelu``) at fp32 accuracy on the f16 MFMAs (K10).
+
+    x: ``Planes`` (its own scale), or (..., K) fp32 device rows (split here with ``a_scale``, a
+    power of two with |x| * a_scale <= 2^15).  Returns (M, N) fp32 -- or, with
+    ``planes_out`` = s > 0 (requires gelu), the Planes of GELU(y) * s for the next projection."""
+    if not isinstance(x, Planes):
+        if x.dtype != torch.float32 or x.shape[-1] != w.K:
+            raise ValueError(f"x must be (..., {w.K}) fp32")
+        lead = x.shape[:-1]
+        x = split_rows(x, a_scale)
+    else:
+        lead = (x.M,)
+    if x.K != w.K:
+        raise ValueError(f"planes have K={x.K}, the weight K={w.K}")
+    dev = x.hi.device
+    common = (L.ptr(x.hi), L.ptr(x.lo), x.M, w.K, L.ptr(w.hi), L.ptr(w.lo),
+              L.ptr(w.bias) if w.bias is not None else None, float(1.0 / (x.scale * w.scale)), w.N)
+    if planes_out:
+        if not gelu:
+            raise ValueError("planes_out is the fused FFN-up epilogue: gelu=True")
+        p = Planes(x.M, w.N, planes_out, dev)
+        L.check(L.fn["cm_linear_f16x3"](*common, L.CM_EPI_PLANES_GELU, None, p.scale, L.ptr(p.hi), L.ptr(p.lo),
+                                        _stream(dev.index)), "cm_linear_f16x3")
+        return p
+    if out is None:
+        out = torch.empty((*lead, w.N), dtype=torch.float32, device=dev)
+    L.check(L.fn["cm_linear_f16x3"](*common, L.CM_EPI_BIAS_GELU if gelu else L.CM_EPI_BIAS, L.ptr(out), 0.0, None,
+                                    None, _stream(dev.index)), "cm_linear_f16x3")
+    return out
+
+
+def add_layernorm_split(x, r, weight, bias, eps: float, a_scale: float, out=None):
+    """add_layernorm (fp32) that also returns its output * a_scale as K10 Planes
+    (cm_add_layernorm_split).  Returns (out, planes)."""
+    D = x.shape[-1]
+    if x.dtype != torch.float32:
+        raise ValueError("add_layernorm_split is fp32")
+    x = x.contiguous()
+    rows = x.numel() // D
+    if r is not None:
+        r = r.contiguous()
+        if r.dtype != x.dtype or r.shape[-1] != D or rows % (r.numel() // D):
+            raise ValueError("residual must match x's dtype and feature dim and tile its rows")
+    if out is None:
+        out = torch.empty_like(x)
+    p = Planes(rows, D, a_scale, x.device)
+    L.check(L.fn["cm_add_layernorm_split"](L.ptr(x), L.ptr(r) if r is not None else None,
+                                           (r.numel() // D) if r is not None else 0, L.ptr(weight), L.ptr(bias), rows,
+                                           D, float(eps), L.ptr(out), p.scale, L.ptr(p.hi), L.ptr(p.lo),
+                                           _stream(x.device.index)), "cm_add_layernorm_split")
+    return out, p
+
+
+def short_attention_split(qkv, heads: int, scale: float, a_scale: float) -> Planes:
+    """cm_short_attention (fp32) writing the context * a_scale as K10 Planes (B*S x heads*64)."""
+    B, S, F3 = qkv.shape
+    if F3 != 3 * heads * 64 or not 0 < S <= 64 or qkv.dtype != torch.float32:
+        raise ValueError("qkv must be fp32 (B, S<=64, 3*heads*64)")
+    qkv = qkv.contiguous()
+    p = Planes(B * S, heads * 64, a_scale, qkv.device)
+    L.check(L.fn["cm_short_attention_split"](L.ptr(qkv), B, S, heads, 64, float(scale), p.scale, L.ptr(p.hi),
+                                             L.ptr(p.lo), _stream(qkv.device.index)), "cm_short_attention_split")
+    return p
+
 # ---------------------------------------------------------------------------
 # Where-filters on the device (SURVEY §8f-2): retrieval.filters compiles, cm_filter_eval runs.
 def filter_bits(prog, device: Optional[int] = None):

@@ -137,6 +137,17 @@ struct KernelTimer {
   }
 };
 
+// K10 split planes (cm_gemm.hip): fp32 v = hi + lo as two f16 halves, stored fragment-major --
+// element (row, k) of an M x K matrix with kb32 = K / 32 lives at this offset (in halves) of
+// each plane: [row / 16][k / 32][lane slot (row % 16) + 16 ((k % 32) / 8)][k % 8]
+__host__ __device__ inline int64_t f16x3_plane_off(int64_t row, int k, int kb32) {
+  return (((row >> 4) * kb32 + (k >> 5)) * 64 + (row & 15) + 16 * ((k & 31) >> 3)) * 8 + (k & 7);
+}
+__device__ inline void f16x3_split1(float a, _Float16 &h, _Float16 &l) {
+  h = (_Float16)a;
+  l = (_Float16)(a - (float)h);
+}
+
 constexpr uint64_t kEmptyKey = ~0ull;
 constexpr int kMaxTopK = 256;
 

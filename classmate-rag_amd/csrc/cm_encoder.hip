@@ -42,10 +42,15 @@ __device__ inline void ln_store4(__hip_bfloat16 *p, const float (&v)[4]) {
   *reinterpret_cast<uint2 *>(p) = o;
 }
 
-template <typename T, int PER>
+// SPLIT (fp32 only): also write the row as K10 split planes (hi/lo f16 halves of y * a_scale,
+// fragment-major, cm_common.h f16x3_plane_off): the next projection's operand, so the GEMM
+// streams it with LDS-DMA and does no conversion work.  A lane's 4 features are 8 bytes of one
+// lane slot of a plane block.
+template <typename T, int PER, bool SPLIT = false>
 __global__ void __launch_bounds__(64 * kLnWaves)
     add_layernorm_kernel(const T *x, const T *__restrict__ r, int64_t r_rows, const T *__restrict__ gamma,
-                         const T *__restrict__ beta, int64_t rows, int D, float eps, T *out) {
+                         const T *__restrict__ beta, int64_t rows, int D, float eps, T *out, float a_scale = 1.f,
+                         _Float16 *__restrict__ ph = nullptr, _Float16 *__restrict__ pl = nullptr) {
   const int lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * kLnWaves + (threadIdx.x >> 6);
   if (row >= rows) return;  // whole wave exits together
@@ -99,8 +104,32 @@ __global__ void __launch_bounds__(64 * kLnWaves)
 #pragma unroll
       for (int e = 0; e < 4; ++e) y[e] = (v[u][e] - mean) * rstd * g[e] + b[e];
       ln_store4(orow + 4 * c, y);
+      if constexpr (SPLIT) {
+        typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+        h4 hh, ll;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          _Float16 a, b2;
+          f16x3_split1(y[e] * a_scale, a, b2);
+          hh[e] = a;
+          ll[e] = b2;
+        }
+        const int64_t off = f16x3_plane_off(row, 4 * c, D >> 5);
+        *reinterpret_cast<h4 *>(ph + off) = hh;
+        *reinterpret_cast<h4 *>(pl + off) = ll;
+      }
     }
   }
+}
+
+template <int PER>
+int launch_add_ln_split(const float *x, const float *r, int64_t r_rows, const float *g, const float *b, int64_t rows,
+                        int D, float eps, float *out, float a_scale, _Float16 *ph, _Float16 *pl, hipStream_t st) {
+  const dim3 grid((unsigned)ceil_div(rows, kLnWaves)), block(64 * kLnWaves);
+  hipLaunchKernelGGL((add_layernorm_kernel<float, PER, true>), grid, block, 0, st, x, r, r_rows, g, b, rows, D, eps,
+                     out, a_scale, ph, pl);
+  CM_HIP(hipGetLastError());
+  return CM_OK;
 }
 
 template <typename T>
@@ -156,9 +185,13 @@ __device__ inline void ld8(const __hip_bfloat16 *p, float (&v)[8]) {
   }
 }
 
-template <typename T>
+// SPLIT (fp32): write the context as K10 split planes of o * a_scale (the O projection's
+// operand) instead of fp32 rows: 8 features = one 16-byte lane slot per plane.
+template <typename T, bool SPLIT = false>
 __global__ void __launch_bounds__(64) short_attention_kernel(const T *__restrict__ qkv, int S, int H, float scale,
-                                                             T *__restrict__ out) {
+                                                             T *__restrict__ out, float a_scale = 1.f,
+                                                             _Float16 *__restrict__ ph = nullptr,
+                                                             _Float16 *__restrict__ pl = nullptr) {
   constexpr int VPR = kAttnDh * sizeof(T) / 16;  // 16-byte vectors per head row
   __shared__ __attribute__((aligned(16))) T ks[kAttnMaxS * kAttnDh];
   __shared__ __attribute__((aligned(16))) T vs[kAttnMaxS * kAttnDh];
@@ -213,11 +246,31 @@ __global__ void __launch_bounds__(64) short_attention_kernel(const T *__restrict
     }
   }
   const float inv = 1.f / l;
-  T *orow = out + (b * S + lane) * (int64_t)H * kAttnDh + (int64_t)h * kAttnDh;
+  if constexpr (SPLIT) {
+    typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+    const int64_t row = b * S + lane;
+    const int kb32 = H * kAttnDh / 32;
 #pragma unroll
-  for (int c = 0; c < kAttnDh / 4; ++c) {
-    float y[4] = {acc[4 * c] * inv, acc[4 * c + 1] * inv, acc[4 * c + 2] * inv, acc[4 * c + 3] * inv};
-    ln_store4(orow + 4 * c, y);
+    for (int c = 0; c < kAttnDh / 8; ++c) {
+      h8 hh, ll;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        _Float16 a, b2;
+        f16x3_split1(acc[8 * c + e] * inv * a_scale, a, b2);
+        hh[e] = a;
+        ll[e] = b2;
+      }
+      const int64_t off = f16x3_plane_off(row, h * kAttnDh + 8 * c, kb32);
+      *reinterpret_cast<h8 *>(ph + off) = hh;
+      *reinterpret_cast<h8 *>(pl + off) = ll;
+    }
+  } else {
+    T *orow = out + (b * S + lane) * (int64_t)H * kAttnDh + (int64_t)h * kAttnDh;
+#pragma unroll
+    for (int c = 0; c < kAttnDh / 4; ++c) {
+      float y[4] = {acc[4 * c] * inv, acc[4 * c + 1] * inv, acc[4 * c + 2] * inv, acc[4 * c + 3] * inv};
+      ln_store4(orow + 4 * c, y);
+    }
   }
 }
 
@@ -369,6 +422,37 @@ extern "C" int cm_short_attention(const void *qkv_dev, int32_t B, int32_t S, int
       break;
     default: CM_FAIL(CM_EINVAL, "dtype must be f32/bf16");
   }
+  CM_HIP(hipGetLastError());
+  return CM_OK;
+}
+
+extern "C" int cm_add_layernorm_split(const float *x_dev, const float *r_dev, int64_t r_rows, const float *gamma_dev,
+                                      const float *beta_dev, int64_t rows, int32_t D, float eps, float *out_dev,
+                                      float a_scale, void *hi_dev, void *lo_dev, void *stream) {
+  if (rows <= 0) return CM_OK;
+  if (!x_dev || !gamma_dev || !beta_dev || !out_dev || !hi_dev || !lo_dev) CM_FAIL(CM_EINVAL, "NULL argument");
+  if (D <= 0 || D % 32 != 0 || D > 4 * 64 * kLnMaxPer) CM_FAIL(CM_EINVAL, "D must be a multiple of 32, <= 2048");
+  if (r_dev && r_rows <= 0) CM_FAIL(CM_EINVAL, "r_rows must be > 0 with a residual");
+  hipStream_t st = (hipStream_t)stream;
+  _Float16 *ph = (_Float16 *)hi_dev, *pl = (_Float16 *)lo_dev;
+  switch ((int)ceil_div(D / 4, 64)) {
+    case 1: return launch_add_ln_split<1>(x_dev, r_dev, r_rows, gamma_dev, beta_dev, rows, D, eps, out_dev, a_scale, ph, pl, st);
+    case 2: return launch_add_ln_split<2>(x_dev, r_dev, r_rows, gamma_dev, beta_dev, rows, D, eps, out_dev, a_scale, ph, pl, st);
+    case 3: return launch_add_ln_split<3>(x_dev, r_dev, r_rows, gamma_dev, beta_dev, rows, D, eps, out_dev, a_scale, ph, pl, st);
+    case 4: return launch_add_ln_split<4>(x_dev, r_dev, r_rows, gamma_dev, beta_dev, rows, D, eps, out_dev, a_scale, ph, pl, st);
+    default: return launch_add_ln_split<8>(x_dev, r_dev, r_rows, gamma_dev, beta_dev, rows, D, eps, out_dev, a_scale, ph, pl, st);
+  }
+}
+
+extern "C" int cm_short_attention_split(const float *qkv_dev, int32_t B, int32_t S, int32_t H, int32_t head_dim,
+                                        float scale, float a_scale, void *hi_dev, void *lo_dev, void *stream) {
+  if (B <= 0) return CM_OK;
+  if (!qkv_dev || !hi_dev || !lo_dev) CM_FAIL(CM_EINVAL, "NULL argument");
+  if (head_dim != kAttnDh) CM_FAIL(CM_EINVAL, "head_dim must be 64");
+  if (S <= 0 || S > kAttnMaxS || H <= 0) CM_FAIL(CM_EINVAL, "need 0 < S <= 64 and H > 0");
+  hipLaunchKernelGGL((short_attention_kernel<float, true>), dim3((unsigned)((int64_t)B * H)), dim3(64), 0,
+                     (hipStream_t)stream, qkv_dev, S, H, scale, nullptr, a_scale, (_Float16 *)hi_dev,
+                     (_Float16 *)lo_dev);
   CM_HIP(hipGetLastError());
   return CM_OK;
 }

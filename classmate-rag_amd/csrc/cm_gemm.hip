@@ -1,0 +1,443 @@
+// K10: fp32-accurate linear layers of the E5 (XLM-R) forward on the f16 matrix cores.
+//
+// The reference encodes in fp32 (sentence-transformers on torch fp32,
+// rag/embeddings/__init__.py:85-105): every projection of XLM-R is y = x W^T + b with fp32
+// operands and fp32 accumulation.  gfx950's fp32 MFMA runs at the fp32 vector rate (157 TF),
+// 1/16 of the f16 rate, and has no reduced-precision xf32 form.  Here each fp32 operand is
+// split into two f16 halves, v = hi + lo (hi = f16(v), lo = f16(v - hi): 22 significant bits),
+// and the product is accumulated from three f16 MFMAs, lo.hi + hi.lo + hi.hi, in fp32
+// (v_mfma_f32_16x16x32_f16 multiplies exactly and accumulates in fp32).  The dropped lo.lo
+// term and the rounding of the lo halves are each <= 2^-22 relative per product, below the
+// 2^-24 rounding of one fp32 accumulation step times the sqrt(K) growth of a K = 768 / 3072
+// reduction -- the result is as accurate as the fp32 GEMM it replaces (tests/test_gpu_gemm.py
+// holds it to 2x torch's fp32 GEMM error against fp64), at 16/3 of its peak rate.
+//
+// Range: f16 has a 5-bit exponent.  Weights are split once (cm_f16x3_split_weights) after a
+// power-of-two scale that puts max|W| at 2^14..2^15, so no weight's lo half is subnormal
+// except where its absolute error is < 2^-39 max|W|.  Activations are split by their
+// producers after a power-of-two a_scale that the host derives from a rigorous bound on |x|
+// (the LayerNorm / attention / GELU bounds in classmate_hip/embeddings) with |x| a_scale <=
+// 2^15; an activation below 2^-14 / a_scale contributes an absolute error < 2^-25 / a_scale.
+// Both scales are exact powers of two, undone exactly in the epilogue (out_scale).
+//
+// Split-plane layout ("planes", HBM): a row-major M x K fp32 matrix becomes two f16 planes,
+// hi and lo, each [ceil(M/16)][K/32][64 lanes][8] -- fragment-major: the 1 KiB block
+// (rows 16 b .. +15, k 32 kb .. +31) holds in lane slot (c, g) = c + 16 g the 8 halves of row
+// 16 b + c, k = 32 kb + 8 g .. + 7, which is exactly what lane c + 16 g feeds to
+// v_mfma_f32_16x16x32_f16 as its A (row) or B (column) operand.  Weights W (N x K, nn.Linear
+// layout) use the same order with N as the row index.  Every operand load of the GEMM is then
+// one global_load_lds_dwordx4 wave-instruction per 1 KiB block (8 full 128-B lines), read back
+// from LDS with a conflict-free ds_read_b128 at lane*16.  Rows of the last block beyond M hold
+// whatever the producer left: they only reach output rows >= M, which are never stored.
+//
+// Producers of planes: cm_f16x3_split_rows (any fp32 matrix), cm_add_layernorm_split (the
+// XLM-R residual + LayerNorm, also writing the fp32 rows the next residual needs),
+// cm_short_attention_split (query-batch attention) and this GEMM's own GELU epilogue
+// (FFN-up -> FFN-down: the intermediate exists only as planes).
+//
+// GEMM (linear_f16x3_kernel): one workgroup of 4 waves (2 x 2) per BM x BN output tile, one
+// workgroup per CU (the ring takes most of the LDS).  The k loop runs over 32-wide steps
+// through an S-stage LDS ring; stage = A_hi | A_lo (BM/16 blocks each) | B_hi | B_lo (BN/16
+// each), all filled by LDS-DMA: per step each wave waits (counted vmcnt) for its own pieces of
+// the step's stage, one raw s_barrier publishes everyone's pieces and retires every read of
+// the previous step's stage, the wave issues its pieces of stage t + S - 1 into that freed
+// slot, then reads its fragments and issues 3 (BM/32)(BN/32) MFMAs.  No VGPR staging, no
+// VALU work in the loop: the DMA of S - 1 steps ahead overlaps the MFMAs.  Tiles map
+// XCD-major (bijective remap) so the column tiles of one row block share its A rows in one
+// XCD's L2.
+#include "cm_common.h"
+
+#include <algorithm>
+
+namespace cm {
+
+typedef _Float16 h16x8 __attribute__((ext_vector_type(8)));
+typedef float g32x4 __attribute__((ext_vector_type(4)));
+// fragments travel as 4 dwords (a loop-carried vector of halves gets split into 16-bit pieces and
+// re-packed with v_perm at every loop back-edge); reinterpreted as 8 halves at the MFMA
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ h16x8 as_h8(i32x4 v) { return __builtin_bit_cast(h16x8, v); }
+
+constexpr int kGemmThreads = 256;
+
+__device__ inline float gelu_erf(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
+
+// one 8-element segment: fp32 -> (hi, lo) f16 halves after the exact power-of-two scale
+__device__ inline void split8(const float (&x)[8], float s, h16x8 &hi, h16x8 &lo) {
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    _Float16 h, l;
+    f16x3_split1(x[e] * s, h, l);
+    hi[e] = h;
+    lo[e] = l;
+  }
+}
+
+// bijective XCD-major remap (MI355X: consecutive workgroup ids go round-robin over 8 XCDs)
+__device__ inline int xcd_remap(int orig, int nwg) {
+  const int xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+}
+
+enum { kEpiF32 = 0, kEpiF32Gelu = 1, kEpiPlanesGelu = 2 };
+
+// Epilogue of one tile for one wave, straight from the accumulators (no LDS: the ring keeps
+// all of it).  fp32 rows: lane (g, c) stores rows 4 g + r of column c (16 consecutive floats per
+// row and store).  Planes: lanes c and c ^ 1 swap half their halves (DPP quad_perm 1,0,3,2) so
+// that each lane stores 4-byte column pairs (c even: rows 0-1, c odd: rows 2-3 of its group).
+template <int BMB, int BNB, int EPI>
+__device__ __forceinline__ void k10_epilogue(g32x4 (&acc)[BMB / 2][BNB / 2], int tm, int tn, int wr, int wc, int lane,
+                                             const float *btab, float out_scale, float next_scale, int64_t M, int N,
+                                             int64_t mblocks, float *__restrict__ Cout, _Float16 *__restrict__ Ch,
+                                             _Float16 *__restrict__ Cl) {
+  constexpr int WMT = BMB / 2, WNT = BNB / 2;
+  const int g4 = lane >> 4, c16 = lane & 15;
+  const int64_t rb0 = (int64_t)tm * BMB + wr * WMT;    // this wave's first row block
+  const int cbase = (tn * BNB + wc * WNT) * 16;        // its first column
+  const bool odd = c16 & 1;
+#pragma unroll
+  for (int j = 0; j < WNT; ++j) {
+    const int col = cbase + 16 * j + c16;
+    const float bv = btab[col];
+#pragma unroll
+    for (int i = 0; i < WMT; ++i) {
+      if constexpr (EPI != kEpiPlanesGelu) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int64_t row = (rb0 + i) * 16 + 4 * g4 + r;
+          float y = acc[i][j][r] * out_scale + bv;
+          if (EPI == kEpiF32Gelu) y = gelu_erf(y);
+          if (row < M) Cout[row * N + col] = y;
+        }
+      } else {
+        uint32_t hh[4], ll[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          _Float16 h, l;
+          f16x3_split1(gelu_erf(acc[i][j][r] * out_scale + bv) * next_scale, h, l);
+          hh[r] = __builtin_bit_cast(uint16_t, h);
+          ll[r] = __builtin_bit_cast(uint16_t, l);
+        }
+        // even lane keeps rows 0-1 and sends 2-3; odd lane keeps 2-3 and sends 0-1
+        const uint32_t sh = odd ? (hh[0] | hh[1] << 16) : (hh[2] | hh[3] << 16);
+        const uint32_t sl = odd ? (ll[0] | ll[1] << 16) : (ll[2] | ll[3] << 16);
+        const uint32_t rh = (uint32_t)__builtin_amdgcn_mov_dpp((int)sh, 0xB1, 0xF, 0xF, false);
+        const uint32_t rl = (uint32_t)__builtin_amdgcn_mov_dpp((int)sl, 0xB1, 0xF, 0xF, false);
+        const int64_t grb = rb0 + i;
+        if (grb < mblocks) {
+          const int r0 = odd ? 2 : 0;
+          const int c0 = col & ~1;
+#pragma unroll
+          for (int q = 0; q < 2; ++q) {
+            const uint32_t mine_h = hh[r0 + q], mine_l = ll[r0 + q];
+            const uint32_t oth_h = (rh >> (16 * q)) & 0xffffu, oth_l = (rl >> (16 * q)) & 0xffffu;
+            // column c0 (even) in the low half, c0 + 1 in the high half
+            const uint32_t wh = odd ? (oth_h | mine_h << 16) : (mine_h | oth_h << 16);
+            const uint32_t wl = odd ? (oth_l | mine_l << 16) : (mine_l | oth_l << 16);
+            const int64_t off = f16x3_plane_off(grb * 16 + 4 * g4 + r0 + q, c0, N >> 5);
+            *reinterpret_cast<uint32_t *>(Ch + off) = wh;
+            *reinterpret_cast<uint32_t *>(Cl + off) = wl;
+          }
+        }
+      }
+      acc[i][j] = g32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  }
+}
+
+// Tile order of the persistent schedule: 8 row tiles per column sweep ("grouped"), so tiles that
+// run concurrently share A rows and weight columns in L2.
+__device__ __forceinline__ void k10_tile(int L, int tiles_m, int tiles_n, int &tm, int &tn) {
+  const int per_group = 8 * tiles_n;
+  const int first_m = (L / per_group) * 8;
+  const int gsz = min(tiles_m - first_m, 8);
+  const int rem = L % per_group;
+  tm = first_m + rem % gsz;
+  tn = rem / gsz;
+}
+
+// One stage's DMA for this wave: PCS 1 KiB fragment blocks (o = 4 i + wave) of k-step kt of
+// tile (tm, tn) into ring slot `st`.
+template <int BMB, int BNB, int PCS>
+__device__ __forceinline__ void k10_issue(unsigned char *st, const _Float16 *Ah, const _Float16 *Al,
+                                          const _Float16 *Wh, const _Float16 *Wl, int64_t mblocks, int kb32,
+                                          int tm, int tn, int kt, int wave, int lane) {
+  const int64_t mb0 = (int64_t)tm * BMB;
+  const int nb0 = tn * BNB;
+#pragma unroll
+  for (int i = 0; i < PCS; ++i) {
+    const int o = 4 * i + wave;
+    const _Float16 *plane;
+    int64_t blkrow;
+    if (o < 2 * BMB) {
+      plane = o < BMB ? Ah : Al;
+      const int64_t rb = mb0 + (o < BMB ? o : o - BMB);
+      blkrow = rb < mblocks ? rb : mblocks - 1;       // clamp: duplicate rows feed unstored outputs
+    } else {
+      const int ob = o - 2 * BMB;
+      plane = ob < BNB ? Wh : Wl;
+      blkrow = nb0 + (ob < BNB ? ob : ob - BNB);
+    }
+    const unsigned char *src = (const unsigned char *)plane + ((blkrow * kb32 + kt) << 10) + lane * 16;
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)src,
+                                     (__attribute__((address_space(3))) void *)(st + o * 1024), 16, 0, 0);
+  }
+}
+
+// BMB x BNB fragment blocks (16 x 16 outputs each) per tile, 2 x 2 waves, S-stage ring.
+// Persistent: gridDim.x <= #CUs workgroups, each runs its tiles' k-steps as one continuous
+// stream g = 0 .. G-1 through the ring, so the DMA of the next tile's first stages overlaps the
+// current tile's last steps and its epilogue.
+template <int BMB, int BNB, int S, int EPI>
+__global__ void __launch_bounds__(kGemmThreads)
+    linear_f16x3_kernel(const _Float16 *__restrict__ Ah, const _Float16 *__restrict__ Al, int64_t M, int K,
+                        const _Float16 *__restrict__ Wh, const _Float16 *__restrict__ Wl,
+                        const float *__restrict__ bias, float out_scale, int N, float *__restrict__ Cout,
+                        float next_scale, _Float16 *__restrict__ Ch, _Float16 *__restrict__ Cl) {
+  constexpr int WMT = BMB / 2, WNT = BNB / 2;         // 16x16 tiles per wave
+  constexpr int NBLK = 2 * (BMB + BNB);               // 1 KiB blocks per stage
+  constexpr int PCS = NBLK / 4;                       // DMA pieces per wave per stage
+  constexpr int STAGE = NBLK * 1024;
+  constexpr int H1 = (WMT + 1) / 2;                   // row tiles before the mid-step barrier
+  static_assert(BMB % 2 == 0 && BNB % 2 == 0 && WNT % 2 == 0 && NBLK % 4 == 0, "tile must split over 2 x 2 waves");
+  static_assert(S >= 3, "the ring needs one stage in use, one landing, one in flight");
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // uniform: piece choice and M0 stay scalar
+  const int wr = wave >> 1, wc = wave & 1;
+  const int64_t mblocks = (M + 15) >> 4;
+  const int kb32 = K >> 5, nk = kb32;
+  const int tiles_m = (int)((mblocks + BMB - 1) / BMB), tiles_n = N / (16 * BNB);
+  const int n_tiles = tiles_m * tiles_n;
+  float *btab = reinterpret_cast<float *>(lds + S * STAGE);                    // bias[N]
+
+  // ---- tile schedule: XCD x (= blockIdx % 8 under round-robin dispatch) takes a contiguous
+  //      chunk of the grouped tile order and its sx workgroups step through it together (a
+  //      placement guess for L2 sharing only: any mapping is correct)
+  const int w = blockIdx.x, nwg = gridDim.x, xcd = w & 7, slot = w >> 3;
+  const int sx = nwg / 8 + (xcd < (nwg & 7));
+  const int q8 = n_tiles / 8, r8 = n_tiles % 8;
+  const int c0 = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + slot;
+  const int cn = q8 + (xcd < r8);
+  const int my_n = slot < cn ? (cn - slot + sx - 1) / sx : 0;
+  if (my_n == 0) return;                              // whole workgroup: no barrier is left waiting
+  const int G = my_n * nk;
+
+  // bias of every column into LDS once (no global load may sit between the counted DMA waits)
+  for (int i = tid; i < N; i += kGemmThreads) btab[i] = bias ? bias[i] : 0.f;
+  __syncthreads();
+
+  // DMA issuer state: stage `issued` = k-step is_kt of this workgroup's tile is_ti (clamped at G-1)
+  int issued = 0, is_ti = 0, is_kt = 0, is_tm, is_tn;
+  k10_tile(c0, tiles_m, tiles_n, is_tm, is_tn);
+#define K10_ISSUE()                                                                                       \
+  do {                                                                                                    \
+    k10_issue<BMB, BNB, PCS>(lds + (issued % S) * STAGE, Ah, Al, Wh, Wl, mblocks, kb32, is_tm, is_tn, is_kt, \
+                             wave, lane);                                                                 \
+    if (++issued < G && ++is_kt == nk) {                                                                  \
+      is_kt = 0;                                                                                          \
+      ++is_ti;                                                                                            \
+      k10_tile(c0 + is_ti * sx, tiles_m, tiles_n, is_tm, is_tn);                                          \
+    }                                                                                                     \
+  } while (0)
+
+  i32x4 ah0[WMT], al0[WMT], bh0[WNT], bl0[WNT];
+  i32x4 ah1[WMT], al1[WMT], bh1[WNT], bl1[WNT];
+#define K10_READ(g, AH, AL, BH, BL)                                                                          \
+  do {                                                                                                       \
+    const unsigned char *st_ = lds + ((g) % S) * STAGE + lane * 16;                                          \
+    _Pragma("unroll") for (int j = 0; j < WNT; ++j) {                                                        \
+      BH[j] = *reinterpret_cast<const i32x4 *>(st_ + (2 * BMB + wc * WNT + j) * 1024);                       \
+      BL[j] = *reinterpret_cast<const i32x4 *>(st_ + (2 * BMB + BNB + wc * WNT + j) * 1024);                 \
+    }                                                                                                        \
+    _Pragma("unroll") for (int i = 0; i < WMT; ++i) {                                                        \
+      AH[i] = *reinterpret_cast<const i32x4 *>(st_ + (wr * WMT + i) * 1024);                                 \
+      AL[i] = *reinterpret_cast<const i32x4 *>(st_ + (BMB + wr * WMT + i) * 1024);                           \
+    }                                                                                                        \
+  } while (0)
+
+  g32x4 acc[WMT][WNT];
+#pragma unroll
+  for (int i = 0; i < WMT; ++i)
+#pragma unroll
+    for (int j = 0; j < WNT; ++j) acc[i][j] = g32x4{0.f, 0.f, 0.f, 0.f};
+#define K10_MFMA(I0, I1, AH, AL, BH, BL)                                                       \
+  _Pragma("unroll") for (int i = (I0); i < (I1); ++i) _Pragma("unroll") for (int j = 0; j < WNT; ++j) { \
+    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_h8(AL[i]), as_h8(BH[j]), acc[i][j], 0, 0, 0); \
+    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_h8(AH[i]), as_h8(BL[j]), acc[i][j], 0, 0, 0); \
+    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_h8(AH[i]), as_h8(BH[j]), acc[i][j], 0, 0, 0); \
+  }
+
+  // ---- the stream: prologue fills the ring, then per step: MFMAs of the first row half, wait
+  //      for the next stage (counted: S - 2 stages may stay in flight), one barrier (publishes
+  //      it, retires every wave's reads of this step's slot), refill that slot with stage g + S,
+  //      read the next step's fragments behind the second half's MFMAs.  After a tile's last
+  //      step its epilogue runs through this wave's private LDS region with 16-byte stores (the
+  //      next wait then also covers those stores: vmcnt counts in issue order).
+#pragma unroll
+  for (int p = 0; p < S; ++p) K10_ISSUE();
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PCS * (S - 1)) : "memory");
+  __builtin_amdgcn_s_barrier();
+  K10_READ(0, ah0, al0, bh0, bl0);
+
+#define K10_STEP(g, AH, AL, BH, BL, NAH, NAL, NBH, NBL)                                        \
+  do {                                                                                         \
+    K10_MFMA(0, H1, AH, AL, BH, BL)                                                            \
+    if ((g) + 1 < G) {                                                                         \
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_waitcnt vmcnt(%0)" ::"n"(PCS * (S - 2)) : "memory"); \
+      __builtin_amdgcn_s_barrier();                                                            \
+      K10_ISSUE();                                                                             \
+      K10_READ((g) + 1, NAH, NAL, NBH, NBL);                                                   \
+    }                                                                                          \
+    K10_MFMA(H1, WMT, AH, AL, BH, BL)                                                          \
+  } while (0)
+
+  for (int ti = 0; ti < my_n; ++ti) {
+    for (int kt = 0; kt < nk; kt += 2) {              // nk is even (K % 64 == 0)
+      const int g = ti * nk + kt;
+      K10_STEP(g, ah0, al0, bh0, bl0, ah1, al1, bh1, bl1);
+      K10_STEP(g + 1, ah1, al1, bh1, bl1, ah0, al0, bh0, bl0);
+    }
+    int tm, tn;
+    k10_tile(c0 + ti * sx, tiles_m, tiles_n, tm, tn);
+    k10_epilogue<BMB, BNB, EPI>(acc, tm, tn, wr, wc, lane, btab, out_scale, next_scale, M, N, mblocks, Cout, Ch,
+                                Cl);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // clamped tail DMAs landed before the LDS is released
+#undef K10_ISSUE
+#undef K10_READ
+#undef K10_MFMA
+#undef K10_STEP
+}
+
+// W fp32 [N][K] row-major (or any fp32 matrix) -> fragment-major f16 planes of W * scale
+__global__ void split_rows_kernel(const float *__restrict__ W, int64_t N, int K, float scale, _Float16 *__restrict__ hi,
+                                  _Float16 *__restrict__ lo) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // one 8-element segment
+  const int64_t nseg = N * (K / 8);
+  if (t >= nseg) return;
+  const int64_t n = t / (K / 8);
+  const int k = (int)(t % (K / 8)) * 8;
+  const float4 *p = reinterpret_cast<const float4 *>(W + n * K + k);
+  const float4 u = p[0], v = p[1];
+  const float x[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
+  h16x8 h, l;
+  split8(x, scale, h, l);
+  const int64_t off = f16x3_plane_off(n, k, K >> 5);
+  *reinterpret_cast<h16x8 *>(hi + off) = h;
+  *reinterpret_cast<h16x8 *>(lo + off) = l;
+}
+
+struct TileCfg {
+  int bmb, bnb;
+};
+
+// Pick the tile minimising (rounds of one-workgroup-per-CU waves) x (tile area): the 96 x 192
+// tile divides M = 6144 (the 256 x 24 query batch) x N in {768, 2304, 3072} into exact
+// multiples of 256 tiles; 128 x 128, 64 x 128 and 64 x 64 cover the other shapes.
+static TileCfg pick_tile(int64_t M, int N, int n_cu) {
+  const TileCfg cands[4] = {{6, 12}, {8, 8}, {4, 8}, {4, 4}};
+  TileCfg best = {0, 0};
+  double best_cost = 0;
+  for (const TileCfg &c : cands) {
+    if (N % (16 * c.bnb)) continue;
+    const int64_t tiles = ceil_div(M, 16 * c.bmb) * (N / (16 * c.bnb));
+    // a tile's time ~ its MFMAs (area) + its per-step DMA / fragment reads (perimeter)
+    const double cost = (double)ceil_div(tiles, n_cu) * (c.bmb * c.bnb + 2 * (c.bmb + c.bnb));
+    if (best.bmb == 0 || cost < best_cost) {
+      best = c;
+      best_cost = cost;
+    }
+  }
+  return best;
+}
+
+template <int BMB, int BNB, int S>
+static int launch_tile(const _Float16 *Ah, const _Float16 *Al, int64_t M, int K, const _Float16 *Wh,
+                       const _Float16 *Wl, const float *bias, float out_scale, int N, int epi, float *C,
+                       float next_scale, _Float16 *Ch, _Float16 *Cl, int n_cu, hipStream_t st) {
+  const int64_t tiles = ceil_div(ceil_div(M, 16), BMB) * (N / (16 * BNB));
+  if (tiles > INT32_MAX / 2) CM_FAIL(CM_EINVAL, "too many tiles");
+  const int lds_bytes = S * 2 * (BMB + BNB) * 1024 + ((N * 4 + 15) & ~15);
+  if (lds_bytes > 160 * 1024) CM_FAIL(CM_EINVAL, "N too large for the LDS bias table");
+  const dim3 grid((unsigned)std::min<int64_t>(tiles, n_cu)), block(kGemmThreads);
+  static int attr_set[3] = {0, 0, 0};  // > 64 KiB of dynamic LDS: opt in (to the largest size seen)
+  switch (epi) {
+#define CM_K10_CASE(E)                                                                                             \
+  case E:                                                                                                          \
+    if (attr_set[E] < lds_bytes) {                                                                                 \
+      CM_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&linear_f16x3_kernel<BMB, BNB, S, E>),             \
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));                         \
+      attr_set[E] = 160 * 1024;                                                                                    \
+    }                                                                                                              \
+    hipLaunchKernelGGL((linear_f16x3_kernel<BMB, BNB, S, E>), grid, block, lds_bytes, st, Ah, Al, M, K, Wh, Wl,  \
+                       bias, out_scale, N, C, next_scale, Ch, Cl);                                                 \
+    break;
+    CM_K10_CASE(kEpiF32)
+    CM_K10_CASE(kEpiF32Gelu)
+    CM_K10_CASE(kEpiPlanesGelu)
+#undef CM_K10_CASE
+    default: CM_FAIL(CM_EINVAL, "unknown epilogue");
+  }
+  CM_HIP(hipGetLastError());
+  return CM_OK;
+}
+
+static int g_n_cu = 0;
+
+}  // namespace cm
+
+using namespace cm;
+
+extern "C" int cm_f16x3_split_weights(const float *w_dev, int32_t N, int32_t K, float scale, void *hi_dev, void *lo_dev,
+                                      void *stream) {
+  if (N <= 0 || K <= 0) return CM_OK;
+  if (!w_dev || !hi_dev || !lo_dev) CM_FAIL(CM_EINVAL, "NULL argument");
+  if (N % 16 || K % 32) CM_FAIL(CM_EINVAL, "need N % 16 == 0 and K % 32 == 0");
+  return cm_f16x3_split_rows(w_dev, N, K, scale, hi_dev, lo_dev, stream);
+}
+
+extern "C" int cm_f16x3_split_rows(const float *x_dev, int64_t M, int32_t K, float scale, void *hi_dev, void *lo_dev,
+                                   void *stream) {
+  if (M <= 0) return CM_OK;
+  if (!x_dev || !hi_dev || !lo_dev) CM_FAIL(CM_EINVAL, "NULL argument");
+  if (K <= 0 || K % 32) CM_FAIL(CM_EINVAL, "K must be a positive multiple of 32");
+  if (((uintptr_t)x_dev & 15) || ((uintptr_t)hi_dev & 15) || ((uintptr_t)lo_dev & 15))
+    CM_FAIL(CM_EINVAL, "x and the planes must be 16-byte aligned");
+  const int64_t nseg = M * (K / 8);
+  hipLaunchKernelGGL(split_rows_kernel, dim3((unsigned)ceil_div(nseg, 256)), dim3(256), 0, (hipStream_t)stream, x_dev,
+                     M, K, scale, (_Float16 *)hi_dev, (_Float16 *)lo_dev);
+  CM_HIP(hipGetLastError());
+  return CM_OK;
+}
+
+extern "C" int cm_linear_f16x3(const void *ah_dev, const void *al_dev, int64_t M, int32_t K, const void *wh_dev,
+                               const void *wl_dev, const float *bias_dev, float out_scale, int32_t N, int32_t epilogue,
+                               float *c_dev, float next_scale, void *ch_dev, void *cl_dev, void *stream) {
+  if (M <= 0) return CM_OK;
+  if (!ah_dev || !al_dev || !wh_dev || !wl_dev) CM_FAIL(CM_EINVAL, "NULL argument");
+  if (K <= 0 || K % 64) CM_FAIL(CM_EINVAL, "K must be a positive multiple of 64");
+  if (N <= 0 || N % 64) CM_FAIL(CM_EINVAL, "N must be a positive multiple of 64");
+  if (epilogue == CM_EPI_PLANES_GELU ? (!ch_dev || !cl_dev) : !c_dev) CM_FAIL(CM_EINVAL, "NULL output");
+  if (epilogue != CM_EPI_BIAS && epilogue != CM_EPI_BIAS_GELU && epilogue != CM_EPI_PLANES_GELU)
+    CM_FAIL(CM_EINVAL, "unknown epilogue");
+  if (!g_n_cu) {
+    int dev = 0, n = 0;
+    CM_HIP(hipGetDevice(&dev));
+    CM_HIP(hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev));
+    g_n_cu = n > 0 ? n : 256;
+  }
+  const TileCfg t = pick_tile(M, N, g_n_cu);
+  const _Float16 *Ah = (const _Float16 *)ah_dev, *Al = (const _Float16 *)al_dev;
+  const _Float16 *Wh = (const _Float16 *)wh_dev, *Wl = (const _Float16 *)wl_dev;
+  _Float16 *Ch = (_Float16 *)ch_dev, *Cl = (_Float16 *)cl_dev;
+  hipStream_t st = (hipStream_t)stream;
+  if (t.bmb == 6)
+    return launch_tile<6, 12, 4>(Ah, Al, M, K, Wh, Wl, bias_dev, out_scale, N, epilogue, c_dev, next_scale, Ch, Cl, g_n_cu, st);
+  if (t.bmb == 8)
+    return launch_tile<8, 8, 4>(Ah, Al, M, K, Wh, Wl, bias_dev, out_scale, N, epilogue, c_dev, next_scale, Ch, Cl, g_n_cu, st);
+  if (t.bnb == 8)
+    return launch_tile<4, 8, 4>(Ah, Al, M, K, Wh, Wl, bias_dev, out_scale, N, epilogue, c_dev, next_scale, Ch, Cl, g_n_cu, st);
+  return launch_tile<4, 4, 4>(Ah, Al, M, K, Wh, Wl, bias_dev, out_scale, N, epilogue, c_dev, next_scale, Ch, Cl, g_n_cu, st);
+}

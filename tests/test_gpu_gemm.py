@@ -1,0 +1,117 @@
+"""K10 (cm_linear_f16x3): the E5 projections at fp32 accuracy on the f16 matrix cores.
+
+The reference runs every XLM-R projection as an fp32 nn.Linear (rag/embeddings/__init__.py:85-105,
+sentence-transformers on torch fp32).  The bar here is "as accurate as an fp32 GEMM": against an
+fp64 reference of the same product, K10's error must stay within 2x the error of torch's own fp32
+GEMM on the same GPU (hipBLASLt, exact fp32 MFMA) -- element-wise max and mean -- plus the GELU
+epilogue against torch's F.gelu (exact erf) of the fp64 product.  The E5 forward built on it is
+held to the Hugging Face fp32 module at 2e-5 (test_gpu_scale.py C3 at B = 32, S = 256, and the
+query shape B = 256, S = 24 below).
+"""
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _case(M, K, N, seed, xs=1.0, ws=0.02):
+    import torch
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    x = xs * torch.randn(M, K, device="cuda", generator=g)
+    w = ws * torch.randn(N, K, device="cuda", generator=g)
+    b = 0.1 * torch.randn(N, device="cuda", generator=g)
+    return x, w, b
+
+
+@pytest.mark.parametrize("M,K,N", [(6144, 768, 2304), (6144, 768, 768), (1000, 768, 3072), (37, 3072, 768),
+                                   (1, 768, 64), (129, 64, 192), (20000, 768, 3072), (8192, 3072, 768)])
+def test_linear_f16x3_fp32_accuracy(M, K, N):
+    import torch
+    from classmate_hip import engine
+    x, w, b = _case(M, K, N, seed=M + N)
+    W = engine.F16x3Weight(w, b)
+    got = engine.linear_f16x3(x, W)
+    torch.cuda.synchronize()
+    ref = x.double() @ w.double().T + b.double()
+    f32 = torch.nn.functional.linear(x, w, b).double()
+    e_ours = (got.double() - ref).abs()
+    e_f32 = (f32 - ref).abs()
+    print(f"\nK10 {M}x{K}x{N}: max err {float(e_ours.max()):.3e} (fp32 GEMM {float(e_f32.max()):.3e}), "
+          f"mean {float(e_ours.mean()):.3e} ({float(e_f32.mean()):.3e})")
+    assert float(e_ours.max()) <= 2 * float(e_f32.max()) + 1e-7
+    assert float(e_ours.mean()) <= 2 * float(e_f32.mean()) + 1e-9
+
+
+def test_linear_f16x3_gelu_epilogue_and_scales():
+    """GELU fused into the epilogue == F.gelu of the fp64 product (fp32 rounding), for activations
+    of widely different magnitudes (the power-of-two a_scale keeps them in f16 range)."""
+    import torch
+    from classmate_hip import engine
+    for xs, a_scale in ((1.0, 1.0), (1e-3, 2.0 ** 12), (3e3, 2.0 ** -4)):
+        x, w, b = _case(300, 768, 3072, seed=5, xs=xs)
+        W = engine.F16x3Weight(w, b)
+        got = engine.linear_f16x3(x, W, a_scale=a_scale, gelu=True)
+        ref64 = x.double() @ w.double().T + b.double()
+        ref = torch.nn.functional.gelu(ref64)
+        f32 = torch.nn.functional.gelu(torch.nn.functional.linear(x, w, b)).double()
+        e_ours, e_f32 = (got.double() - ref).abs(), (f32 - ref).abs()
+        assert float(e_ours.max()) <= 2 * float(e_f32.max()) + 1e-7, (xs, float(e_ours.max()), float(e_f32.max()))
+
+
+def test_linear_f16x3_rejects_bad_shapes():
+    import torch
+    from classmate_hip import engine
+    with pytest.raises(ValueError):
+        engine.F16x3Weight(torch.zeros(100, 768, device="cuda"))          # N % 64
+    W = engine.F16x3Weight(torch.ones(64, 96, device="cuda"))
+    with pytest.raises(ValueError):
+        engine.linear_f16x3(torch.zeros(4, 64, device="cuda"), W)          # K mismatch
+
+
+def test_e5_query_shape_f16x3_matches_hf_fp32():
+    """The bench's query encode (B = 256, S = 24, 12 layers, graph-captured lean forward on K10 +
+    cm_short_attention fp32 + K8 + K6) == the Hugging Face module in fp32 within 2e-5."""
+    import torch
+    from classmate_hip.embeddings import E5MultilingualEmbedder
+    emb = E5MultilingualEmbedder.random_init(seed=0, device="cuda", dtype="float32")
+    assert emb._lean_forward() is not None and emb.f16x3
+    B, S = 256, 24
+    g = torch.Generator(device="cuda").manual_seed(13)
+    ids = torch.randint(5, 250002, (B, S), device="cuda", generator=g)
+    ids[:, 0] = 0
+    ids[:, -1] = 2
+    mask = torch.ones_like(ids)
+    u_ids, _, u_out, graph = emb.capture_graph(B, S, unpadded=True)
+    u_ids.copy_(ids)
+    graph.replay()
+    torch.cuda.synchronize()
+    ref = emb._encode_hf(ids, mask)
+    err = float((u_out - ref).abs().max())
+    print(f"\nE5 f16x3 query encode vs HF fp32: max abs err {err:.2e}")
+    torch.testing.assert_close(u_out, ref, atol=2e-5, rtol=0)
+
+
+def test_plane_producers_match_split_rows():
+    """The fused producers (K8 add+LayerNorm, fp32 short attention, the GELU epilogue) write the
+    same planes, bit for bit, as splitting their fp32 outputs with cm_f16x3_split_rows."""
+    import torch
+    from classmate_hip import engine
+    torch.manual_seed(0)
+    B, S, D, H = 8, 24, 768, 12          # B * S = 192: whole 16-row plane blocks, no pad rows compared
+    x = torch.randn(B, S, D, device="cuda")
+    r = torch.randn(S, D, device="cuda")
+    g, b = 1 + 0.1 * torch.randn(D, device="cuda"), 0.1 * torch.randn(D, device="cuda")
+    out, p = engine.add_layernorm_split(x, r, g, b, 1e-5, 2.0 ** 9)
+    assert torch.equal(out, engine.add_layernorm(x, r, g, b, 1e-5))
+    q = engine.split_rows(out, 2.0 ** 9)
+    n = B * S * D
+    assert torch.equal(p.hi.view(-1)[:n], q.hi.view(-1)[:n]) and torch.equal(p.lo.view(-1)[:n], q.lo.view(-1)[:n])
+    qkv = torch.randn(B, S, 3 * D, device="cuda")
+    pa = engine.short_attention_split(qkv, H, 0.125, 2.0 ** 10)
+    qa = engine.split_rows(engine.short_attention(qkv, H, 0.125), 2.0 ** 10)
+    assert torch.equal(pa.hi.view(-1)[:n], qa.hi.view(-1)[:n]) and torch.equal(pa.lo.view(-1)[:n], qa.lo.view(-1)[:n])
+    w = 0.02 * torch.randn(3072, D, device="cuda")
+    W = engine.F16x3Weight(w, 0.1 * torch.randn(3072, device="cuda"))
+    hp = engine.linear_f16x3(p, W, gelu=True, planes_out=2.0 ** 11)
+    hq = engine.split_rows(engine.linear_f16x3(p, W, gelu=True), 2.0 ** 11)
+    m = B * S * 3072
+    assert torch.equal(hp.hi.view(-1)[:m], hq.hi.view(-1)[:m]) and torch.equal(hp.lo.view(-1)[:m], hq.lo.view(-1)[:m])

@@ -5,9 +5,9 @@ set -o pipefail
 name=$1; kern=$2; shift 3
 mkdir -p gpurun_out; export TMPDIR=/tmp
 i=0
-for set in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS" \
-           "SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_SMEM SQ_WAIT_INST_LDS SQ_INSTS_VALU_MFMA_MOPS_F16 SQ_VALU_MFMA_BUSY_CYCLES" \
-           "FETCH_SIZE GRBM_GUI_ACTIVE"; do
+SETS=${PMC_SETS:-"SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS;SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_SMEM SQ_WAIT_INST_LDS SQ_INSTS_VALU_MFMA_MOPS_F16 SQ_VALU_MFMA_BUSY_CYCLES;FETCH_SIZE GRBM_GUI_ACTIVE"}
+IFS=';' read -ra SETARR <<< "$SETS"
+for set in "${SETARR[@]}"; do
   i=$((i+1))
   timeout -k 10 600 rocprofv3 --pmc $set -d gpurun_out/pmc_${name}_$i -o pmc --output-format csv -- "$@" > gpurun_out/pmc_${name}_$i.log 2>&1 || { tail -20 gpurun_out/pmc_${name}_$i.log; exit 1; }
 done
