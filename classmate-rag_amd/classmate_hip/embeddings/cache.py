@@ -8,7 +8,11 @@ unchanged: one ``<root>/<model>/<mode>/<sha1(text.strip())>.npy`` fp32 vector pe
 * model sub-directory from ``base.model.name_or_path`` else ``base.model_name`` else
   ``unknown-model``, sanitised to ``[A-Za-z0-9._-]`` (cache.py:52-59); a base embedder running
   below the reference's fp32 (``dtype`` bfloat16, the opt-in fast path) gets ``__bfloat16``
-  appended, so its vectors never mix with fp32 ones under the same key;
+  appended, so its vectors never mix with fp32 ones under the same key.  fp32 (the default
+  since round 2, and the reference's precision) keeps the reference's unsuffixed directory, so
+  an existing reference cache is reused; a directory written by a round-1 build of this package
+  (whose default was bf16, unsuffixed) must be cleared -- this build marks the directories it
+  writes with ``.classmate_hip_dtype`` and refuses an unsuffixed directory marked otherwise;
 * a file that fails to load is a miss (cache.py:100-106); write errors are swallowed (cache.py:136-141);
 * all misses of one call go to the base embedder as ONE batch, in input order, duplicates
   included (cache.py:132-133) — with the HIP E5 path that is one padded forward + the K6
@@ -55,6 +59,16 @@ class CachingEmbedder:
         self.root = Path(root).expanduser().resolve()
         self.model_dir = self.root / _model_dirname(base)
         self.model_dir.mkdir(parents=True, exist_ok=True)
+        dt = str(getattr(base, "dtype", "") or "float32").rsplit(".", 1)[-1]
+        marker = self.model_dir / ".classmate_hip_dtype"
+        try:
+            prev = marker.read_text().strip() if marker.exists() else None
+            if prev is not None and prev != dt:
+                raise ValueError(f"embedding cache {self.model_dir} holds {prev} vectors, this embedder is {dt}")
+            if prev is None:
+                marker.write_text(dt + "\n")
+        except OSError:
+            pass
 
     def _key_path(self, mode: str, text: str) -> Path:
         return self.model_dir / mode / f"{_text_key(text)}.npy"

@@ -647,9 +647,10 @@ def _pow2_at_most(x: float) -> float:
 
 
 class F16x3Weight:
-    """An nn.Linear weight (N, K) fp32 prepared for ``linear_f16x3``: the two f16 halves of
-    W * scale in the fragment-major order the kernel streams (cm_f16x3_split_weights), scale a
-    power of two putting max|W| in [2^14, 2^15).  Keeps the fp32 bias (or None)."""
+    """An nn.Linear weight (N, K) fp32 prepared for ``linear_f16x3``: the split blocks (f16 hi
+    and lo halves) of W * scale in the fragment-major order the kernel streams
+    (cm_f16x3_split_weights), scale a power of two putting max|W| in [2^14, 2^15).  Keeps the fp32
+    bias (or None)."""
 
     def __init__(self, weight, bias=None):
         if weight.dtype != torch.float32 or weight.dim() != 2 or not weight.is_cuda:
@@ -661,26 +662,32 @@ class F16x3Weight:
         amax = float(w.abs().max())
         self.scale = (2.0 ** 14) / _pow2_at_most(amax) if amax > 0 else 1.0
         self.N, self.K = N, K
-        self.hi = torch.empty((N, K), dtype=torch.float16, device=w.device)
-        self.lo = torch.empty((N, K), dtype=torch.float16, device=w.device)
+        self.planes = torch.empty((N, K, 2), dtype=torch.float16, device=w.device)   # split blocks
         self.bias = bias.detach().float().contiguous() if bias is not None else None
         if self.bias is not None and self.bias.numel() != N:
             raise ValueError("bias must have N elements")
-        L.check(L.fn["cm_f16x3_split_weights"](L.ptr(w), N, K, float(self.scale), L.ptr(self.hi), L.ptr(self.lo),
+        L.check(L.fn["cm_f16x3_split_weights"](L.ptr(w), N, K, float(self.scale), L.ptr(self.planes),
                                                _stream(w.device.index)), "cm_f16x3_split_weights")
 
 
 class Planes:
-    """An M x K fp32 matrix as K10 split planes: hi/lo f16 tensors of (ceil(M/16)*16, K) in the
-    fragment-major order (include/classmate_hip.h), holding the values times ``scale``."""
+    """An M x K fp32 matrix as K10 split planes: one f16 buffer of cm_f16x3_plane_rows(M) x K x 2
+    halves (2 KiB split blocks [hi 1 KiB][lo 1 KiB], fragment-major; include/classmate_hip.h),
+    holding the values times ``scale``."""
 
-    __slots__ = ("hi", "lo", "M", "K", "scale")
+    __slots__ = ("data", "M", "K", "scale")
 
     def __init__(self, M: int, K: int, scale: float, device):
-        rows = -(-M // 16) * 16
-        self.hi = torch.empty((rows, K), dtype=torch.float16, device=device)
-        self.lo = torch.empty((rows, K), dtype=torch.float16, device=device)
+        rows = int(L.fn["cm_f16x3_plane_rows"](int(M)))
+        self.data = torch.empty((max(rows, 1), K, 2), dtype=torch.float16, device=device)
         self.M, self.K, self.scale = M, K, float(scale)
+
+    def halves(self):
+        """(hi, lo) f16 views of rows 0 .. M-1 in row-major (M, K) order (for tests)."""
+        kb = self.K // 32
+        blk = self.data.view(-1, kb, 2, 4, 16, 8)          # [row block][kb][plane][g][c][e]
+        v = blk.permute(2, 0, 4, 1, 3, 5).reshape(2, -1, self.K)   # [plane][row][k]
+        return v[0, :self.M], v[1, :self.M]
 
 
 def split_rows(x, scale: float = 1.0) -> Planes:
@@ -690,7 +697,7 @@ def split_rows(x, scale: float = 1.0) -> Planes:
     x = x.contiguous()
     K = x.shape[-1]
     p = Planes(x.numel() // K, K, scale, x.device)
-    L.check(L.fn["cm_f16x3_split_rows"](L.ptr(x), p.M, K, p.scale, L.ptr(p.hi), L.ptr(p.lo), _stream(x.device.index)),
+    L.check(L.fn["cm_f16x3_split_rows"](L.ptr(x), p.M, K, p.scale, L.ptr(p.data), _stream(x.device.index)),
             "cm_f16x3_split_rows")
     return p
 
@@ -710,20 +717,20 @@ def linear_f16x3(x, w: "F16x3Weight", a_scale: float = 1.0, gelu: bool = False, 
         lead = (x.M,)
     if x.K != w.K:
         raise ValueError(f"planes have K={x.K}, the weight K={w.K}")
-    dev = x.hi.device
-    common = (L.ptr(x.hi), L.ptr(x.lo), x.M, w.K, L.ptr(w.hi), L.ptr(w.lo),
-              L.ptr(w.bias) if w.bias is not None else None, float(1.0 / (x.scale * w.scale)), w.N)
+    dev = x.data.device
+    common = (L.ptr(x.data), x.M, w.K, L.ptr(w.planes), L.ptr(w.bias) if w.bias is not None else None,
+              float(1.0 / (x.scale * w.scale)), w.N)
     if planes_out:
         if not gelu:
             raise ValueError("planes_out is the fused FFN-up epilogue: gelu=True")
         p = Planes(x.M, w.N, planes_out, dev)
-        L.check(L.fn["cm_linear_f16x3"](*common, L.CM_EPI_PLANES_GELU, None, p.scale, L.ptr(p.hi), L.ptr(p.lo),
+        L.check(L.fn["cm_linear_f16x3"](*common, L.CM_EPI_PLANES_GELU, None, p.scale, L.ptr(p.data),
                                         _stream(dev.index)), "cm_linear_f16x3")
         return p
     if out is None:
         out = torch.empty((*lead, w.N), dtype=torch.float32, device=dev)
     L.check(L.fn["cm_linear_f16x3"](*common, L.CM_EPI_BIAS_GELU if gelu else L.CM_EPI_BIAS, L.ptr(out), 0.0, None,
-                                    None, _stream(dev.index)), "cm_linear_f16x3")
+                                    _stream(dev.index)), "cm_linear_f16x3")
     return out
 
 
@@ -744,7 +751,7 @@ def add_layernorm_split(x, r, weight, bias, eps: float, a_scale: float, out=None
     p = Planes(rows, D, a_scale, x.device)
     L.check(L.fn["cm_add_layernorm_split"](L.ptr(x), L.ptr(r) if r is not None else None,
                                            (r.numel() // D) if r is not None else 0, L.ptr(weight), L.ptr(bias), rows,
-                                           D, float(eps), L.ptr(out), p.scale, L.ptr(p.hi), L.ptr(p.lo),
+                                           D, float(eps), L.ptr(out), p.scale, L.ptr(p.data),
                                            _stream(x.device.index)), "cm_add_layernorm_split")
     return out, p
 
@@ -756,8 +763,8 @@ def short_attention_split(qkv, heads: int, scale: float, a_scale: float) -> Plan
         raise ValueError("qkv must be fp32 (B, S<=64, 3*heads*64)")
     qkv = qkv.contiguous()
     p = Planes(B * S, heads * 64, a_scale, qkv.device)
-    L.check(L.fn["cm_short_attention_split"](L.ptr(qkv), B, S, heads, 64, float(scale), p.scale, L.ptr(p.hi),
-                                             L.ptr(p.lo), _stream(qkv.device.index)), "cm_short_attention_split")
+    L.check(L.fn["cm_short_attention_split"](L.ptr(qkv), B, S, heads, 64, float(scale), p.scale, L.ptr(p.data),
+                                             _stream(qkv.device.index)), "cm_short_attention_split")
     return p
 
 # ---------------------------------------------------------------------------

@@ -225,7 +225,7 @@ class GpuVectorStore:
         # k beyond the fused kernels' lists (cm_max_topk) runs the full-order device path
         return self._index.search(q, k, allow, return_vectors=include_embeddings)
 
-    def _items(self, dist, rows, vecs, i, include_documents, include_embeddings) -> List[Dict[str, Any]]:
+    def _items(self, dist, rows, vecs, i, include_documents, include_embeddings, copy=False) -> List[Dict[str, Any]]:
         out = []
         for j in range(rows.shape[1]):
             r = int(rows[i, j])
@@ -234,8 +234,10 @@ class GpuVectorStore:
             item = {"id": self._ids[r], "document": self._docs[r] if include_documents else None,
                     "metadata": self._meta.metas[r],
                     "distance": float(dist[i, j])}
-            if include_embeddings:   # a row view of this call's own (B, k, D) fp32 buffer
-                item["embedding"] = vecs[i, j]
+            if include_embeddings:
+                # query(): an independent array per item, as Chroma returns; query_batch(): a
+                # read-only row view of the call's own (B, k, D) buffer (zero-copy for the MMR pool)
+                item["embedding"] = np.array(vecs[i, j]) if copy else vecs[i, j]
             out.append(item)
         return out
 
@@ -249,7 +251,7 @@ class GpuVectorStore:
             return []
         dist, rows = res[0], res[1]
         vecs = res[2] if include_embeddings else None
-        return self._items(dist, rows, vecs, 0, include_documents, include_embeddings)
+        return self._items(dist, rows, vecs, 0, include_documents, include_embeddings, copy=True)
 
     def query_batch(self, *, query_embeddings: np.ndarray, where: Optional[Dict[str, Any]] = None, top_k: int = 8,
                     include_documents: bool = True, include_embeddings: bool = False) -> List[List[Dict[str, Any]]]:
@@ -259,6 +261,8 @@ class GpuVectorStore:
             return [[] for _ in range(q.shape[0])]
         dist, rows = res[0], res[1]
         vecs = res[2] if include_embeddings else None
+        if vecs is not None:
+            vecs.setflags(write=False)   # the items share it: an in-place edit must not reach the others
         return [self._items(dist, rows, vecs, i, include_documents, include_embeddings) for i in range(q.shape[0])]
 
     # ---- admin ------------------------------------------------------------------

@@ -137,11 +137,17 @@ struct KernelTimer {
   }
 };
 
-// K10 split planes (cm_gemm.hip): fp32 v = hi + lo as two f16 halves, stored fragment-major --
-// element (row, k) of an M x K matrix with kb32 = K / 32 lives at this offset (in halves) of
-// each plane: [row / 16][k / 32][lane slot (row % 16) + 16 ((k % 32) / 8)][k % 8]
+// K10 split planes (cm_gemm.hip): fp32 v = hi + lo as two f16 halves.  An M x K matrix is one
+// buffer of 2 KiB "split blocks": block (row / 16, k / 32) = [hi 1 KiB][lo 1 KiB], each half in
+// fragment-major order (lane slot (row % 16) + 16 ((k % 32) / 8), 8 halves of k).  Offset (in
+// halves) of the hi element; the lo element is 512 halves after it.  Buffers hold
+// f16x3_plane_rows(M) rows (a multiple of every K10 tile height: the last tile reads no clamp).
+constexpr int64_t kF16x3RowAlign = 384;
+__host__ __device__ inline int64_t f16x3_plane_rows(int64_t M) {
+  return (M + kF16x3RowAlign - 1) / kF16x3RowAlign * kF16x3RowAlign;
+}
 __host__ __device__ inline int64_t f16x3_plane_off(int64_t row, int k, int kb32) {
-  return (((row >> 4) * kb32 + (k >> 5)) * 64 + (row & 15) + 16 * ((k & 31) >> 3)) * 8 + (k & 7);
+  return (((row >> 4) * kb32 + (k >> 5)) * 128 + (row & 15) + 16 * ((k & 31) >> 3)) * 8 + (k & 7);
 }
 __device__ inline void f16x3_split1(float a, _Float16 &h, _Float16 &l) {
   h = (_Float16)a;

@@ -50,7 +50,7 @@ template <typename T, int PER, bool SPLIT = false>
 __global__ void __launch_bounds__(64 * kLnWaves)
     add_layernorm_kernel(const T *x, const T *__restrict__ r, int64_t r_rows, const T *__restrict__ gamma,
                          const T *__restrict__ beta, int64_t rows, int D, float eps, T *out, float a_scale = 1.f,
-                         _Float16 *__restrict__ ph = nullptr, _Float16 *__restrict__ pl = nullptr) {
+                         _Float16 *__restrict__ ph = nullptr) {
   const int lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * kLnWaves + (threadIdx.x >> 6);
   if (row >= rows) return;  // whole wave exits together
@@ -116,7 +116,7 @@ __global__ void __launch_bounds__(64 * kLnWaves)
         }
         const int64_t off = f16x3_plane_off(row, 4 * c, D >> 5);
         *reinterpret_cast<h4 *>(ph + off) = hh;
-        *reinterpret_cast<h4 *>(pl + off) = ll;
+        *reinterpret_cast<h4 *>(ph + off + 512) = ll;
       }
     }
   }
@@ -124,10 +124,10 @@ __global__ void __launch_bounds__(64 * kLnWaves)
 
 template <int PER>
 int launch_add_ln_split(const float *x, const float *r, int64_t r_rows, const float *g, const float *b, int64_t rows,
-                        int D, float eps, float *out, float a_scale, _Float16 *ph, _Float16 *pl, hipStream_t st) {
+                        int D, float eps, float *out, float a_scale, _Float16 *ph, hipStream_t st) {
   const dim3 grid((unsigned)ceil_div(rows, kLnWaves)), block(64 * kLnWaves);
   hipLaunchKernelGGL((add_layernorm_kernel<float, PER, true>), grid, block, 0, st, x, r, r_rows, g, b, rows, D, eps,
-                     out, a_scale, ph, pl);
+                     out, a_scale, ph);
   CM_HIP(hipGetLastError());
   return CM_OK;
 }
@@ -190,8 +190,7 @@ __device__ inline void ld8(const __hip_bfloat16 *p, float (&v)[8]) {
 template <typename T, bool SPLIT = false>
 __global__ void __launch_bounds__(64) short_attention_kernel(const T *__restrict__ qkv, int S, int H, float scale,
                                                              T *__restrict__ out, float a_scale = 1.f,
-                                                             _Float16 *__restrict__ ph = nullptr,
-                                                             _Float16 *__restrict__ pl = nullptr) {
+                                                             _Float16 *__restrict__ ph = nullptr) {
   constexpr int VPR = kAttnDh * sizeof(T) / 16;  // 16-byte vectors per head row
   __shared__ __attribute__((aligned(16))) T ks[kAttnMaxS * kAttnDh];
   __shared__ __attribute__((aligned(16))) T vs[kAttnMaxS * kAttnDh];
@@ -262,7 +261,7 @@ __global__ void __launch_bounds__(64) short_attention_kernel(const T *__restrict
       }
       const int64_t off = f16x3_plane_off(row, h * kAttnDh + 8 * c, kb32);
       *reinterpret_cast<h8 *>(ph + off) = hh;
-      *reinterpret_cast<h8 *>(pl + off) = ll;
+      *reinterpret_cast<h8 *>(ph + off + 512) = ll;
     }
   } else {
     T *orow = out + (b * S + lane) * (int64_t)H * kAttnDh + (int64_t)h * kAttnDh;
@@ -428,31 +427,30 @@ extern "C" int cm_short_attention(const void *qkv_dev, int32_t B, int32_t S, int
 
 extern "C" int cm_add_layernorm_split(const float *x_dev, const float *r_dev, int64_t r_rows, const float *gamma_dev,
                                       const float *beta_dev, int64_t rows, int32_t D, float eps, float *out_dev,
-                                      float a_scale, void *hi_dev, void *lo_dev, void *stream) {
+                                      float a_scale, void *planes_dev, void *stream) {
   if (rows <= 0) return CM_OK;
-  if (!x_dev || !gamma_dev || !beta_dev || !out_dev || !hi_dev || !lo_dev) CM_FAIL(CM_EINVAL, "NULL argument");
+  if (!x_dev || !gamma_dev || !beta_dev || !out_dev || !planes_dev) CM_FAIL(CM_EINVAL, "NULL argument");
   if (D <= 0 || D % 32 != 0 || D > 4 * 64 * kLnMaxPer) CM_FAIL(CM_EINVAL, "D must be a multiple of 32, <= 2048");
   if (r_dev && r_rows <= 0) CM_FAIL(CM_EINVAL, "r_rows must be > 0 with a residual");
   hipStream_t st = (hipStream_t)stream;
-  _Float16 *ph = (_Float16 *)hi_dev, *pl = (_Float16 *)lo_dev;
+  _Float16 *ph = (_Float16 *)planes_dev;
   switch ((int)ceil_div(D / 4, 64)) {
-    case 1: return launch_add_ln_split<1>(x_dev, r_dev, r_rows, gamma_dev, beta_dev, rows, D, eps, out_dev, a_scale, ph, pl, st);
-    case 2: return launch_add_ln_split<2>(x_dev, r_dev, r_rows, gamma_dev, beta_dev, rows, D, eps, out_dev, a_scale, ph, pl, st);
-    case 3: return launch_add_ln_split<3>(x_dev, r_dev, r_rows, gamma_dev, beta_dev, rows, D, eps, out_dev, a_scale, ph, pl, st);
-    case 4: return launch_add_ln_split<4>(x_dev, r_dev, r_rows, gamma_dev, beta_dev, rows, D, eps, out_dev, a_scale, ph, pl, st);
-    default: return launch_add_ln_split<8>(x_dev, r_dev, r_rows, gamma_dev, beta_dev, rows, D, eps, out_dev, a_scale, ph, pl, st);
+    case 1: return launch_add_ln_split<1>(x_dev, r_dev, r_rows, gamma_dev, beta_dev, rows, D, eps, out_dev, a_scale, ph, st);
+    case 2: return launch_add_ln_split<2>(x_dev, r_dev, r_rows, gamma_dev, beta_dev, rows, D, eps, out_dev, a_scale, ph, st);
+    case 3: return launch_add_ln_split<3>(x_dev, r_dev, r_rows, gamma_dev, beta_dev, rows, D, eps, out_dev, a_scale, ph, st);
+    case 4: return launch_add_ln_split<4>(x_dev, r_dev, r_rows, gamma_dev, beta_dev, rows, D, eps, out_dev, a_scale, ph, st);
+    default: return launch_add_ln_split<8>(x_dev, r_dev, r_rows, gamma_dev, beta_dev, rows, D, eps, out_dev, a_scale, ph, st);
   }
 }
 
 extern "C" int cm_short_attention_split(const float *qkv_dev, int32_t B, int32_t S, int32_t H, int32_t head_dim,
-                                        float scale, float a_scale, void *hi_dev, void *lo_dev, void *stream) {
+                                        float scale, float a_scale, void *planes_dev, void *stream) {
   if (B <= 0) return CM_OK;
-  if (!qkv_dev || !hi_dev || !lo_dev) CM_FAIL(CM_EINVAL, "NULL argument");
+  if (!qkv_dev || !planes_dev) CM_FAIL(CM_EINVAL, "NULL argument");
   if (head_dim != kAttnDh) CM_FAIL(CM_EINVAL, "head_dim must be 64");
   if (S <= 0 || S > kAttnMaxS || H <= 0) CM_FAIL(CM_EINVAL, "need 0 < S <= 64 and H > 0");
   hipLaunchKernelGGL((short_attention_kernel<float, true>), dim3((unsigned)((int64_t)B * H)), dim3(64), 0,
-                     (hipStream_t)stream, qkv_dev, S, H, scale, nullptr, a_scale, (_Float16 *)hi_dev,
-                     (_Float16 *)lo_dev);
+                     (hipStream_t)stream, qkv_dev, S, H, scale, nullptr, a_scale, (_Float16 *)planes_dev);
   CM_HIP(hipGetLastError());
   return CM_OK;
 }

@@ -20,31 +20,32 @@
 // 2^15; an activation below 2^-14 / a_scale contributes an absolute error < 2^-25 / a_scale.
 // Both scales are exact powers of two, undone exactly in the epilogue (out_scale).
 //
-// Split-plane layout ("planes", HBM): a row-major M x K fp32 matrix becomes two f16 planes,
-// hi and lo, each [ceil(M/16)][K/32][64 lanes][8] -- fragment-major: the 1 KiB block
-// (rows 16 b .. +15, k 32 kb .. +31) holds in lane slot (c, g) = c + 16 g the 8 halves of row
-// 16 b + c, k = 32 kb + 8 g .. + 7, which is exactly what lane c + 16 g feeds to
-// v_mfma_f32_16x16x32_f16 as its A (row) or B (column) operand.  Weights W (N x K, nn.Linear
-// layout) use the same order with N as the row index.  Every operand load of the GEMM is then
-// one global_load_lds_dwordx4 wave-instruction per 1 KiB block (8 full 128-B lines), read back
-// from LDS with a conflict-free ds_read_b128 at lane*16.  Rows of the last block beyond M hold
-// whatever the producer left: they only reach output rows >= M, which are never stored.
+// Split-plane layout ("planes", HBM): a row-major M x K fp32 matrix becomes one buffer of 2 KiB
+// split blocks [row / 16][k / 32] = [hi 1 KiB][lo 1 KiB]; each 1 KiB half is fragment-major:
+// lane slot (c, g) = c + 16 g holds the 8 halves of row 16 b + c, k = 32 kb + 8 g .. + 7, which
+// is exactly what lane c + 16 g feeds to v_mfma_f32_16x16x32_f16 as its A (row) or B (column)
+// operand.  Weights W (N x K, nn.Linear layout) use the same order with N as the row index.
+// Every operand load of the GEMM is one global_load_lds_dwordx4 wave-instruction per 1 KiB
+// (8 full 128-B lines), read back with a conflict-free ds_read_b128 at lane*16; a k-step of a
+// row block is one contiguous 2 KiB run.  Buffers hold f16x3_plane_rows(M) rows (a multiple of
+// 384, every tile height): rows >= M hold whatever the producer left and only reach output rows
+// >= M, which are never stored as fp32 (planes outputs carry them along as padding).
 //
 // Producers of planes: cm_f16x3_split_rows (any fp32 matrix), cm_add_layernorm_split (the
 // XLM-R residual + LayerNorm, also writing the fp32 rows the next residual needs),
 // cm_short_attention_split (query-batch attention) and this GEMM's own GELU epilogue
 // (FFN-up -> FFN-down: the intermediate exists only as planes).
 //
-// GEMM (linear_f16x3_kernel): one workgroup of 4 waves (2 x 2) per BM x BN output tile, one
-// workgroup per CU (the ring takes most of the LDS).  The k loop runs over 32-wide steps
-// through an S-stage LDS ring; stage = A_hi | A_lo (BM/16 blocks each) | B_hi | B_lo (BN/16
-// each), all filled by LDS-DMA: per step each wave waits (counted vmcnt) for its own pieces of
-// the step's stage, one raw s_barrier publishes everyone's pieces and retires every read of
-// the previous step's stage, the wave issues its pieces of stage t + S - 1 into that freed
-// slot, then reads its fragments and issues 3 (BM/32)(BN/32) MFMAs.  No VGPR staging, no
-// VALU work in the loop: the DMA of S - 1 steps ahead overlaps the MFMAs.  Tiles map
-// XCD-major (bijective remap) so the column tiles of one row block share its A rows in one
-// XCD's L2.
+// GEMM (linear_f16x3_kernel): a persistent grid of one workgroup (4 waves, 2 x 2) per CU; each
+// runs its output tiles' k-steps as one stream through an S-stage LDS ring (stage = the tile's
+// BM/16 A split blocks then its BN/16 weight split blocks of one 32-wide k-step), all filled by
+// LDS-DMA.  Per step: the first row tile's MFMAs, a counted vmcnt wait for the next stage + one
+// raw s_barrier (publishes it, retires every read of this step's slot), then the remaining
+// MFMAs with the next step's 18 fragment reads and this wave's DMA pieces of stage g + S
+// threaded between them (sched_group_barrier).  No VGPR staging and no address arithmetic in
+// the loop beyond one scalar add: per-piece offsets are fixed, per-tile bases change once per
+// tile.  Tile order: XCD x takes a contiguous chunk of a grouped (8 row tiles per column
+// sweep) order, so concurrently running tiles share A rows and weight columns in its L2.
 #include "cm_common.h"
 
 #include <algorithm>
@@ -58,7 +59,16 @@ typedef float g32x4 __attribute__((ext_vector_type(4)));
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ h16x8 as_h8(i32x4 v) { return __builtin_bit_cast(h16x8, v); }
 
-constexpr int kGemmThreads = 256;
+#ifndef K10_W6
+#define K10_W6 12              // waves per workgroup at the 96 x 192 tile (2 x 6: three per SIMD)
+#endif
+
+// Timing ablations for variant builds only (tools/build_k10_variant.sh; the product build has
+// K10_ABL = 0): bit 0 no MFMA, bit 1 no DMA, bit 2 every DMA reads k-step 0 of the tile (an
+// L2-resident source), bit 3 no epilogue stores.  Results are wrong in every ablated build.
+#ifndef K10_ABL
+#define K10_ABL 0
+#endif
 
 __device__ inline float gelu_erf(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
 
@@ -73,24 +83,27 @@ __device__ inline void split8(const float (&x)[8], float s, h16x8 &hi, h16x8 &lo
   }
 }
 
-// bijective XCD-major remap (MI355X: consecutive workgroup ids go round-robin over 8 XCDs)
-__device__ inline int xcd_remap(int orig, int nwg) {
-  const int xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
-  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
-}
-
 enum { kEpiF32 = 0, kEpiF32Gelu = 1, kEpiPlanesGelu = 2 };
+
+// Tile order of the persistent schedule: 8 row tiles per column sweep ("grouped").
+__device__ __forceinline__ void k10_tile(int L, int tiles_m, int tiles_n, int &tm, int &tn) {
+  const int per_group = 8 * tiles_n;
+  const int first_m = (L / per_group) * 8;
+  const int gsz = min(tiles_m - first_m, 8);
+  const int rem = L % per_group;
+  tm = first_m + rem % gsz;
+  tn = rem / gsz;
+}
 
 // Epilogue of one tile for one wave, straight from the accumulators (no LDS: the ring keeps
 // all of it).  fp32 rows: lane (g, c) stores rows 4 g + r of column c (16 consecutive floats per
 // row and store).  Planes: lanes c and c ^ 1 swap half their halves (DPP quad_perm 1,0,3,2) so
 // that each lane stores 4-byte column pairs (c even: rows 0-1, c odd: rows 2-3 of its group).
-template <int BMB, int BNB, int EPI>
-__device__ __forceinline__ void k10_epilogue(g32x4 (&acc)[BMB / 2][BNB / 2], int tm, int tn, int wr, int wc, int lane,
-                                             const float *btab, float out_scale, float next_scale, int64_t M, int N,
-                                             int64_t mblocks, float *__restrict__ Cout, _Float16 *__restrict__ Ch,
-                                             _Float16 *__restrict__ Cl) {
-  constexpr int WMT = BMB / 2, WNT = BNB / 2;
+template <int BMB, int BNB, int NW, int EPI>
+__device__ __forceinline__ void k10_epilogue(g32x4 (&acc)[BMB / 2][BNB / (NW / 2)], int tm, int tn, int wr, int wc,
+                                             int lane, const float *btab, float out_scale, float next_scale,
+                                             int64_t M, int N, float *__restrict__ Cout, _Float16 *__restrict__ Cp) {
+  constexpr int WMT = BMB / 2, WNT = BNB / (NW / 2);
   const int g4 = lane >> 4, c16 = lane & 15;
   const int64_t rb0 = (int64_t)tm * BMB + wr * WMT;    // this wave's first row block
   const int cbase = (tn * BNB + wc * WNT) * 16;        // its first column
@@ -123,21 +136,18 @@ __device__ __forceinline__ void k10_epilogue(g32x4 (&acc)[BMB / 2][BNB / 2], int
         const uint32_t sl = odd ? (ll[0] | ll[1] << 16) : (ll[2] | ll[3] << 16);
         const uint32_t rh = (uint32_t)__builtin_amdgcn_mov_dpp((int)sh, 0xB1, 0xF, 0xF, false);
         const uint32_t rl = (uint32_t)__builtin_amdgcn_mov_dpp((int)sl, 0xB1, 0xF, 0xF, false);
-        const int64_t grb = rb0 + i;
-        if (grb < mblocks) {
-          const int r0 = odd ? 2 : 0;
-          const int c0 = col & ~1;
+        const int r0 = odd ? 2 : 0;
+        const int c0 = col & ~1;
 #pragma unroll
-          for (int q = 0; q < 2; ++q) {
-            const uint32_t mine_h = hh[r0 + q], mine_l = ll[r0 + q];
-            const uint32_t oth_h = (rh >> (16 * q)) & 0xffffu, oth_l = (rl >> (16 * q)) & 0xffffu;
-            // column c0 (even) in the low half, c0 + 1 in the high half
-            const uint32_t wh = odd ? (oth_h | mine_h << 16) : (mine_h | oth_h << 16);
-            const uint32_t wl = odd ? (oth_l | mine_l << 16) : (mine_l | oth_l << 16);
-            const int64_t off = f16x3_plane_off(grb * 16 + 4 * g4 + r0 + q, c0, N >> 5);
-            *reinterpret_cast<uint32_t *>(Ch + off) = wh;
-            *reinterpret_cast<uint32_t *>(Cl + off) = wl;
-          }
+        for (int q = 0; q < 2; ++q) {
+          const uint32_t mine_h = hh[r0 + q], mine_l = ll[r0 + q];
+          const uint32_t oth_h = (rh >> (16 * q)) & 0xffffu, oth_l = (rl >> (16 * q)) & 0xffffu;
+          // column c0 (even) in the low half, c0 + 1 in the high half
+          const uint32_t wh = odd ? (oth_h | mine_h << 16) : (mine_h | oth_h << 16);
+          const uint32_t wl = odd ? (oth_l | mine_l << 16) : (mine_l | oth_l << 16);
+          const int64_t off = f16x3_plane_off((rb0 + i) * 16 + 4 * g4 + r0 + q, c0, N >> 5);
+          *reinterpret_cast<uint32_t *>(Cp + off) = wh;
+          *reinterpret_cast<uint32_t *>(Cp + off + 512) = wl;
         }
       }
       acc[i][j] = g32x4{0.f, 0.f, 0.f, 0.f};
@@ -145,70 +155,34 @@ __device__ __forceinline__ void k10_epilogue(g32x4 (&acc)[BMB / 2][BNB / 2], int
   }
 }
 
-// Tile order of the persistent schedule: 8 row tiles per column sweep ("grouped"), so tiles that
-// run concurrently share A rows and weight columns in L2.
-__device__ __forceinline__ void k10_tile(int L, int tiles_m, int tiles_n, int &tm, int &tn) {
-  const int per_group = 8 * tiles_n;
-  const int first_m = (L / per_group) * 8;
-  const int gsz = min(tiles_m - first_m, 8);
-  const int rem = L % per_group;
-  tm = first_m + rem % gsz;
-  tn = rem / gsz;
-}
-
-// One stage's DMA for this wave: PCS 1 KiB fragment blocks (o = 4 i + wave) of k-step kt of
-// tile (tm, tn) into ring slot `st`.
-template <int BMB, int BNB, int PCS>
-__device__ __forceinline__ void k10_issue(unsigned char *st, const _Float16 *Ah, const _Float16 *Al,
-                                          const _Float16 *Wh, const _Float16 *Wl, int64_t mblocks, int kb32,
-                                          int tm, int tn, int kt, int wave, int lane) {
-  const int64_t mb0 = (int64_t)tm * BMB;
-  const int nb0 = tn * BNB;
-#pragma unroll
-  for (int i = 0; i < PCS; ++i) {
-    const int o = 4 * i + wave;
-    const _Float16 *plane;
-    int64_t blkrow;
-    if (o < 2 * BMB) {
-      plane = o < BMB ? Ah : Al;
-      const int64_t rb = mb0 + (o < BMB ? o : o - BMB);
-      blkrow = rb < mblocks ? rb : mblocks - 1;       // clamp: duplicate rows feed unstored outputs
-    } else {
-      const int ob = o - 2 * BMB;
-      plane = ob < BNB ? Wh : Wl;
-      blkrow = nb0 + (ob < BNB ? ob : ob - BNB);
-    }
-    const unsigned char *src = (const unsigned char *)plane + ((blkrow * kb32 + kt) << 10) + lane * 16;
-    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)src,
-                                     (__attribute__((address_space(3))) void *)(st + o * 1024), 16, 0, 0);
-  }
-}
-
-// BMB x BNB fragment blocks (16 x 16 outputs each) per tile, 2 x 2 waves, S-stage ring.
-// Persistent: gridDim.x <= #CUs workgroups, each runs its tiles' k-steps as one continuous
-// stream g = 0 .. G-1 through the ring, so the DMA of the next tile's first stages overlaps the
-// current tile's last steps and its epilogue.
-template <int BMB, int BNB, int S, int EPI>
-__global__ void __launch_bounds__(kGemmThreads)
-    linear_f16x3_kernel(const _Float16 *__restrict__ Ah, const _Float16 *__restrict__ Al, int64_t M, int K,
-                        const _Float16 *__restrict__ Wh, const _Float16 *__restrict__ Wl,
+// BMB x BNB fragment blocks (16 x 16 outputs each) per tile, NW waves (2 x NW/2), S-stage ring.
+template <int BMB, int BNB, int S, int NW, int EPI>
+__global__ void __launch_bounds__(64 * NW)
+    linear_f16x3_kernel(const _Float16 *__restrict__ Ap, int64_t M, int K, const _Float16 *__restrict__ Wp,
                         const float *__restrict__ bias, float out_scale, int N, float *__restrict__ Cout,
-                        float next_scale, _Float16 *__restrict__ Ch, _Float16 *__restrict__ Cl) {
-  constexpr int WMT = BMB / 2, WNT = BNB / 2;         // 16x16 tiles per wave
+                        float next_scale, _Float16 *__restrict__ Cp) {
+  constexpr int WGN = NW / 2;                         // waves: 2 rows x WGN columns
+  constexpr int WMT = BMB / 2, WNT = BNB / WGN;       // 16x16 tiles per wave
   constexpr int NBLK = 2 * (BMB + BNB);               // 1 KiB blocks per stage
-  constexpr int PCS = NBLK / 4;                       // DMA pieces per wave per stage
-  constexpr int STAGE = NBLK * 1024;
-  constexpr int H1 = (WMT + 1) / 2;                   // row tiles before the mid-step barrier
-  static_assert(BMB % 2 == 0 && BNB % 2 == 0 && WNT % 2 == 0 && NBLK % 4 == 0, "tile must split over 2 x 2 waves");
+  constexpr int PCS = (NBLK + NW - 1) / NW;           // DMA pieces per wave per stage (uniform count:
+                                                      // pieces past NBLK re-load block 0 into a pad)
+  constexpr int STAGE = PCS * NW * 1024;
+  constexpr int H1 = WMT / 2;                         // row tiles before the mid-step barrier
+  constexpr int NMF2 = 3 * (WMT - H1) * WNT;          // MFMAs after it
+  constexpr int NRD = 2 * (WMT + WNT);                // fragment reads per step
+  static_assert(BMB % 2 == 0 && BNB % WGN == 0, "tile must split over the waves");
   static_assert(S >= 3, "the ring needs one stage in use, one landing, one in flight");
+  static_assert(H1 >= 1, "a row tile before the barrier");
+  // threaded schedule of the second half: PCS groups of (NMF2 / PCS MFMAs, NRD / PCS reads, 1 DMA piece)
+  constexpr bool THREAD = NMF2 % PCS == 0 && NRD % PCS == 0 && NMF2 / PCS >= NRD / PCS + 1;
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // uniform: piece choice and M0 stay scalar
-  const int wr = wave >> 1, wc = wave & 1;
-  const int64_t mblocks = (M + 15) >> 4;
+  const int wr = wave / WGN, wc = wave % WGN;
   const int kb32 = K >> 5, nk = kb32;
-  const int tiles_m = (int)((mblocks + BMB - 1) / BMB), tiles_n = N / (16 * BNB);
+  const int64_t rstride = (int64_t)kb32 * 2048;       // bytes per row block of a split buffer
+  const int tiles_m = (int)((M + 16 * BMB - 1) / (16 * BMB)), tiles_n = N / (16 * BNB);
   const int n_tiles = tiles_m * tiles_n;
   float *btab = reinterpret_cast<float *>(lds + S * STAGE);                    // bias[N]
 
@@ -222,38 +196,66 @@ __global__ void __launch_bounds__(kGemmThreads)
   const int cn = q8 + (xcd < r8);
   const int my_n = slot < cn ? (cn - slot + sx - 1) / sx : 0;
   if (my_n == 0) return;                              // whole workgroup: no barrier is left waiting
-  const int G = my_n * nk;
-
   // bias of every column into LDS once (no global load may sit between the counted DMA waits)
-  for (int i = tid; i < N; i += kGemmThreads) btab[i] = bias ? bias[i] : 0.f;
+  for (int i = tid; i < N; i += 64 * NW) btab[i] = bias ? bias[i] : 0.f;
   __syncthreads();
 
-  // DMA issuer state: stage `issued` = k-step is_kt of this workgroup's tile is_ti (clamped at G-1)
-  int issued = 0, is_ti = 0, is_kt = 0, is_tm, is_tn;
-  k10_tile(c0, tiles_m, tiles_n, is_tm, is_tn);
-#define K10_ISSUE()                                                                                       \
-  do {                                                                                                    \
-    k10_issue<BMB, BNB, PCS>(lds + (issued % S) * STAGE, Ah, Al, Wh, Wl, mblocks, kb32, is_tm, is_tn, is_kt, \
-                             wave, lane);                                                                 \
-    if (++issued < G && ++is_kt == nk) {                                                                  \
-      is_kt = 0;                                                                                          \
-      ++is_ti;                                                                                            \
-      k10_tile(c0 + is_ti * sx, tiles_m, tiles_n, is_tm, is_tn);                                          \
-    }                                                                                                     \
+  // ---- DMA: piece i of this wave = stage block o = 4 i + wave; its source is a fixed offset
+  //      (block's row within the tile, hi/lo half, lane) from the tile's A or W base + k-step
+  uint32_t voff[PCS];
+#pragma unroll
+  for (int i = 0; i < PCS; ++i) {
+    const int o = NW * i + wave;
+    const int ob = o >= NBLK ? 0 : o < 2 * BMB ? o : o - 2 * BMB;
+    voff[i] = (uint32_t)((ob >> 1) * rstride + (ob & 1) * 1024 + lane * 16);
+  }
+  const unsigned char *is_a, *is_w;                   // issue cursor: tile bases
+  int is_kt = 0, is_ti = 0;
+#define K10_TILE_BASES(ti)                                                                                 \
+  do {                                                                                                     \
+    int tm_, tn_;                                                                                          \
+    k10_tile(c0 + (ti) * sx, tiles_m, tiles_n, tm_, tn_);                                                  \
+    is_a = reinterpret_cast<const unsigned char *>(Ap) + (int64_t)tm_ * BMB * rstride;                     \
+    is_w = reinterpret_cast<const unsigned char *>(Wp) + (int64_t)tn_ * BNB * rstride;                     \
+  } while (0)
+  K10_TILE_BASES(0);
+#define K10_ISSUE(slotidx)                                                                                 \
+  do {                                                                                                     \
+    unsigned char *st_ = lds + (slotidx) * STAGE;                                                          \
+    const int64_t ko_ = (K10_ABL & 4) ? 0 : (int64_t)is_kt * 2048;                                         \
+    _Pragma("unroll") for (int i = 0; i < PCS; ++i) {                                                      \
+      const unsigned char *src_ = (NW * i + wave < 2 * BMB || NW * i + wave >= NBLK ? is_a : is_w) + ko_ + voff[i]; \
+      if (!(K10_ABL & 2))                                                                                  \
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)src_,             \
+                                         (__attribute__((address_space(3))) void *)(st_ + (NW * i + wave) * 1024), \
+                                         16, 0, 0);                                                        \
+    }                                                                                                      \
+  } while (0)
+#define K10_ADVANCE()                                                                                      \
+  do {                                                                                                     \
+    if (++is_kt == nk) {                                                                                   \
+      if (is_ti + 1 < my_n) {                                                                              \
+        is_kt = 0;                                                                                         \
+        ++is_ti;                                                                                           \
+        K10_TILE_BASES(is_ti);                                                                             \
+      } else {                                                                                             \
+        is_kt = nk - 1;                              /* clamped: the last stage repeats past the end */    \
+      }                                                                                                    \
+    }                                                                                                      \
   } while (0)
 
   i32x4 ah0[WMT], al0[WMT], bh0[WNT], bl0[WNT];
   i32x4 ah1[WMT], al1[WMT], bh1[WNT], bl1[WNT];
-#define K10_READ(g, AH, AL, BH, BL)                                                                          \
+#define K10_READ(slotidx, AH, AL, BH, BL)                                                                    \
   do {                                                                                                       \
-    const unsigned char *st_ = lds + ((g) % S) * STAGE + lane * 16;                                          \
+    const unsigned char *st_ = lds + (slotidx) * STAGE + lane * 16;                                          \
     _Pragma("unroll") for (int j = 0; j < WNT; ++j) {                                                        \
-      BH[j] = *reinterpret_cast<const i32x4 *>(st_ + (2 * BMB + wc * WNT + j) * 1024);                       \
-      BL[j] = *reinterpret_cast<const i32x4 *>(st_ + (2 * BMB + BNB + wc * WNT + j) * 1024);                 \
+      BH[j] = *reinterpret_cast<const i32x4 *>(st_ + (2 * BMB + 2 * (wc * WNT + j)) * 1024);                 \
+      BL[j] = *reinterpret_cast<const i32x4 *>(st_ + (2 * BMB + 2 * (wc * WNT + j) + 1) * 1024);             \
     }                                                                                                        \
     _Pragma("unroll") for (int i = 0; i < WMT; ++i) {                                                        \
-      AH[i] = *reinterpret_cast<const i32x4 *>(st_ + (wr * WMT + i) * 1024);                                 \
-      AL[i] = *reinterpret_cast<const i32x4 *>(st_ + (BMB + wr * WMT + i) * 1024);                           \
+      AH[i] = *reinterpret_cast<const i32x4 *>(st_ + (2 * (wr * WMT + i)) * 1024);                           \
+      AL[i] = *reinterpret_cast<const i32x4 *>(st_ + (2 * (wr * WMT + i) + 1) * 1024);                       \
     }                                                                                                        \
   } while (0)
 
@@ -263,34 +265,51 @@ __global__ void __launch_bounds__(kGemmThreads)
 #pragma unroll
     for (int j = 0; j < WNT; ++j) acc[i][j] = g32x4{0.f, 0.f, 0.f, 0.f};
 #define K10_MFMA(I0, I1, AH, AL, BH, BL)                                                       \
-  _Pragma("unroll") for (int i = (I0); i < (I1); ++i) _Pragma("unroll") for (int j = 0; j < WNT; ++j) { \
+  if (!(K10_ABL & 1)) _Pragma("unroll") for (int i = (I0); i < (I1); ++i) _Pragma("unroll") for (int j = 0; j < WNT; ++j) { \
     acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_h8(AL[i]), as_h8(BH[j]), acc[i][j], 0, 0, 0); \
     acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_h8(AH[i]), as_h8(BL[j]), acc[i][j], 0, 0, 0); \
     acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_h8(AH[i]), as_h8(BH[j]), acc[i][j], 0, 0, 0); \
   }
 
-  // ---- the stream: prologue fills the ring, then per step: MFMAs of the first row half, wait
-  //      for the next stage (counted: S - 2 stages may stay in flight), one barrier (publishes
-  //      it, retires every wave's reads of this step's slot), refill that slot with stage g + S,
-  //      read the next step's fragments behind the second half's MFMAs.  After a tile's last
-  //      step its epilogue runs through this wave's private LDS region with 16-byte stores (the
-  //      next wait then also covers those stores: vmcnt counts in issue order).
+  // ---- the stream.  Prologue: stages 0 .. S-1 in flight, wait for stage 0, read its fragments.
+  //      Step g (slot g % S): MFMAs of the first H1 row tiles; wait (counted: stages g+2 ..
+  //      g+S-1 may stay in flight) + barrier: stage g+1 is published, every read of slot g % S
+  //      is retired; then the rest of the MFMAs with the next step's fragment reads (slot
+  //      (g+1) % S) and the DMA of stage g+S into slot g % S threaded between them.  Past the
+  //      end the DMA repeats the last stage and the reads fetch unused data: every step runs
+  //      the same uniform code.
 #pragma unroll
-  for (int p = 0; p < S; ++p) K10_ISSUE();
+  for (int p = 0; p < S; ++p) {
+    K10_ISSUE(p);
+    K10_ADVANCE();
+  }
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PCS * (S - 1)) : "memory");
   __builtin_amdgcn_s_barrier();
   K10_READ(0, ah0, al0, bh0, bl0);
 
-#define K10_STEP(g, AH, AL, BH, BL, NAH, NAL, NBH, NBL)                                        \
-  do {                                                                                         \
-    K10_MFMA(0, H1, AH, AL, BH, BL)                                                            \
-    if ((g) + 1 < G) {                                                                         \
-      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_waitcnt vmcnt(%0)" ::"n"(PCS * (S - 2)) : "memory"); \
-      __builtin_amdgcn_s_barrier();                                                            \
-      K10_ISSUE();                                                                             \
-      K10_READ((g) + 1, NAH, NAL, NBH, NBL);                                                   \
-    }                                                                                          \
-    K10_MFMA(H1, WMT, AH, AL, BH, BL)                                                          \
+#define K10_STEP(g, AH, AL, BH, BL, NAH, NAL, NBH, NBL)                                                      \
+  do {                                                                                                       \
+    const int cs_ = (g) % S, ns_ = ((g) + 1) % S;                                                            \
+    K10_MFMA(0, H1, AH, AL, BH, BL)                                                                          \
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_waitcnt vmcnt(%0)" ::"n"(PCS * (S - 2)) : "memory");             \
+    __builtin_amdgcn_s_barrier();                                                                            \
+    __builtin_amdgcn_sched_barrier(0);                                                                       \
+    K10_READ(ns_, NAH, NAL, NBH, NBL);                                                                       \
+    K10_ISSUE(cs_);                                                                                          \
+    K10_MFMA(H1, WMT, AH, AL, BH, BL)                                                                        \
+    if constexpr (THREAD) {                                                                                  \
+      _Pragma("unroll") for (int q_ = 0; q_ < PCS; ++q_) {                                                   \
+        _Pragma("unroll") for (int r_ = 0; r_ < NRD / PCS; ++r_) {                                           \
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                                                 \
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                                                 \
+        }                                                                                                    \
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                                                   \
+        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);                                                   \
+        __builtin_amdgcn_sched_group_barrier(0x008, NMF2 / PCS - NRD / PCS - 1, 0);                          \
+      }                                                                                                      \
+    }                                                                                                        \
+    __builtin_amdgcn_sched_barrier(0);                                                                       \
+    K10_ADVANCE();                                                                                           \
   } while (0)
 
   for (int ti = 0; ti < my_n; ++ti) {
@@ -301,19 +320,20 @@ __global__ void __launch_bounds__(kGemmThreads)
     }
     int tm, tn;
     k10_tile(c0 + ti * sx, tiles_m, tiles_n, tm, tn);
-    k10_epilogue<BMB, BNB, EPI>(acc, tm, tn, wr, wc, lane, btab, out_scale, next_scale, M, N, mblocks, Cout, Ch,
-                                Cl);
+    if (!(K10_ABL & 8))
+      k10_epilogue<BMB, BNB, NW, EPI>(acc, tm, tn, wr, wc, lane, btab, out_scale, next_scale, M, N, Cout, Cp);
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // clamped tail DMAs landed before the LDS is released
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tail DMAs landed before the LDS is released
+#undef K10_TILE_BASES
 #undef K10_ISSUE
+#undef K10_ADVANCE
 #undef K10_READ
 #undef K10_MFMA
 #undef K10_STEP
 }
 
-// W fp32 [N][K] row-major (or any fp32 matrix) -> fragment-major f16 planes of W * scale
-__global__ void split_rows_kernel(const float *__restrict__ W, int64_t N, int K, float scale, _Float16 *__restrict__ hi,
-                                  _Float16 *__restrict__ lo) {
+// fp32 rows [N][K] (weights or activations) -> split blocks of rows * scale
+__global__ void split_rows_kernel(const float *__restrict__ W, int64_t N, int K, float scale, _Float16 *__restrict__ P) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // one 8-element segment
   const int64_t nseg = N * (K / 8);
   if (t >= nseg) return;
@@ -325,17 +345,17 @@ __global__ void split_rows_kernel(const float *__restrict__ W, int64_t N, int K,
   h16x8 h, l;
   split8(x, scale, h, l);
   const int64_t off = f16x3_plane_off(n, k, K >> 5);
-  *reinterpret_cast<h16x8 *>(hi + off) = h;
-  *reinterpret_cast<h16x8 *>(lo + off) = l;
+  *reinterpret_cast<h16x8 *>(P + off) = h;
+  *reinterpret_cast<h16x8 *>(P + off + 512) = l;
 }
 
 struct TileCfg {
   int bmb, bnb;
 };
 
-// Pick the tile minimising (rounds of one-workgroup-per-CU waves) x (tile area): the 96 x 192
-// tile divides M = 6144 (the 256 x 24 query batch) x N in {768, 2304, 3072} into exact
-// multiples of 256 tiles; 128 x 128, 64 x 128 and 64 x 64 cover the other shapes.
+// Pick the tile minimising (rounds of one-workgroup-per-CU waves) x (tile area + perimeter):
+// the 96 x 192 tile divides M = 6144 (the 256 x 24 query batch) x N in {768, 2304, 3072} into
+// exact multiples of 256 tiles; 128 x 128, 64 x 128 and 64 x 64 cover the other shapes.
 static TileCfg pick_tile(int64_t M, int N, int n_cu) {
   const TileCfg cands[4] = {{6, 12}, {8, 8}, {4, 8}, {4, 4}};
   TileCfg best = {0, 0};
@@ -343,7 +363,6 @@ static TileCfg pick_tile(int64_t M, int N, int n_cu) {
   for (const TileCfg &c : cands) {
     if (N % (16 * c.bnb)) continue;
     const int64_t tiles = ceil_div(M, 16 * c.bmb) * (N / (16 * c.bnb));
-    // a tile's time ~ its MFMAs (area) + its per-step DMA / fragment reads (perimeter)
     const double cost = (double)ceil_div(tiles, n_cu) * (c.bmb * c.bnb + 2 * (c.bmb + c.bnb));
     if (best.bmb == 0 || cost < best_cost) {
       best = c;
@@ -353,26 +372,25 @@ static TileCfg pick_tile(int64_t M, int N, int n_cu) {
   return best;
 }
 
-template <int BMB, int BNB, int S>
-static int launch_tile(const _Float16 *Ah, const _Float16 *Al, int64_t M, int K, const _Float16 *Wh,
-                       const _Float16 *Wl, const float *bias, float out_scale, int N, int epi, float *C,
-                       float next_scale, _Float16 *Ch, _Float16 *Cl, int n_cu, hipStream_t st) {
-  const int64_t tiles = ceil_div(ceil_div(M, 16), BMB) * (N / (16 * BNB));
+template <int BMB, int BNB, int S, int NW>
+static int launch_tile(const _Float16 *A, int64_t M, int K, const _Float16 *W, const float *bias, float out_scale,
+                       int N, int epi, float *C, float next_scale, _Float16 *Cp, int n_cu, hipStream_t st) {
+  const int64_t tiles = ceil_div(M, 16 * BMB) * (N / (16 * BNB));
   if (tiles > INT32_MAX / 2) CM_FAIL(CM_EINVAL, "too many tiles");
-  const int lds_bytes = S * 2 * (BMB + BNB) * 1024 + ((N * 4 + 15) & ~15);
+  const int lds_bytes = S * ((2 * (BMB + BNB) + NW - 1) / NW) * NW * 1024 + ((N * 4 + 15) & ~15);
   if (lds_bytes > 160 * 1024) CM_FAIL(CM_EINVAL, "N too large for the LDS bias table");
-  const dim3 grid((unsigned)std::min<int64_t>(tiles, n_cu)), block(kGemmThreads);
-  static int attr_set[3] = {0, 0, 0};  // > 64 KiB of dynamic LDS: opt in (to the largest size seen)
+  const dim3 grid((unsigned)std::min<int64_t>(tiles, n_cu)), block(64 * NW);
+  static int attr_set[3] = {0, 0, 0};  // > 64 KiB of dynamic LDS: opt in once per kernel
   switch (epi) {
 #define CM_K10_CASE(E)                                                                                             \
   case E:                                                                                                          \
-    if (attr_set[E] < lds_bytes) {                                                                                 \
-      CM_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&linear_f16x3_kernel<BMB, BNB, S, E>),             \
+    if (!attr_set[E]) {                                                                                            \
+      CM_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&linear_f16x3_kernel<BMB, BNB, S, NW, E>),         \
                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));                         \
-      attr_set[E] = 160 * 1024;                                                                                    \
+      attr_set[E] = 1;                                                                                             \
     }                                                                                                              \
-    hipLaunchKernelGGL((linear_f16x3_kernel<BMB, BNB, S, E>), grid, block, lds_bytes, st, Ah, Al, M, K, Wh, Wl,  \
-                       bias, out_scale, N, C, next_scale, Ch, Cl);                                                 \
+    hipLaunchKernelGGL((linear_f16x3_kernel<BMB, BNB, S, NW, E>), grid, block, lds_bytes, st, A, M, K, W, bias,   \
+                       out_scale, N, C, next_scale, Cp);                                                           \
     break;
     CM_K10_CASE(kEpiF32)
     CM_K10_CASE(kEpiF32Gelu)
@@ -390,36 +408,36 @@ static int g_n_cu = 0;
 
 using namespace cm;
 
-extern "C" int cm_f16x3_split_weights(const float *w_dev, int32_t N, int32_t K, float scale, void *hi_dev, void *lo_dev,
-                                      void *stream) {
-  if (N <= 0 || K <= 0) return CM_OK;
-  if (!w_dev || !hi_dev || !lo_dev) CM_FAIL(CM_EINVAL, "NULL argument");
-  if (N % 16 || K % 32) CM_FAIL(CM_EINVAL, "need N % 16 == 0 and K % 32 == 0");
-  return cm_f16x3_split_rows(w_dev, N, K, scale, hi_dev, lo_dev, stream);
-}
+extern "C" int64_t cm_f16x3_plane_rows(int64_t M) { return M <= 0 ? 0 : f16x3_plane_rows(M); }
 
-extern "C" int cm_f16x3_split_rows(const float *x_dev, int64_t M, int32_t K, float scale, void *hi_dev, void *lo_dev,
+extern "C" int cm_f16x3_split_rows(const float *x_dev, int64_t M, int32_t K, float scale, void *planes_dev,
                                    void *stream) {
   if (M <= 0) return CM_OK;
-  if (!x_dev || !hi_dev || !lo_dev) CM_FAIL(CM_EINVAL, "NULL argument");
+  if (!x_dev || !planes_dev) CM_FAIL(CM_EINVAL, "NULL argument");
   if (K <= 0 || K % 32) CM_FAIL(CM_EINVAL, "K must be a positive multiple of 32");
-  if (((uintptr_t)x_dev & 15) || ((uintptr_t)hi_dev & 15) || ((uintptr_t)lo_dev & 15))
-    CM_FAIL(CM_EINVAL, "x and the planes must be 16-byte aligned");
+  if (((uintptr_t)x_dev & 15) || ((uintptr_t)planes_dev & 15)) CM_FAIL(CM_EINVAL, "x and planes must be 16-byte aligned");
   const int64_t nseg = M * (K / 8);
   hipLaunchKernelGGL(split_rows_kernel, dim3((unsigned)ceil_div(nseg, 256)), dim3(256), 0, (hipStream_t)stream, x_dev,
-                     M, K, scale, (_Float16 *)hi_dev, (_Float16 *)lo_dev);
+                     M, K, scale, (_Float16 *)planes_dev);
   CM_HIP(hipGetLastError());
   return CM_OK;
 }
 
-extern "C" int cm_linear_f16x3(const void *ah_dev, const void *al_dev, int64_t M, int32_t K, const void *wh_dev,
-                               const void *wl_dev, const float *bias_dev, float out_scale, int32_t N, int32_t epilogue,
-                               float *c_dev, float next_scale, void *ch_dev, void *cl_dev, void *stream) {
+extern "C" int cm_f16x3_split_weights(const float *w_dev, int32_t N, int32_t K, float scale, void *planes_dev,
+                                      void *stream) {
+  if (N <= 0 || K <= 0) return CM_OK;
+  if (N % 16) CM_FAIL(CM_EINVAL, "need N % 16 == 0");
+  return cm_f16x3_split_rows(w_dev, N, K, scale, planes_dev, stream);
+}
+
+extern "C" int cm_linear_f16x3(const void *a_planes, int64_t M, int32_t K, const void *w_planes, const float *bias_dev,
+                               float out_scale, int32_t N, int32_t epilogue, float *c_dev, float next_scale,
+                               void *c_planes, void *stream) {
   if (M <= 0) return CM_OK;
-  if (!ah_dev || !al_dev || !wh_dev || !wl_dev) CM_FAIL(CM_EINVAL, "NULL argument");
+  if (!a_planes || !w_planes) CM_FAIL(CM_EINVAL, "NULL argument");
   if (K <= 0 || K % 64) CM_FAIL(CM_EINVAL, "K must be a positive multiple of 64");
   if (N <= 0 || N % 64) CM_FAIL(CM_EINVAL, "N must be a positive multiple of 64");
-  if (epilogue == CM_EPI_PLANES_GELU ? (!ch_dev || !cl_dev) : !c_dev) CM_FAIL(CM_EINVAL, "NULL output");
+  if (epilogue == CM_EPI_PLANES_GELU ? !c_planes : !c_dev) CM_FAIL(CM_EINVAL, "NULL output");
   if (epilogue != CM_EPI_BIAS && epilogue != CM_EPI_BIAS_GELU && epilogue != CM_EPI_PLANES_GELU)
     CM_FAIL(CM_EINVAL, "unknown epilogue");
   if (!g_n_cu) {
@@ -429,15 +447,16 @@ extern "C" int cm_linear_f16x3(const void *ah_dev, const void *al_dev, int64_t M
     g_n_cu = n > 0 ? n : 256;
   }
   const TileCfg t = pick_tile(M, N, g_n_cu);
-  const _Float16 *Ah = (const _Float16 *)ah_dev, *Al = (const _Float16 *)al_dev;
-  const _Float16 *Wh = (const _Float16 *)wh_dev, *Wl = (const _Float16 *)wl_dev;
-  _Float16 *Ch = (_Float16 *)ch_dev, *Cl = (_Float16 *)cl_dev;
+  const _Float16 *A = (const _Float16 *)a_planes, *W = (const _Float16 *)w_planes;
+  _Float16 *Cp = (_Float16 *)c_planes;
   hipStream_t st = (hipStream_t)stream;
+  // waves per workgroup: two or three per SIMD, so one wave's MFMAs cover another's waits
   if (t.bmb == 6)
-    return launch_tile<6, 12, 4>(Ah, Al, M, K, Wh, Wl, bias_dev, out_scale, N, epilogue, c_dev, next_scale, Ch, Cl, g_n_cu, st);
+    return launch_tile<6, 12, K10_W6 == 8 ? 3 : 4, K10_W6>(A, M, K, W, bias_dev, out_scale, N, epilogue, c_dev,
+                                                           next_scale, Cp, g_n_cu, st);
   if (t.bmb == 8)
-    return launch_tile<8, 8, 4>(Ah, Al, M, K, Wh, Wl, bias_dev, out_scale, N, epilogue, c_dev, next_scale, Ch, Cl, g_n_cu, st);
+    return launch_tile<8, 8, 4, 8>(A, M, K, W, bias_dev, out_scale, N, epilogue, c_dev, next_scale, Cp, g_n_cu, st);
   if (t.bnb == 8)
-    return launch_tile<4, 8, 4>(Ah, Al, M, K, Wh, Wl, bias_dev, out_scale, N, epilogue, c_dev, next_scale, Ch, Cl, g_n_cu, st);
-  return launch_tile<4, 4, 4>(Ah, Al, M, K, Wh, Wl, bias_dev, out_scale, N, epilogue, c_dev, next_scale, Ch, Cl, g_n_cu, st);
+    return launch_tile<4, 8, 4, 8>(A, M, K, W, bias_dev, out_scale, N, epilogue, c_dev, next_scale, Cp, g_n_cu, st);
+  return launch_tile<4, 4, 4, 8>(A, M, K, W, bias_dev, out_scale, N, epilogue, c_dev, next_scale, Cp, g_n_cu, st);
 }

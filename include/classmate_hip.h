@@ -344,20 +344,22 @@ int cm_short_attention(const void *qkv_dev, int32_t B, int32_t S, int32_t H, int
  * fp32 operand v = hi + lo (two f16 halves, 22 significant bits), product =
  * lo.hi + hi.lo + hi.hi accumulated in fp32 by v_mfma_f32_16x16x32_f16.
  *
- * "Planes": an M x K fp32 matrix as two f16 planes (hi, lo), each
- * ceil(M/16)*16 x K halves in fragment-major order [M/16][K/32][64][8]
- * (lane slot c + 16 g of block (b, kb) = row 16 b + c, k = 32 kb + 8 g..+7).
- * Values are stored times a power-of-two scale with |v * scale| <= 2^15.
+ * "Planes": an M x K fp32 matrix as ONE buffer of 2 KiB split blocks, block
+ * (row / 16, k / 32) = [hi halves 1 KiB][lo halves 1 KiB], each in fragment-
+ * major order (lane slot c + 16 g = row 16 b + c, k = 32 kb + 8 g .. + 7).
+ * A buffer holds cm_f16x3_plane_rows(M) rows (M rounded up to 384, so the
+ * GEMM's last tile reads in bounds) x K x 2 halves.  Values are stored times a
+ * power-of-two scale with |v * scale| <= 2^15.
  *
  * cm_f16x3_split_rows: fp32 rows (device, M x K row-major) * scale -> planes.
  * cm_f16x3_split_weights: the same for an nn.Linear weight (N x K), once per
  *   model; scale puts max|W| at 2^14..2^15.  N % 16 == 0, K % 32 == 0.
  * cm_linear_f16x3: C = (A planes)(W planes)^T * out_scale + bias, where
- *   out_scale = 1 / (A scale * W scale), bias may be NULL; epilogue
- *   CM_EPI_BIAS / CM_EPI_BIAS_GELU (exact erf, torch's F.gelu default) write
- *   c_dev (M x N fp32 row-major); CM_EPI_PLANES_GELU writes GELU(C) *
- *   next_scale as planes (ch_dev/cl_dev, ceil(M/16)*16 x N each) for the next
- *   projection (FFN-up -> FFN-down).  K % 32 == 0, N % 64 == 0, any M.
+ *   out_scale = 1 / (A scale * W scale), bias may be NULL (N <= 4096);
+ *   epilogue CM_EPI_BIAS / CM_EPI_BIAS_GELU (exact erf, torch's F.gelu
+ *   default) write c_dev (M x N fp32 row-major); CM_EPI_PLANES_GELU writes
+ *   GELU(C) * next_scale as planes (c_planes, cm_f16x3_plane_rows(M) x N) for
+ *   the next projection (FFN-up -> FFN-down).  K % 64 == 0, N % 64 == 0, any M.
  * cm_add_layernorm_split: cm_add_layernorm (fp32) that also writes its output
  *   rows * a_scale as planes.  D % 32 == 0.
  * cm_short_attention_split: cm_short_attention (fp32) writing the context
@@ -365,18 +367,17 @@ int cm_short_attention(const void *qkv_dev, int32_t B, int32_t S, int32_t H, int
 #define CM_EPI_BIAS 0
 #define CM_EPI_BIAS_GELU 1
 #define CM_EPI_PLANES_GELU 2
-int cm_f16x3_split_rows(const float *x_dev, int64_t M, int32_t K, float scale, void *hi_dev, void *lo_dev,
-                        void *stream);
-int cm_f16x3_split_weights(const float *w_dev, int32_t N, int32_t K, float scale, void *hi_dev, void *lo_dev,
-                           void *stream);
-int cm_linear_f16x3(const void *ah_dev, const void *al_dev, int64_t M, int32_t K, const void *wh_dev,
-                    const void *wl_dev, const float *bias_dev, float out_scale, int32_t N, int32_t epilogue,
-                    float *c_dev, float next_scale, void *ch_dev, void *cl_dev, void *stream);
+int64_t cm_f16x3_plane_rows(int64_t M);
+int cm_f16x3_split_rows(const float *x_dev, int64_t M, int32_t K, float scale, void *planes_dev, void *stream);
+int cm_f16x3_split_weights(const float *w_dev, int32_t N, int32_t K, float scale, void *planes_dev, void *stream);
+int cm_linear_f16x3(const void *a_planes, int64_t M, int32_t K, const void *w_planes, const float *bias_dev,
+                    float out_scale, int32_t N, int32_t epilogue, float *c_dev, float next_scale, void *c_planes,
+                    void *stream);
 int cm_add_layernorm_split(const float *x_dev, const float *r_dev, int64_t r_rows, const float *gamma_dev,
                            const float *beta_dev, int64_t rows, int32_t D, float eps, float *out_dev, float a_scale,
-                           void *hi_dev, void *lo_dev, void *stream);
+                           void *planes_dev, void *stream);
 int cm_short_attention_split(const float *qkv_dev, int32_t B, int32_t S, int32_t H, int32_t head_dim, float scale,
-                             float a_scale, void *hi_dev, void *lo_dev, void *stream);
+                             float a_scale, void *planes_dev, void *stream);
 
 #ifdef __cplusplus
 }
