@@ -62,10 +62,14 @@ def parse_args():
     ap.add_argument("--q-terms", type=int, default=8)
     ap.add_argument("--q-tokens", type=int, default=24)
     ap.add_argument("--e5-layers", type=int, default=12)
-    ap.add_argument("--e5-dtype", choices=["bfloat16", "float32"], default="bfloat16",
-                    help="E5 forward dtype of the headline step (the drop-in default is float32)")
-    ap.add_argument("--e5-fp32-leg", type=int, default=1,
-                    help="also time the step with the reference-precision fp32 E5 forward (reported as e5_fp32)")
+    ap.add_argument("--e5-dtype", choices=["bfloat16", "float32"], default="float32",
+                    help="E5 forward dtype of the headline step: float32 = the reference's precision (K10 "
+                         "split-precision MFMA GEMMs), the drop-in default")
+    ap.add_argument("--e5-other-leg", type=int, default=1,
+                    help="also time the step with the other E5 precision (reported as e5_bf16 / e5_fp32)")
+    ap.add_argument("--dense-legs", type=int, default=1,
+                    help="hybrid mode: also time the north_star dense configs -- C2' (this 10M shard, B=16, "
+                         "k=10, the >=80%% HBM target) and C2 (a 1M-chunk shard, B=256, k=10)")
     ap.add_argument("--no-e5", action="store_true", help="use perturbed corpus rows as query embeddings")
     ap.add_argument("--no-graph", action="store_true", help="run the E5 query encode eagerly (no hipGraph)")
     ap.add_argument("--serial", action="store_true", help="run BM25 on the main stream (no overlap with E5 + dense)")
@@ -135,7 +139,7 @@ def sample_query_terms(tokens, doc_off, B, q_terms, seed):
 
 # ---------------------------------------------------------------------------
 ABLATION_ENV = ("CM_DENSE_DEBUG", "CM_BM25_DEBUG")
-KNOB_ENV = ("CM_DENSE_PATH", "CM_E5_FUSED_LN", "CM_E5_FUSED_ATTN", "CM_E5_TUNABLEOP", "CM_E5_DTYPE")
+KNOB_ENV = ("CM_DENSE_PATH", "CM_E5_FUSED_LN", "CM_E5_FUSED_ATTN", "CM_E5_TUNABLEOP", "CM_E5_DTYPE", "CM_E5_F16X3")
 
 
 def main():
@@ -191,9 +195,14 @@ def main():
         torch.cuda.empty_cache()
         log(f"bm25 shard: {bm25.num_postings} postings, V={args.vocab} ({time.perf_counter() - t_setup:.1f}s)")
 
-    # queries
+    # queries: every rank holds the same B queries (token ids / term ids); the E5 encode is split
+    # across ranks -- rank r encodes block [q_lo, q_lo + bq) and the (B, D) embeddings are
+    # all-gathered (at N = 1 the block is the whole batch)
+    if B % ws:
+        sys.exit(f"bench.py: --batch {B} must be divisible by the number of GPUs ({ws})")
+    bq, q_lo = B // ws, rank * (B // ws)
+    blk = slice(q_lo, q_lo + bq)
     use_e5 = not args.no_e5 and args.mode == "hybrid"
-    emb = None
     if use_e5:
         from classmate_hip.embeddings import E5MultilingualEmbedder
         g = torch.Generator(device="cuda").manual_seed(args.seed * 13)
@@ -203,30 +212,33 @@ def main():
         mask = torch.ones_like(ids)
 
         def make_e5(dtype):
-            """E5 query encoder of one dtype: dict(emb, graph or None, qbuf = output buffer, and the
-            graph's input buffers, which must stay alive as long as the graph is replayed)."""
+            """E5 query encoder of one dtype for this rank's block: dict(emb, graph or None, qbuf =
+            output buffer, and the graph's input buffers, which must stay alive with the graph)."""
             m = E5MultilingualEmbedder.random_init(seed=0, device=str(dev), num_layers=args.e5_layers, dtype=dtype)
             if args.no_graph:
-                return dict(emb=m, graph=None, qbuf=torch.empty((B, D), dtype=torch.float32, device=dev))
+                return dict(emb=m, graph=None, qbuf=torch.empty((bq, D), dtype=torch.float32, device=dev),
+                            dtype=dtype)
             # one hipGraph replay per batch instead of ~200 launches (fixed-length queries: lean forward)
-            g_ids, g_mask, out_buf, gr = m.capture_graph(B, args.q_tokens, unpadded=True)
-            g_ids.copy_(ids)
-            g_mask.copy_(mask)
-            return dict(emb=m, graph=gr, qbuf=out_buf, ids=g_ids, mask=g_mask)
+            g_ids, g_mask, out_buf, gr = m.capture_graph(bq, args.q_tokens, unpadded=True)
+            g_ids.copy_(ids[blk])
+            g_mask.copy_(mask[blk])
+            return dict(emb=m, graph=gr, qbuf=out_buf, ids=g_ids, mask=g_mask, dtype=dtype)
 
         e5 = make_e5(args.e5_dtype)
     else:
         g = torch.Generator(device="cuda").manual_seed(args.seed * 17)
         qfix = torch.randn(B, D, device=dev, generator=g)
         qfix /= qfix.norm(dim=1, keepdim=True)
+    qfull = torch.empty((B, D), dtype=torch.float32, device=dev) if ws > 1 else None
+    starts = [i * N for i in range(ws + 1)]            # global rows of the shards
 
-    # buffers (allocated once: the step is allocation-free on our side)
+    # buffers (allocated once: the step is allocation-free on our side at N = 1)
     dws = torch.empty(dense.workspace_bytes(B, P), dtype=torch.uint8, device=dev)
     dout = (torch.empty((B, P), dtype=torch.float32, device=dev), torch.empty((B, P), dtype=torch.int64, device=dev))
     vbuf = torch.empty((B * P, D), dtype=torch.float32, device=dev)
-    obuf = torch.empty((B, K), dtype=torch.int32, device=dev)
-    pbuf = (torch.empty((B, K), dtype=torch.int64, device=dev), torch.empty((B, K), dtype=torch.float32, device=dev),
-            torch.empty((B,), dtype=torch.int32, device=dev), torch.empty((B,), dtype=torch.int32, device=dev))
+    obuf = torch.empty((bq, K), dtype=torch.int32, device=dev)
+    pbuf = (torch.empty((bq, K), dtype=torch.int64, device=dev), torch.empty((bq, K), dtype=torch.float32, device=dev),
+            torch.empty((bq,), dtype=torch.int32, device=dev), torch.empty((bq,), dtype=torch.int32, device=dev))
     if bm25 is not None:
         bws = torch.empty(bm25.workspace_bytes(B, q_terms.numel(), K), dtype=torch.uint8, device=dev)
         bout = (torch.empty((B, K), dtype=torch.float64, device=dev), torch.empty((B, K), dtype=torch.int64, device=dev))
@@ -247,79 +259,97 @@ def main():
         # encode and the dense search (joined before fusion)
         with torch.cuda.stream(side):
             if e:
-                e[2].record()
+                e["b0"].record()
             out = bm25.search_dev(q_terms, q_off, K, out=bout, workspace=bws)
             if e:
-                e[3].record()
+                e["b1"].record()
         return out
 
+    def encode(e):
+        """This rank's E5 block -> (B, D) query embeddings on the main stream."""
+        if e:
+            e["e0"].record()
+        if e5["graph"] is not None:
+            e5["graph"].replay()
+            q_local = e5["qbuf"]
+        else:
+            q_local = e5["emb"].encode_token_ids(ids[blk], mask[blk], out=e5["qbuf"])
+        if e:
+            e["e1"].record()
+        if ws == 1:
+            return q_local
+        return parallel.all_gather_into(qfull, q_local)
+
     def step(record=False):
-        e = [torch.cuda.Event(enable_timing=True) for _ in range(4)] if record else None
+        e = {n: torch.cuda.Event(enable_timing=True) for n in ("e0", "e1", "d0", "d1", "b0", "b1")} if record else None
         if bm25 is not None and not args.bm25_after_e5:
             side.wait_stream(main)          # previous step's fusion has read bout
             bs, br = run_bm25(e)
-        if use_e5:
-            if e5["graph"] is not None:
-                e5["graph"].replay()
-                q = e5["qbuf"]
-            else:
-                q = e5["emb"].encode_token_ids(ids, mask, out=e5["qbuf"])
-        else:
-            q = qfix
+        q = encode(e) if use_e5 else qfix
         if bm25 is not None and args.bm25_after_e5:
             side.wait_stream(main)
             bs, br = run_bm25(e)
         if record:
-            e[0].record()
+            e["d0"].record()
         d, r = dense.search_dev(q, P, out=dout, workspace=dws)
         if record:
-            e[1].record()
+            e["d1"].record()
         if args.mode == "dense":
             if record:
                 ev.append(e)
             return r
-        if ws > 1:
-            rg = torch.where(r >= 0, r + row0, r)
-            d, rg = parallel.merge_dense_topk(d, rg, P)
-            rloc = torch.where((rg >= row0) & (rg < row0 + N), rg - row0, torch.full_like(rg, -1))
-            vecs = dense.gather_dev(rloc.reshape(-1), out=vbuf).view(B, P, D)
-            vecs = parallel.assemble_pool_vectors(rg, vecs, row0, N)
-        else:
-            rg = r
+        if ws == 1:
             vecs = dense.gather_dev(r.reshape(-1), out=vbuf).view(B, P, D)
-        order = engine.mmr_dev(q, vecs, K, 0.5, out=obuf)
-        main.wait_stream(side)
+            order = engine.mmr_dev(q, vecs, K, 0.5, out=obuf)     # overlaps the BM25 tail
+            main.wait_stream(side)
+            rg, dm, brg, bsm = r, d, br, bs
+        else:
+            # ONE packed all-gather of both shard lists (merged identically everywhere), then this
+            # rank fuses its query block: its pool rows arrive from their owners in one all-to-all
+            main.wait_stream(side)
+            rgl = torch.where(r >= 0, r + row0, r)
+            brl = torch.where(br >= 0, br + row0, br)
+            dm, rg, bsm, brg = parallel.exchange_topk(d, rgl, bs, brl)
+            vecs = parallel.fetch_pool_vectors(rg, q_lo, bq, lambda lr: dense.gather_dev(lr), starts, D)
+            order = engine.mmr_dev(q[blk].contiguous(), vecs, K, 0.5, out=obuf)
         if record:
             ev.append(e)
-        if ws > 1:
-            brg = torch.where(br >= 0, br + row0, br)
-            bs, brg = parallel.merge_bm25_topk(bs, brg, K)
-        else:
-            brg = br
         # MMR-ordered vector list + list counts in one device pass, then the fused merge
-        vk, vd, vn, bn = engine.rrf_pool_prep_dev(rg.contiguous(), d.contiguous(), order, brg.contiguous(), out=pbuf)
-        return engine.rrf_merge_dev(vk, vd, vn, brg.contiguous(), bs.contiguous(), bn,
-                                    w_vec=1.0, w_bm25=1.0, rrf_k=60, top_k=K)
+        vk, vd, vn, bn = engine.rrf_pool_prep_dev(rg[blk].contiguous(), dm[blk].contiguous(), order,
+                                                  brg[blk].contiguous(), out=pbuf)
+        res = engine.rrf_merge_dev(vk, vd, vn, brg[blk].contiguous(), bsm[blk].contiguous(), bn,
+                                   w_vec=1.0, w_bm25=1.0, rrf_k=60, top_k=K)
+        if ws > 1:   # the fused top-k of every block, on every rank
+            keys = torch.empty((B, K), dtype=res[0].dtype, device=dev)
+            res = (parallel.all_gather_into(keys, res[0]),) + tuple(res[1:])
+        return res
 
-    for _ in range(args.warmup):
-        res = step()
-    torch.cuda.synchronize()
+    def timed(steps):
+        """W untimed + `steps` timed steps between barriers; max over ranks."""
+        for _ in range(args.warmup):
+            step()
+        torch.cuda.synchronize()
+        if ws > 1:
+            torch.distributed.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        out = None
+        for _ in range(steps):
+            out = step(record=True)
+        torch.cuda.synchronize()
+        if ws > 1:
+            torch.distributed.barrier()
+        return parallel.max_over_ranks(time.perf_counter() - t0, device=dev), out
+
     dense.timing(True)
     if bm25 is not None:
         bm25.timing(True)
-    if ws > 1:
-        torch.distributed.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        res = step(record=True)
-    torch.cuda.synchronize()
-    if ws > 1:
-        torch.distributed.barrier()
-    elapsed = time.perf_counter() - t0
-    elapsed = parallel.max_over_ranks(elapsed, device=dev)
-    search_ms = sum(e[0].elapsed_time(e[1]) for e in ev) / len(ev)
-    bsearch_ms = sum(e[2].elapsed_time(e[3]) for e in ev) / len(ev) if args.mode == "hybrid" else None
+    elapsed, res = timed(args.steps)
+    mean_ms = lambda a, b: sum(x[a].elapsed_time(x[b]) for x in ev) / len(ev)   # noqa: E731
+    search_ms = mean_ms("d0", "d1")
+    bsearch_ms = mean_ms("b0", "b1") if bm25 is not None else None
+    e5_ms = mean_ms("e0", "e1") if use_e5 else None
+    ev.clear()
     # scan-kernel launch times: HIP events the library records on the launch stream
     kt = dense.timing_drain()
     dense_ms = sum(kt) / len(kt)
@@ -327,55 +357,55 @@ def main():
     if bm25 is not None:
         bt = bm25.timing_drain()
         bm25_ms = sum(bt) / len(bt)
+    dense.timing(False)
+    if bm25 is not None:
+        bm25.timing(False)
     kind = dense.search_kind(B, P)
     fallbacks = dense.workspace_fallbacks(B, P, dws)
     rescored = bm25.workspace_rescored(B, q_terms.numel(), K, bws) if bm25 is not None else None
     qps = B * args.steps / elapsed
-    e5_fp32 = None
-    if use_e5 and args.e5_fp32_leg and args.e5_dtype != "float32":
-        # the same step with the reference-precision fp32 E5 forward (rag/embeddings/__init__.py:87-94)
-        dense.timing(False)
-        if bm25 is not None:
-            bm25.timing(False)
-        main_e5 = e5
-        e5 = make_e5("float32")
-        for _ in range(args.warmup):
-            step()
-        torch.cuda.synchronize()
-        if ws > 1:
-            torch.distributed.barrier()
-        t1 = time.perf_counter()
-        for _ in range(args.steps):
-            step()
-        torch.cuda.synchronize()
-        if ws > 1:
-            torch.distributed.barrier()
-        el32 = parallel.max_over_ranks(time.perf_counter() - t1, device=dev)
-        e5_fp32 = {"value": B * args.steps / el32, "unit": "queries/s", "ms_per_step": el32 / args.steps * 1e3,
-                   "e5_forward": "float32"}
-        log(f"fp32 E5 leg: {e5_fp32['value']:.1f} q/s ({e5_fp32['ms_per_step']:.3f} ms/step)")
-        del e5
-        e5 = main_e5
-    log(f"{args.steps} steps in {elapsed:.3f}s -> {qps:.1f} q/s; dense search {search_ms:.3f} ms "
-        f"(scan kernel {dense_ms:.3f} ms, {DENSE_KINDS[kind]}, {fallbacks} exact re-runs)"
+    log(f"{args.steps} steps in {elapsed:.3f}s -> {qps:.1f} q/s; E5 ({args.e5_dtype}, {bq} queries/rank) "
+        f"{e5_ms if e5_ms is not None else 0:.3f} ms; dense search {search_ms:.3f} ms (scan kernel {dense_ms:.3f} ms, "
+        f"{DENSE_KINDS[kind]}, {fallbacks} exact re-runs)"
         + (f", bm25 search {bsearch_ms:.3f} ms (K2a tail pass {bm25_ms:.3f} ms, {rescored} (query, range) pairs "
            f"re-scored)" if bm25_ms is not None else ""))
 
     roofs = {"dense": _dense_roofline(kind, N, D, B, dense_ms, _pmc_traffic(args, "dense"))}
     if bm25 is not None:
-        roofs["bm25"] = _bm25_roofline(bm25, q_terms, N, bm25_ms, _pmc_traffic(args, "bm25"))
+        roofs["bm25"] = _bm25_roofline(bm25, q_terms, N, bm25_ms, _pmc_traffic(args, "bm25"), args.q_terms)
     dominant = max(roofs, key=lambda n: roofs[n]["avg_launch_ms"])
     roof = roofs[dominant]
+    if use_e5:   # the whole encode (48 K10 GEMMs + attention + LayerNorms) against the MFMA peak
+        roofs["e5"] = _e5_roofline(bq, args.q_tokens, args.e5_layers, e5_ms, args.e5_dtype)
+
+    # side legs (not the headline): the other E5 precision, and the north_star dense configs
+    legs = {}
+    if use_e5 and args.e5_other_leg:
+        other = "bfloat16" if args.e5_dtype == "float32" else "float32"
+        main_e5, e5 = e5, make_e5(other)
+        el2, _ = timed(args.steps)
+        ev.clear()
+        legs["e5_" + {"bfloat16": "bf16", "float32": "fp32"}[other]] = {
+            "value": B * args.steps / el2, "unit": "queries/s", "ms_per_step": el2 / args.steps * 1e3,
+            "e5_forward": other, "note": "same step with the other E5 forward precision (not the headline)"}
+        log(f"{other} E5 leg: {B * args.steps / el2:.1f} q/s ({el2 / args.steps * 1e3:.3f} ms/step)")
+        del e5
+        e5 = main_e5
+    if args.mode == "hybrid" and args.dense_legs:
+        legs.update(dense_legs(args, dense, N, D, dev, ws))
 
     out = {
         "metric": METRIC if args.mode == "hybrid" else f"dense cosine top-{K} queries/sec, {N}x{D} fp32",
         "value": qps, "unit": "queries/s", "n_gpus": ws, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
-        "vs_baseline": None, "dtype": "f16+f64",
+        "vs_baseline": None,
+        "dtype": ("fp32-accurate E5 (K10 f16x3 MFMA) + f16/f64 dense + f64 BM25" if use_e5 and
+                  args.e5_dtype == "float32" else "f16+f64"),
         "dtypes": {"dense_knn": {1: "f32 (MFMA)", 3: "f16 coarse (MFMA) + fp64 exact re-rank of the certified band",
                                  4: "f16 coarse (MFMA) + fp64 exact re-rank of the certified band"}[kind],
-                   "bm25": "f64", "e5_forward": args.e5_dtype if use_e5 else None, "fusion": "f64"},
-        "e5_fp32": e5_fp32,
+                   "bm25": "f64", "fusion": "f64",
+                   "e5_forward": ({"float32": "fp32 (K10: split-precision f16 hi/lo MFMA, fp32 accumulate)",
+                                   "bfloat16": "bf16"}[args.e5_dtype] if use_e5 else None)},
         "data": "synthetic (seeded): unit-norm Gaussian chunk embeddings, Zipf BM25 postings, random-init "
                 "E5-base weights (no checkpoint offline)",
         "config": {"workload": ("hybrid retrieve: E5 query encode + cosine top-24 + MMR-10 + BM25 top-10 + RRF "
@@ -383,17 +413,20 @@ def main():
                    "chunks_per_gpu": N, "chunks_total": N * ws, "dim": D, "global_batch": B, "k": K, "pool": P,
                    "bm25_vocab": args.vocab, "zipf_s": args.zipf, "chunk_len_mean": args.avg_len,
                    "query_terms": args.q_terms, "e5_query_tokens": args.q_tokens if use_e5 else None,
+                   "e5_queries_per_rank": bq if use_e5 else None,
                    "parallelism": f"corpus-shard x{ws}"},
-        "breakdown_ms": {"dense_search": search_ms, "dense_scan_kernel": dense_ms, "bm25_search": bsearch_ms,
-                         "bm25_tail_kernel": bm25_ms},
+        "breakdown_ms": {"e5_encode": e5_ms, "dense_search": search_ms, "dense_scan_kernel": dense_ms,
+                         "bm25_search": bsearch_ms, "bm25_tail_kernel": bm25_ms},
         "dense_exact_reruns": fallbacks,
         "bm25_rescored_pairs": rescored,
         "roofline": roof,
         "rooflines": roofs,
+        **legs,
         "env": {e: os.environ[e] for e in KNOB_ENV if e in os.environ},
     }
-    if rank == 0 and ws == 1 and args.cpu_baseline and args.mode == "hybrid":
-        cpu, recall = cpu_baseline_and_recall(args, dense, bm25, res, q_terms, e5["qbuf"] if use_e5 else qfix)
+    if args.cpu_baseline and args.mode == "hybrid":
+        q_emb = ((qfull if ws > 1 else e5["qbuf"]) if use_e5 else qfix)   # the last step's embeddings
+        cpu, recall = cpu_baseline_and_recall(args, dense, bm25, res, q_terms, q_emb, rank, ws, row0, N)
         out["cpu_baseline"] = cpu
         out["recall_at_10"] = recall
     else:
@@ -437,7 +470,7 @@ def _dense_roofline(kind, N, D, B, ms, traffic):
     return r
 
 
-def _bm25_roofline(bm25, q_terms, N, ms, traffic):
+def _bm25_roofline(bm25, q_terms, N, ms, traffic, terms_per_query):
     """K2a (the pruned search's tail pass, its largest kernel) per launch, algorithmic bytes:
     every walked posting read once (4 B doc + 2 B tf) and, per posting, the candidate's doc
     length (4 B) and one tf byte per head term of its query.  Walked terms = non-head terms, or
@@ -448,7 +481,7 @@ def _bm25_roofline(bm25, q_terms, N, ms, traffic):
     df, _ = bm25.term_stats()
     nh = bm25.num_head_terms                       # the tiles: the nh highest-df terms
     head_df = np.sort(df)[::-1][nh - 1] if nh > 0 else np.iinfo(np.int64).max
-    qt = q_terms.view(-1, 8).cpu().numpy() if q_terms.numel() % 8 == 0 else q_terms.view(1, -1).cpu().numpy()
+    qt = q_terms.view(-1, terms_per_query).cpu().numpy()
     bytes_ = 0.0
     for row in qt:
         row = row[(row >= 0) & (row < df.shape[0])]
@@ -463,6 +496,75 @@ def _bm25_roofline(bm25, q_terms, N, ms, traffic):
     return r
 
 
+def _e5_roofline(bq, S, layers, ms, dtype):
+    """The E5 query encode of one rank's block against the MFMA peak of the dtype it issues.
+    Algorithmic (fp32-equivalent) flops per sequence: 12 x (24 S d^2 + 4 S^2 d).
+    fp32 runs on K10: every product is three f16 MFMAs, so the issued f16 flops are 3x; bf16 issues
+    the algorithmic flops once.  The encode is many kernels (48 GEMMs, attention, LayerNorms), timed
+    as a whole with HIP events around the graph replay."""
+    d = 768
+    alg = float(bq) * layers * (24.0 * S * d * d + 4.0 * S * S * d)
+    issued = 3.0 * alg if dtype == "float32" else alg
+    tf = issued / (ms * 1e-3) / 1e12
+    return {"bound": "mfma", "achieved": tf, "peak": PEAK_F16_MFMA_TFLOPS, "unit": "TFLOP/s",
+            "frac": tf / PEAK_F16_MFMA_TFLOPS, "traffic": None, "avg_launch_ms": ms,
+            "kernel": ("E5 encode (K10 split-precision f16 MFMA GEMMs x48 + f16x3 MFMA attention + K8 LayerNorm)"
+                       if dtype == "float32" else "E5 encode (bf16, hipBLASLt GEMMs + K9 + K8)"),
+            "algorithmic_per_launch": {"flops_fp32_equiv": alg, "flops_issued": issued, "queries": bq,
+                                       "tokens": S, "layers": layers},
+            "fp32_equiv_tflops": alg / (ms * 1e-3) / 1e12,
+            "vs_fp32_mfma_peak": alg / (ms * 1e-3) / 1e12 / PEAK_F32_MFMA_TFLOPS}
+
+
+def dense_legs(args, dense, N, D, dev, ws):
+    """north_star's dense configurations, timed in the same run (side fields, not the headline):
+    C2' = this rank's 10M shard at B = 16, k = 10 (the HBM-bound case the >= 80 % target names);
+    C2 = a 1M-chunk shard (its own index), B = 256, k = 10.  Queries: unit Gaussian."""
+    import torch
+    from classmate_hip import engine, parallel
+    legs = {}
+
+    def leg(index, n, b, name):
+        g = torch.Generator(device="cuda").manual_seed(args.seed * 31 + b)
+        q = torch.randn(b, D, device=dev, generator=g)
+        q /= q.norm(dim=1, keepdim=True)
+        ws_buf = torch.empty(index.workspace_bytes(b, args.k), dtype=torch.uint8, device=dev)
+        o = (torch.empty((b, args.k), dtype=torch.float32, device=dev),
+             torch.empty((b, args.k), dtype=torch.int64, device=dev))
+        for _ in range(args.warmup):
+            index.search_dev(q, args.k, out=o, workspace=ws_buf)
+        torch.cuda.synchronize()
+        index.timing(True)
+        if ws > 1:
+            torch.distributed.barrier()
+        t0 = time.perf_counter()
+        steps = max(args.steps, 10)
+        for _ in range(steps):
+            index.search_dev(q, args.k, out=o, workspace=ws_buf)
+        torch.cuda.synchronize()
+        if ws > 1:
+            torch.distributed.barrier()
+        el = parallel.max_over_ranks(time.perf_counter() - t0, device=dev)
+        kt = index.timing_drain()
+        index.timing(False)
+        kind = index.search_kind(b, args.k)
+        r = _dense_roofline(kind, n, D, b, sum(kt) / len(kt), None)
+        legs[name] = {"value": b * steps * ws / el, "unit": "queries/s", "ms_per_step": el / steps * 1e3,
+                      "config": {"chunks_per_gpu": n, "batch": b, "k": args.k, "dim": D},
+                      "roofline": r}
+        log(f"{name}: {b * steps * ws / el:.0f} q/s, scan {r['avg_launch_ms']:.3f} ms = {r['frac']:.3f} of {r['bound']}")
+
+    leg(dense, N, 16, "c2p_dense_10m_b16")
+    n1 = min(1_000_000, N)
+    d1 = engine.DenseIndex(D, device=dev.index, capacity=n1)
+    gen_dense(d1, n1, D, seed=args.seed * 1000 + 77)
+    leg(d1, n1, 256, "c2_dense_1m_b256")
+    d1.close()
+    del d1
+    torch.cuda.empty_cache()
+    return legs
+
+
 def _pmc_traffic(args, which):
     """HBM bytes per launch (FETCH_SIZE x 2, the gfx950 correction) from a committed rocprofv3
     --pmc summary of this config (profiles/pmc_traffic.json), or None."""
@@ -475,11 +577,15 @@ def _pmc_traffic(args, which):
 
 
 # ---------------------------------------------------------------------------
-def cpu_baseline_and_recall(args, dense, bm25, res, q_terms, q_dev):
-    """Time the CPU oracle on a bounded sample of the same queries (the step's query embeddings)
-    over the same shard; recall@10."""
+def cpu_baseline_and_recall(args, dense, bm25, res, q_terms, q_dev, rank, ws, row0, N):
+    """Time the CPU oracle on a bounded sample of the step's queries (its query embeddings) over
+    every rank's shard (each rank scans its own, in parallel), merge the per-shard exact lists
+    (a merge of exact per-shard top lists is the exact global list), run MMR + RRF on the merged
+    pools, and compare with the GPU's final top-10: recall@10 at any N.  cpu_baseline.value is
+    the rate of ONE host doing all shards' scans and the fusion (sum of the shard times)."""
     import numpy as np
     import torch
+    from classmate_hip import parallel
     from oracle import corc
     from oracle import ref_semantics as orc
 
@@ -488,10 +594,10 @@ def cpu_baseline_and_recall(args, dense, bm25, res, q_terms, q_dev):
     qh = q_dev[:Qc].float().cpu().numpy()
     qt = q_terms.view(args.batch, -1)[:Qc].cpu().numpy()
     gpu_keys = res[0][:Qc].cpu().numpy()
+    threads = max(corc.num_threads(), torch.get_num_threads())
+    # BM25 statistics: global (build-time, not timed)
     t = time.perf_counter()
-    C = dense.export()                                  # host copy of the shard (not timed)
     csr = bm25.export()
-    log(f"cpu baseline: exported shard to host ({time.perf_counter() - t:.1f}s)")
     term_off = csr["term_off"]
     df = np.diff(term_off)
     first = np.full(df.shape[0], np.uint64(0xFFFFFFFFFFFFFFFF))
@@ -501,49 +607,87 @@ def cpu_baseline_and_recall(args, dense, bm25, res, q_terms, q_dev):
     ccsr = dict(term_off=term_off, post_doc=csr["post_doc"], post_tf=csr["post_tf"], dl=csr["dl"],
                 vocab=int(df.shape[0]), ndocs=int(csr["dl"].shape[0]))
     n_docs = ccsr["ndocs"]
-    avgdl = float(csr["dl"].astype(np.int64).sum()) / n_docs
-    idf, _ = corc.bm25_idf(df, first, n_docs)          # statistics: build-time, not timed
+    sum_len = int(csr["dl"].astype(np.int64).sum())
+    if ws == 1:
+        idf, _ = corc.bm25_idf(df, first, n_docs)
+        gn, gsum = n_docs, sum_len
+    else:
+        gdf, gfk, gn, gsum = parallel.allreduce_bm25_stats(df, first, row0, n_docs, sum_len)
+        idf, _ = parallel.bm25_idf_table(gdf, gfk, gn)
+    avgdl = float(gsum) / gn
+    log(f"cpu baseline: shard CSR exported, global statistics ({time.perf_counter() - t:.1f}s)")
 
-    threads = max(corc.num_threads(), torch.get_num_threads())
-    t0 = time.perf_counter()
-    # dense: fp32 BLAS scan for candidates, exact fp64 re-rank (oracle semantics: 1 - cos, ties -> lower row)
-    sims = C @ qh.T                                    # (N, Qc)
-    cand = np.argpartition(-sims, 4 * P, axis=0)[: 4 * P].T
-    dense_rows, dense_dist = [], []
-    for i in range(Qc):
-        c = np.sort(cand[i])
-        cv = C[c].astype(np.float64)
-        d = 1.0 - (cv @ qh[i].astype(np.float64)) / np.linalg.norm(cv, axis=1) / np.linalg.norm(qh[i])
-        o = np.lexsort((c, d))[:P]
-        dense_rows.append(c[o])
-        dense_dist.append(d[o])
-    t_dense = time.perf_counter() - t0
+    # dense: exact fp64 top-P over this shard, chunk by chunk (fp32 BLAS scan for candidates, fp64
+    # re-rank of 4P per chunk; export of each chunk not timed)
+    t_dense = 0.0
+    best_d = np.full((Qc, 0), np.inf)
+    best_r = np.zeros((Qc, 0), np.int64)
+    best_v = np.zeros((Qc, 0, qh.shape[1]), np.float32)
+    qn = np.linalg.norm(qh.astype(np.float64), axis=1)
+    chunk = 1 << 20
+    for c0 in range(0, N, chunk):
+        C = dense.export(c0, min(chunk, N - c0))
+        t0 = time.perf_counter()
+        sims = C @ qh.T                                        # (n, Qc)
+        m = min(4 * P, C.shape[0])
+        cand = np.argpartition(-sims, m - 1, axis=0)[:m].T     # (Qc, m)
+        cv = C[cand].astype(np.float64)                        # (Qc, m, D)
+        dd = 1.0 - np.einsum("qmd,qd->qm", cv, qh.astype(np.float64)) / np.linalg.norm(cv, axis=2) / qn[:, None]
+        best_d = np.concatenate([best_d, dd], 1)
+        best_r = np.concatenate([best_r, cand + c0 + row0], 1)
+        best_v = np.concatenate([best_v, C[cand]], 1)
+        o = np.lexsort((best_r, best_d), axis=1)[:, :P]
+        best_d = np.take_along_axis(best_d, o, 1)
+        best_r = np.take_along_axis(best_r, o, 1)
+        best_v = np.take_along_axis(best_v, o[:, :, None], 1)
+        t_dense += time.perf_counter() - t0
+        del C, sims
     t1 = time.perf_counter()
     bs, br = corc.bm25_topk(ccsr, idf, avgdl, [list(x) for x in qt], K)
     t_bm25 = time.perf_counter() - t1
+    br = np.where(br >= 0, br + row0, br)
+    shard = dict(rank=rank, d=best_d, r=best_r, v=best_v, bs=bs, br=br, t_dense=t_dense, t_bm25=t_bm25)
+    if ws > 1:
+        allv = [None] * ws
+        torch.distributed.all_gather_object(allv, shard)
+    else:
+        allv = [shard]
+    # merge (exact per-shard lists -> exact global lists), then MMR + RRF (oracle semantics)
+    D_ = np.concatenate([x["d"] for x in allv], 1)
+    R_ = np.concatenate([x["r"] for x in allv], 1)
+    V_ = np.concatenate([x["v"] for x in allv], 1)
+    o = np.lexsort((R_, D_), axis=1)[:, :P]
+    dense_dist, dense_rows = np.take_along_axis(D_, o, 1), np.take_along_axis(R_, o, 1)
+    pool_v = np.take_along_axis(V_, o[:, :, None], 1)
+    BS = np.concatenate([x["bs"] for x in allv], 1)
+    BR = np.concatenate([x["br"] for x in allv], 1)
     t2 = time.perf_counter()
     cpu_keys = []
     for i in range(Qc):
-        pool = C[dense_rows[i]]
-        order = orc.mmr_order(qh[i], pool, list(range(P)), K, 0.5)
+        valid = BR[i] >= 0
+        cand = sorted(zip(-BS[i][valid], BR[i][valid]))[:K]          # score desc, row asc
+        bm_ids = [int(r_) for _, r_ in cand]
+        order = orc.mmr_order(qh[i], pool_v[i], list(range(P)), K, 0.5)
         vec_ids = [int(dense_rows[i][j]) for j in order]
-        bm_ids = [int(x) for x in br[i] if x >= 0]
         fused = orc.rrf_fuse(rank_lists=[vec_ids, bm_ids], weights=[1.0, 1.0], rrf_k=60)
         vdist = {int(dense_rows[i][j]): float(np.float32(dense_dist[i][j])) for j in order}
         items = list(dict.fromkeys(vec_ids + bm_ids))
         items.sort(key=lambda x: (fused[x], -vdist.get(x, 0.0)), reverse=True)
         cpu_keys.append(items[:K])
     t_fuse = time.perf_counter() - t2
-    total = time.perf_counter() - t0
     recall = float(np.mean([len(set(cpu_keys[i]) & set(int(x) for x in gpu_keys[i] if x >= 0)) / K
                             for i in range(Qc)]))
-    full_n = args.docs_per_gpu
+    shard_s = [x["t_dense"] + x["t_bm25"] for x in allv]
+    total = sum(shard_s) + t_fuse
     cpu = dict(value=Qc / total, unit="queries/s", cores=int(threads), kind="port",
-               sample=f"{Qc} of the {args.batch} queries of one step over the full {full_n}-chunk shard "
-                      f"(dense: numpy fp32 BLAS scan + fp64 re-rank; BM25: oracle/cm_oracle.c OpenMP; "
-                      f"MMR/RRF: oracle/ref_semantics.py; E5 encode excluded)",
-               seconds=total, breakdown_s=dict(dense=t_dense, bm25=t_bm25, mmr_rrf=t_fuse))
-    log(f"cpu baseline {cpu['value']:.2f} q/s on {threads} threads; recall@10 {recall:.4f}")
+               sample=f"{Qc} of the {args.batch} queries of one step over all {ws} x {N}-chunk shards (dense: numpy "
+                      f"fp32 BLAS scan + fp64 re-rank per 1M-row chunk; BM25: oracle/cm_oracle.c OpenMP with the "
+                      f"global statistics; MMR/RRF: oracle/ref_semantics.py; E5 encode excluded); value = one host "
+                      f"doing every shard's scan in turn",
+               seconds=total, per_shard_s=shard_s,
+               breakdown_s=dict(dense=sum(x["t_dense"] for x in allv), bm25=sum(x["t_bm25"] for x in allv),
+                                mmr_rrf=t_fuse))
+    log(f"cpu baseline {cpu['value']:.2f} q/s ({threads} threads per shard, {ws} shards); recall@10 {recall:.4f}")
     return cpu, recall
 
 

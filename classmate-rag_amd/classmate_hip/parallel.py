@@ -8,10 +8,16 @@ global rows [row0_r, row0_r + n_r).  Exchanges, and only these:
   all-reduce MIN of each term's first (global row, position) key, so every rank
   computes the same idf table (including rank_bm25's epsilon floor, averaged in
   the reference's first-occurrence order) and avgdl;
-* per query batch — all-gather of each shard's top-k (dense: distance + global
-  row; BM25: score + global row), then a deterministic merge identical on all
-  ranks; the MMR pool's embeddings are assembled with one all-reduce SUM (each
-  rank contributes the rows it owns, zeros elsewhere);
+* per query batch (``exchange_topk`` + ``fetch_pool_vectors``, the batched path):
+  the B queries are encoded split across ranks (B / G each) and all-gathered;
+  every shard's dense top-P (distance, global row) and BM25 top-k (score,
+  global row) travel in ONE packed all-gather and are merged deterministically
+  on every rank; rank r then fuses query block r only, so the MMR pool vectors
+  move as one all-to-all in which each owner sends exactly the merged pool rows
+  it holds to the rank fusing that query (about B.P.D.4 / G bytes per rank,
+  instead of an all-reduce of the whole B x P x D pool); a final all-gather
+  assembles the fused top-k.  ``merge_dense_topk`` / ``merge_bm25_topk`` /
+  ``assemble_pool_vectors`` remain for the host-API paths;
 * per filtered BM25 batch (quirk Q2: rank_bm25's statistics over the filtered
   candidates, rag/retrieval/bm25.py:184-191) — one all-reduce SUM of the
   candidate count, their total length and the candidate df of the query terms,
@@ -216,6 +222,105 @@ def assemble_pool_vectors(rows_t, local_vecs, row0: int, n_local: int, group=Non
     if ws > 1:
         dist.all_reduce(out, op=dist.ReduceOp.SUM, group=group)
     return out
+
+
+def _host_staged(group=None) -> bool:
+    """gloo (the CPU tests, and the one-GPU rehearsal of the N > 1 path) moves host tensors only;
+    RCCL ("nccl") moves device tensors in place over xGMI."""
+    return dist.get_backend(group) != "nccl"
+
+
+def all_gather_into(out, t, group=None):
+    """out (ws * n, ...) <- every rank's t (n, ...), rank order."""
+    if _host_staged(group) and t.is_cuda:
+        parts = [torch.empty_like(t, device="cpu") for _ in range(world()[1])]
+        dist.all_gather(parts, t.cpu(), group=group)
+        out.copy_(torch.cat(parts, 0))
+    else:
+        dist.all_gather_into_tensor(out, t.contiguous(), group=group)
+    return out
+
+
+def all_to_all(recv, send, recv_splits, send_splits, group=None):
+    """Variable-size all-to-all of rows (splits: row counts per rank)."""
+    if _host_staged(group) and send.is_cuda:
+        r = torch.empty_like(recv, device="cpu")
+        dist.all_to_all_single(r, send.cpu(), output_split_sizes=recv_splits, input_split_sizes=send_splits,
+                               group=group)
+        recv.copy_(r)
+    else:
+        dist.all_to_all_single(recv, send.contiguous(), output_split_sizes=recv_splits,
+                               input_split_sizes=send_splits, group=group)
+    return recv
+
+
+def _all_gather_cat(t, group=None):
+    """(ws, *t.shape) stack of every rank's t (same shape on all ranks)."""
+    _, ws = world()
+    out = torch.empty((ws * t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+    return all_gather_into(out, t.contiguous(), group).view((ws,) + tuple(t.shape))
+
+
+def exchange_topk(d, r, bs, br, group=None):
+    """Every shard's dense (B, P) (distance f32, global row) and BM25 (B, K) (score f64, global row)
+    top lists -> the global ones, identical on every rank, through ONE all-gather of a packed int64
+    tensor.  Merge order as merge_dense_topk (distance asc, row asc) and merge_bm25_topk (score
+    desc, row asc; -1 pads last)."""
+    _, ws = world()
+    if ws == 1:
+        return d, r, bs, br
+    B, P = d.shape
+    K = bs.shape[1]
+    pack = torch.cat([d.contiguous().view(torch.int32).to(torch.int64), r.to(torch.int64),
+                      bs.contiguous().view(torch.int64), br.to(torch.int64)], 1)
+    allp = _all_gather_cat(pack, group)                                    # (ws, B, 2P + 2K)
+    D = allp[:, :, :P].to(torch.int32).view(torch.float32).permute(1, 0, 2).reshape(B, ws * P)
+    R = allp[:, :, P:2 * P].permute(1, 0, 2).reshape(B, ws * P)
+    S = allp[:, :, 2 * P:2 * P + K].contiguous().view(torch.float64).permute(1, 0, 2).reshape(B, ws * K)
+    BR = allp[:, :, 2 * P + K:].permute(1, 0, 2).reshape(B, ws * K)
+    _, idx = torch.sort(f32_order_key(D, R), dim=1)
+    idx = idx[:, :P]
+    d_m, r_m = torch.gather(D, 1, idx), torch.gather(R, 1, idx)
+    big = torch.iinfo(torch.int64).max
+    Rk = torch.where(BR < 0, torch.full_like(BR, big), BR)
+    S = S + 0.0                                   # -0.0 == 0.0 like Python
+    Sk = torch.where(BR < 0, torch.full_like(S, -math.inf), S)
+    i1 = torch.argsort(Rk, dim=1, stable=True)
+    i2 = torch.argsort(-torch.gather(Sk, 1, i1), dim=1, stable=True)
+    idx = torch.gather(i1, 1, i2)[:, :K]
+    return d_m, r_m, torch.gather(S, 1, idx), torch.gather(BR, 1, idx)
+
+
+def fetch_pool_vectors(rows, q_lo: int, bq: int, gather_local, shard_starts, dim: int, group=None):
+    """Embeddings of the merged MMR pool for THIS rank's query block [q_lo, q_lo + bq).
+
+    rows: (B, P) merged global rows (-1 pad), identical on all ranks; gather_local(local_rows
+    int64 device tensor) -> (n, D) fp32 rows of this rank's shard; shard_starts: G + 1 global row
+    boundaries.  Every rank derives the same send/receive counts from ``rows``, so one all-to-all
+    moves each pool row exactly once, from its owner to the rank fusing its query.  Returns
+    (bq, P, D) fp32 (zeros for -1 pads)."""
+    rank, ws = world()
+    B, P = rows.shape
+    dev = rows.device
+    if ws == 1:
+        return gather_local(rows.reshape(-1)).view(B, P, -1)
+    starts = torch.as_tensor(shard_starts, dtype=torch.int64, device=dev)
+    owner = torch.where(rows >= 0, torch.searchsorted(starts, rows, right=True) - 1, torch.full_like(rows, -1))
+    flat_rows, flat_owner = rows.reshape(-1), owner.reshape(-1)
+    dest = (torch.arange(B * P, device=dev) // P) // bq                       # query block of each entry
+    mine = torch.nonzero(flat_owner == rank).squeeze(1)                       # (q, p) order == dest order
+    send = gather_local(flat_rows[mine] - shard_starts[rank]).reshape(-1, dim)
+    send_counts = torch.bincount(dest[mine], minlength=ws)
+    blk_owner = owner[q_lo:q_lo + bq].reshape(-1)
+    valid = torch.nonzero(blk_owner >= 0).squeeze(1)
+    recv_counts = torch.bincount(blk_owner[valid], minlength=ws)
+    D = int(dim)
+    recv = torch.empty((int(recv_counts.sum()), D), dtype=torch.float32, device=dev)
+    all_to_all(recv, send, recv_counts.tolist(), send_counts.tolist(), group)
+    pos = valid[torch.argsort(blk_owner[valid], stable=True)]                # owner-major, (q, p) inside
+    pool = torch.zeros((bq * P, D), dtype=torch.float32, device=dev)
+    pool[pos] = recv
+    return pool.view(bq, P, D)
 
 
 def max_over_ranks(x: float, device=None, group=None) -> float:

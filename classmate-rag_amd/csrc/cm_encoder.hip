@@ -283,6 +283,7 @@ __global__ void __launch_bounds__(64) short_attention_kernel(const T *__restrict
 // in that order.  Padded keys (>= S) get probability 0 and zero V rows; padded queries
 // are computed and not stored.
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef _Float16 h16x8_t __attribute__((ext_vector_type(8)));
 typedef float f32x4_t __attribute__((ext_vector_type(4)));
 
 __global__ void __launch_bounds__(64) short_attention_mfma_kernel(const __hip_bfloat16 *__restrict__ qkv, int S, int H,
@@ -378,6 +379,156 @@ __global__ void __launch_bounds__(64) short_attention_mfma_kernel(const __hip_bf
   }
 }
 
+// fp32-accurate twin of short_attention_mfma_kernel for the K10 path (fp32 query encode, S <= 32):
+// every MFMA operand is split into f16 halves (v = hi + lo) and each product is lo.hi + hi.lo +
+// hi.hi on v_mfma_f32_16x16x32_f16 (as K10, cm_gemm.hip): S^T = K Q^T from fp32 Q/K fragments
+// split in registers, fp32 softmax on the accumulators, O = P V with P split in registers and
+// V^T staged split in LDS in the permuted key order of the accumulator layout.  The context is
+// written as K10 planes of o * a_scale (the O projection's operand) through an LDS image of the
+// (S x 64) head slice: 16-byte slot stores.
+__device__ inline void split_frag8(const float *p, bool ok, h16x8_t &hi, h16x8_t &lo) {
+  float4 u = make_float4(0.f, 0.f, 0.f, 0.f), v = u;
+  if (ok) {
+    u = reinterpret_cast<const float4 *>(p)[0];
+    v = reinterpret_cast<const float4 *>(p)[1];
+  }
+  const float x[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    _Float16 h, l;
+    f16x3_split1(x[e], h, l);
+    hi[e] = h;
+    lo[e] = l;
+  }
+}
+
+__device__ inline f32x4_t mfma3(const h16x8_t &ah, const h16x8_t &al, const h16x8_t &bh, const h16x8_t &bl, f32x4_t c) {
+  c = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl, c, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh, c, 0, 0, 0);
+}
+
+__global__ void __launch_bounds__(64) short_attention_f16x3_kernel(const float *__restrict__ qkv, int S, int H,
+                                                                   float scale, float a_scale,
+                                                                   _Float16 *__restrict__ planes) {
+  constexpr int VT = 40;  // V^T row stride (keys, halves): 80 B keeps the 8-byte reads aligned
+  __shared__ __attribute__((aligned(16))) _Float16 vt[2][kAttnDh * VT];
+  __shared__ __attribute__((aligned(16))) float oimg[32 * (kAttnDh + 4)];
+  const int lane = threadIdx.x;
+  const int g = lane >> 4, c = lane & 15;
+  const int h = blockIdx.x % H;
+  const int64_t b = blockIdx.x / H;
+  const int64_t tok = 3LL * H * kAttnDh;
+  const float *base = qkv + b * S * tok + (int64_t)h * kAttnDh;
+  const float *kb = base + (int64_t)H * kAttnDh;
+  const float *vb = base + 2LL * H * kAttnDh;
+  // V (S x 64 fp32) -> split V^T in LDS: lane handles key kk = t >> 4, dims 4 (t & 15) .. + 3
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const int t = lane + 64 * u, kk = t >> 4, d0 = 4 * (t & 15);
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (kk < S) v = *reinterpret_cast<const float4 *>(vb + kk * tok + d0);
+    const float x[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      _Float16 hh, ll;
+      f16x3_split1(x[e], hh, ll);
+      vt[0][(d0 + e) * VT + kk] = hh;
+      vt[1][(d0 + e) * VT + kk] = ll;
+    }
+  }
+  h16x8_t qh[2][2], ql[2][2], kh[2][2], kl[2][2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+      const int r = 16 * t + c;
+      const int d0 = 32 * st + 8 * g;
+      split_frag8(base + r * tok + d0, r < S, qh[t][st], ql[t][st]);
+      split_frag8(kb + r * tok + d0, r < S, kh[t][st], kl[t][st]);
+    }
+  f32x4_t sc[2][2];  // [key tile][query tile]: S^T
+#pragma unroll
+  for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+      f32x4_t a = {0.f, 0.f, 0.f, 0.f};
+      a = mfma3(kh[kt][0], kl[kt][0], qh[it][0], ql[it][0], a);
+      a = mfma3(kh[kt][1], kl[kt][1], qh[it][1], ql[it][1], a);
+      sc[kt][it] = a;
+    }
+  h16x8_t ph[2], pl[2];
+#pragma unroll
+  for (int it = 0; it < 2; ++it) {
+    float v[8];
+    float m = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int kt = j >> 2, r = j & 3;
+      const int kk = 16 * kt + 4 * g + r;
+      v[j] = kk < S ? sc[kt][it][r] * scale : -INFINITY;
+      m = fmaxf(m, v[j]);
+    }
+    m = fmaxf(m, __shfl_xor(m, 16));
+    m = fmaxf(m, __shfl_xor(m, 32));
+    float sum = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      v[j] = v[j] == -INFINITY ? 0.f : __expf(v[j] - m);
+      sum += v[j];
+    }
+    sum += __shfl_xor(sum, 16);
+    sum += __shfl_xor(sum, 32);
+    const float inv = 1.f / sum;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      _Float16 hh, ll;
+      f16x3_split1(v[j] * inv, hh, ll);
+      ph[it][j] = hh;
+      pl[it][j] = ll;
+    }
+  }
+  __syncthreads();  // V^T staged
+#pragma unroll
+  for (int dt = 0; dt < kAttnDh / 16; ++dt) {
+    const int d = 16 * dt + c;
+    auto vfrag = [&](int pl2) __attribute__((always_inline)) {
+      const uint2 lo4 = *reinterpret_cast<const uint2 *>(&vt[pl2][d * VT + 4 * g]);
+      const uint2 hi4 = *reinterpret_cast<const uint2 *>(&vt[pl2][d * VT + 16 + 4 * g]);
+      const uint4 w = make_uint4(lo4.x, lo4.y, hi4.x, hi4.y);
+      return *reinterpret_cast<const h16x8_t *>(&w);
+    };
+    const h16x8_t vh = vfrag(0), vl = vfrag(1);
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+      f32x4_t o = {0.f, 0.f, 0.f, 0.f};
+      o = mfma3(ph[it], pl[it], vh, vl, o);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) oimg[(16 * it + 4 * g + r) * (kAttnDh + 4) + d] = o[r] * a_scale;
+    }
+  }
+  __syncthreads();
+  // planes: query row i, dims h*64 + 8 s .. + 7 -> one 16-byte slot per plane
+  const int kb32 = H * kAttnDh / 32;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int t = lane + 64 * u, i = t >> 3, s8 = t & 7;
+    if (i < S) {
+      h16x8_t hh, ll;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        _Float16 a, b2;
+        f16x3_split1(oimg[i * (kAttnDh + 4) + 8 * s8 + e], a, b2);
+        hh[e] = a;
+        ll[e] = b2;
+      }
+      const int64_t off = f16x3_plane_off(b * S + i, h * kAttnDh + 8 * s8, kb32);
+      *reinterpret_cast<h16x8_t *>(planes + off) = hh;
+      *reinterpret_cast<h16x8_t *>(planes + off + 512) = ll;
+    }
+  }
+}
+
 }  // namespace cm
 
 using namespace cm;
@@ -449,8 +600,12 @@ extern "C" int cm_short_attention_split(const float *qkv_dev, int32_t B, int32_t
   if (!qkv_dev || !planes_dev) CM_FAIL(CM_EINVAL, "NULL argument");
   if (head_dim != kAttnDh) CM_FAIL(CM_EINVAL, "head_dim must be 64");
   if (S <= 0 || S > kAttnMaxS || H <= 0) CM_FAIL(CM_EINVAL, "need 0 < S <= 64 and H > 0");
-  hipLaunchKernelGGL((short_attention_kernel<float, true>), dim3((unsigned)((int64_t)B * H)), dim3(64), 0,
-                     (hipStream_t)stream, qkv_dev, S, H, scale, nullptr, a_scale, (_Float16 *)planes_dev);
+  if (S <= 32)   // matrix cores, split precision
+    hipLaunchKernelGGL(short_attention_f16x3_kernel, dim3((unsigned)((int64_t)B * H)), dim3(64), 0,
+                       (hipStream_t)stream, qkv_dev, S, H, scale, a_scale, (_Float16 *)planes_dev);
+  else
+    hipLaunchKernelGGL((short_attention_kernel<float, true>), dim3((unsigned)((int64_t)B * H)), dim3(64), 0,
+                       (hipStream_t)stream, qkv_dev, S, H, scale, nullptr, a_scale, (_Float16 *)planes_dev);
   CM_HIP(hipGetLastError());
   return CM_OK;
 }

@@ -119,3 +119,24 @@ def test_plane_producers_match_split_rows():
     W = engine.F16x3Weight(w, 0.1 * torch.randn(3072, device="cuda"))
     hp = engine.linear_f16x3(p, W, gelu=True, planes_out=2.0 ** 11)
     assert same(hp, engine.split_rows(engine.linear_f16x3(p, W, gelu=True), 2.0 ** 11))
+
+
+@pytest.mark.parametrize("S", [1, 7, 24, 32, 40])
+def test_short_attention_split_f16x3_matches_fp64(S):
+    """The fp32 query-encode attention writing K10 planes (S <= 32: split-precision MFMA kernel,
+    else the fp32 VALU kernel) against an fp64 softmax(q k^T / 8) v, as accurate as torch's fp32."""
+    import torch
+    from classmate_hip import engine
+    torch.manual_seed(S)
+    B, H = 37, 12
+    qkv = 2 * torch.randn(B, S, 3 * H * 64, device="cuda")
+    q, k, v = qkv.double().view(B, S, 3, H, 64).permute(2, 0, 3, 1, 4)
+    ref = (torch.softmax(q @ k.transpose(-1, -2) / 8.0, dim=-1) @ v).transpose(1, 2).reshape(B * S, H * 64)
+    q32, k32, v32 = qkv.view(B, S, 3, H, 64).permute(2, 0, 3, 1, 4)
+    t32 = (torch.softmax(q32 @ k32.transpose(-1, -2) / 8.0, dim=-1) @ v32).transpose(1, 2).reshape(B * S, H * 64)
+    p = engine.short_attention_split(qkv, H, 0.125, 2.0 ** 8)
+    hi, lo = p.halves()
+    got = (hi.double() + lo.double()) / 2.0 ** 8
+    e, e32 = float((got - ref).abs().max()), float((t32.double() - ref).abs().max())
+    print(f"\nattention S={S}: max err {e:.2e} (torch fp32 {e32:.2e})")
+    assert e <= 2 * e32 + 2e-6

@@ -116,6 +116,17 @@ def _worker(rank, port, out_q):
         local = torch.from_numpy(emb)[rows.clamp(0, nd - 1)] * own.unsqueeze(-1)
         res["pool"] = P.assemble_pool_vectors(rows, local, row0, n).numpy()
         res["max"] = P.max_over_ranks(float(rank) + 0.5)
+        # the batched path's exchanges: ONE packed all-gather of both shard lists, then the pool
+        # rows of this rank's query block fetched from their owners with one all-to-all
+        sc, rw = corc.bm25_topk(csr, idf, avgdl, queries[:6], 10)
+        d_m, r_m, s_m, b_m = P.exchange_topk(torch.from_numpy(d.astype(np.float32)), torch.from_numpy(r + row0),
+                                             torch.from_numpy(sc), torch.from_numpy(np.where(rw >= 0, rw + row0, rw)))
+        res["xchg"] = (d_m.numpy(), r_m.numpy(), s_m.numpy(), b_m.numpy())
+        bq = 6 // WS
+        shard_emb = torch.from_numpy(emb[row0:row0 + n])
+        pool = P.fetch_pool_vectors(r_m, rank * bq, bq, lambda lr: shard_emb[lr],
+                                    [P.shard_range(nd, i, WS)[0] for i in range(WS)] + [nd], 32)
+        res["pool_block"] = pool.numpy()
         # filtered BM25 (quirk Q2): candidate statistics all-reduced, epsilon floor from the
         # global first-occurrence order -- the exchange bm25_search_filtered_sharded runs
         for k in (1, 10, 64):
@@ -208,3 +219,27 @@ def test_filtered_bm25_exchange_equals_unsharded_oracle(results, k):
         S, R = r[f"filt_{k}"]
         assert np.array_equal(R, rw)
         assert np.array_equal(S, sc)
+
+
+def test_packed_exchange_and_pool_fetch(results):
+    """exchange_topk (one packed all-gather) == the two separate merges == the unsharded oracle;
+    fetch_pool_vectors gives every rank exactly the embeddings of its query block's merged pool."""
+    rng = np.random.default_rng(8)
+    toks, off, vocab, queries = _corpus()
+    nd = off.shape[0] - 1
+    emb = rng.standard_normal((nd, 32)).astype(np.float32)
+    emb[5] = emb[4]
+    emb[nd // 2 + 1] = emb[4]
+    q = rng.standard_normal((6, 32)).astype(np.float32)
+    q[0] = emb[4]
+    d, r = corc.dense_topk_f64(emb, q, 16)
+    csr = corc.build_csr(toks, off, vocab)
+    idf, _ = corc.bm25_idf(csr["df"], csr["first_key"], nd)
+    sc, rw = corc.bm25_topk(csr, idf, float(off[-1]) / nd, queries[:6], 10)
+    bq = 6 // WS
+    for res in results:
+        D, R, S, BR = res["xchg"]
+        assert np.array_equal(R, r) and np.array_equal(D, d.astype(np.float32))
+        assert np.array_equal(BR, rw) and np.array_equal(S, sc)
+        blk = r[res["rank"] * bq:(res["rank"] + 1) * bq]
+        np.testing.assert_array_equal(res["pool_block"], emb[blk])
