@@ -370,7 +370,7 @@ struct Carver {
   size_t off = 0;
   template <typename T>
   T *take(size_t n) {
-    T *p = reinterpret_cast<T *>(base + off);
+    T *p = base ? reinterpret_cast<T *>(base + off) : nullptr;  // base == nullptr: sizing pass only
     off += round_up((int64_t)std::max<size_t>(n, 1) * sizeof(T), 256);
     return p;
   }

@@ -10,7 +10,10 @@ from pathlib import Path
 
 import numpy as np
 
-_LIB = Path(__file__).with_name("liboracle.so")
+import os
+
+# CM_ORACLE_LIB: an alternative build of the same source (tools/asan_check.sh: ASan/UBSan)
+_LIB = Path(os.environ.get("CM_ORACLE_LIB") or Path(__file__).with_name("liboracle.so"))
 _lib = None
 
 
