@@ -329,13 +329,16 @@ class E5MultilingualEmbedder:
         """TunableOp lookup of the hipBLASLt solutions measured on MI355X for the E5 GEMM shapes of
         a 256 x 24-token query batch (tunableop_e5_gfx950.csv; tools/tune_probe.sh regenerates it),
         scoped to a graph capture: the table is read first and lookup is switched on only if it
-        loaded; no tuning, no recording of untuned shapes, results file /dev/null; the previous
-        TunableOp state is restored on exit, so later GEMMs of the host application are untouched
-        (the captured graph keeps the tuned kernels).  Yields whether the table is in use.
-        CM_E5_TUNABLEOP=0 disables it."""
+        loaded; no tuning, no recording of untuned shapes, results file /dev/null; the enable,
+        tuning, recording and filename flags are restored on exit (the captured graph keeps the
+        tuned kernels).  The table's entries stay in the process's TunableOp results table (torch
+        has no way to drop them), so the table is skipped when the host application already uses
+        TunableOp (enabled, or a results file set): its own results are never mixed with ours.
+        Yields whether the table is in use.  CM_E5_TUNABLEOP=0 disables it."""
         import torch.cuda.tunable as tun
         table = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tunableop_e5_gfx950.csv")
-        if os.environ.get("CM_E5_TUNABLEOP", "1") == "0" or not os.path.exists(table):
+        host_uses = tun.is_enabled() or bool(os.environ.get("PYTORCH_TUNABLEOP_FILENAME"))
+        if os.environ.get("CM_E5_TUNABLEOP", "1") == "0" or not os.path.exists(table) or host_uses:
             yield False
             return
         prev = (tun.is_enabled(), tun.tuning_is_enabled(), tun.record_untuned_is_enabled(), tun.get_filename())

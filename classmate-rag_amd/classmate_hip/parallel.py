@@ -183,33 +183,97 @@ def allreduce_filtered_stats(stats_t, df_t, group=None):
 def filtered_eps_global(df_v: np.ndarray, first_key: np.ndarray, row0: int, n_cand: int, group=None) -> float:
     """rank_bm25's epsilon over the global candidate set: every term's candidate df summed and its
     first (global row, position) key minimised over the shards, then the idf average in that
-    first-occurrence order (bm25_idf_table)."""
-    gdf, gfk, _, _ = allreduce_bm25_stats(np.asarray(df_v, np.int64), np.asarray(first_key, np.uint64), row0, 0, 0,
-                                          group=group)
+    first-occurrence order (bm25_idf_table).  A shard whose vocabulary is shorter (an empty shard
+    has none) pads with absent terms."""
+    df_v, first_key = np.asarray(df_v, np.int64), np.asarray(first_key, np.uint64)
+    V = _max_flags([df_v.shape[0]], group)[0]
+    if df_v.shape[0] < V:
+        df_v = np.concatenate([df_v, np.zeros(V - df_v.shape[0], np.int64)])
+        first_key = np.concatenate([first_key, np.full(V - first_key.shape[0], EMPTY_U64)])
+    gdf, gfk, _, _ = allreduce_bm25_stats(df_v, first_key, row0, 0, 0, group=group)
     _, eps = bm25_idf_table(gdf, gfk, int(n_cand))
     return eps
+
+
+def _max_flags(vals, group=None):
+    """Element-wise MAX of small integers over the ranks (identity when world == 1)."""
+    _, ws = world()
+    if ws == 1:
+        return [int(v) for v in vals]
+    t = torch.tensor([int(v) for v in vals], dtype=torch.int64, device=_coll_device(group))
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    return [int(v) for v in t.cpu().tolist()]
+
+
+def _raise_together(err, group=None):
+    """Every rank raises when any rank failed, so no rank is left blocked in the next collective:
+    the failing rank re-raises its own exception, the others a RuntimeError naming it."""
+    if _max_flags([err is not None], group)[0]:
+        if err is not None:
+            raise err
+        raise RuntimeError("sharded BM25 search failed on another rank")
 
 
 def bm25_search_filtered_sharded(bm, q_terms, q_off, k: int, allow, row0: int, group=None):
     """Filtered BM25 over a sharded corpus: local candidate statistics -> all-reduce -> every shard
     scores its allowed documents with the global statistics (device idf) -> all-gather merge.
     bm: this rank's engine.BM25Index (prepare_filtered(global docs) called); allow: this shard's
-    device allow words.  Returns the global (scores, global rows) top-k, identical on all ranks."""
-    stats, df = bm.filter_stats_dev(allow, q_terms)
+    device allow words.  Returns the global (scores, global rows) top-k, identical on all ranks.
+
+    Every rank joins every exchange: a shard without documents contributes zero statistics and
+    empty lists, and an error on one rank is raised on all of them (_raise_together)."""
+    nq = q_off.numel() - 1
+    dev = q_terms.device
+    empty = bm.num_docs == 0
+    err = stats = df = None
+    try:
+        if empty:
+            stats = torch.zeros(2, dtype=torch.int64, device=dev)
+            df = torch.zeros(max(q_terms.numel(), 1), dtype=torch.int64, device=dev)
+        else:
+            stats, df = bm.filter_stats_dev(allow, q_terms)
+    except Exception as e:  # noqa: BLE001 -- re-raised below on every rank
+        err = e
+    _raise_together(err, group)
     allreduce_filtered_stats(stats, df, group)
-    s, r, st = bm.search_stats_dev(q_terms, q_off, k, allow, stats, df)
-    code = int(st.item())
-    if code & bm.FILT_EPS_MISSING:          # the same on every rank: the statistics are global
-        dfv, fkv = bm.filter_term_stats_dev(allow)
-        eps = filtered_eps_global(dfv.cpu().numpy(), fkv.cpu().numpy().view(np.uint64), row0,
-                                  int(stats[0].item()), group)
-        eps_t = torch.tensor([eps], dtype=torch.float64, device=q_terms.device)
-        s, r, st = bm.search_stats_dev(q_terms, q_off, k, allow, stats, df, eps=eps_t)
-        code = int(st.item())
-    if code & bm.FILT_ZERO_DIV:
+
+    def local_search(eps_t=None):
+        if empty:
+            return (torch.zeros((nq, k), dtype=torch.float64, device=dev),
+                    torch.full((nq, k), -1, dtype=torch.int64, device=dev), 0)
+        s_, r_, st_ = bm.search_stats_dev(q_terms, q_off, k, allow, stats, df, eps=eps_t)
+        return s_, r_, int(st_.item())
+
+    s = r = None
+    code = 0
+    try:
+        s, r, code = local_search()
+    except Exception as e:  # noqa: BLE001
+        err = e
+    _raise_together(err, group)
+    eps_missing = _max_flags([code & bm.FILT_EPS_MISSING], group)[0]
+    if eps_missing:                         # global statistics: the epsilon floor over all shards
+        try:
+            if empty:
+                dfv, fkv = np.zeros(0, np.int64), np.zeros(0, np.uint64)
+            else:
+                dfv_t, fkv_t = bm.filter_term_stats_dev(allow)
+                dfv, fkv = dfv_t.cpu().numpy(), fkv_t.cpu().numpy().view(np.uint64)
+        except Exception as e:  # noqa: BLE001
+            err = e
+        _raise_together(err, group)
+        eps = filtered_eps_global(dfv, fkv, row0, int(stats[0].item()), group)
+        eps_t = torch.tensor([eps], dtype=torch.float64, device=dev)
+        try:
+            s, r, code = local_search(eps_t)
+        except Exception as e:  # noqa: BLE001
+            err = e
+        _raise_together(err, group)
+    zero_div, other = _max_flags([code & bm.FILT_ZERO_DIV, code & ~(bm.FILT_ZERO_DIV | bm.FILT_EPS_MISSING)], group)
+    if zero_div:
         raise ZeroDivisionError("float division by zero (candidate documents have no tokens)")
-    if code:
-        raise RuntimeError(f"filtered BM25 search status {code}")
+    if other:
+        raise RuntimeError(f"filtered BM25 search status {other}")
     rg = torch.where(r >= 0, r + row0, r)
     return merge_bm25_topk(s, rg, k, group)
 

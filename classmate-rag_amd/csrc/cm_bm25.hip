@@ -45,6 +45,8 @@ constexpr int kTermLanesQd = 16;             // K2b descriptor slots per query (
 // Candidate lists, one per (query, range), k slots each: slot 0 of every list of query q lies
 // contiguous at [q * nr + r] (the merge's first read of all lists is coalesced), slots 1..k-1 of
 // a list contiguous after the heads, at nl + (q * nr + r) * (k - 1) + j - 1 (nl = nq * nr lists).
+// A list holds its entries in slots 0..c-1 and, when c < k, the sentinel (kEmptyKey, ~0u) in slot
+// c; slots past the sentinel are never written or read (most lists are empty: one 12-B write).
 __device__ inline int64_t lslot(int64_t list, int64_t nl, int k, int j) {
   return j == 0 ? list : nl + list * (int64_t)(k - 1) + (j - 1);
 }
@@ -656,8 +658,8 @@ __global__ void __launch_bounds__(kBmThreads) __attribute__((amdgpu_waves_per_eu
           br = bk == kEmptyKey ? 0xffffffffu : (uint32_t)db + (uint32_t)bu;
         }
       }
-      for (int j = i + lane; j < k; j += 64) {
-        const int64_t o = lslot((int64_t)qi * nr + r, (int64_t)nq * nr, k, j);
+      if (lane == 0 && i < k) {  // list terminator (readers stop at the first empty slot)
+        const int64_t o = lslot((int64_t)qi * nr + r, (int64_t)nq * nr, k, i);
         cand_key[o] = kEmptyKey;
         cand_row[o] = 0xffffffffu;
       }

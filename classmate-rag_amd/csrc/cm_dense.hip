@@ -1340,6 +1340,11 @@ struct cm_dense {
   KernelTimer timer;                       // scan-kernel events (cm_dense_timing)
   uint32_t *live = nullptr;
   hipStream_t stream = nullptr;
+  // growth in place (cm_common.h VmBuf): C / invc / live / Xh live in reserved address ranges and
+  // grow by mapping chunks; vm = false -> hipMalloc + prefix copy (devices without VMM)
+  bool vm = false;
+  VmBuf vC, vInvc, vLive, vXh;
+  int64_t mem_cur = 0, mem_peak = 0;       // bytes of the four row arrays (cm_dense_mem_stats)
   DevBuf staging, rows_buf, allow_buf, ws, out_buf;
   std::vector<float> host_tmp;
 };
@@ -1447,8 +1452,51 @@ DenseWs dense_ws_layout(const cm_dense *h, const DenseCfg &c, int nq, int k, voi
   return w;
 }
 
+// Bytes of the four row arrays at `rows` rows (C fp32, invc, live bits, Xh plane).
+int64_t dense_row_bytes(const cm_dense *h, int64_t rows) { return rows * h->ld * 6 + rows * 4 + rows / 8; }
+
+// Reserve the row arrays' address ranges: enough rows to fill the whole device memory, so the
+// index can grow to any size that fits without ever moving (VmBuf).  false -> hipMalloc path.
+bool dense_vm_reserve(cm_dense *h) {
+  const char *e = getenv("CM_DENSE_VMM");
+  if (e && e[0] == '0') return false;
+  size_t free_b = 0, total_b = 0;
+  if (hipMemGetInfo(&free_b, &total_b) != hipSuccess || total_b == 0) return false;
+  const int64_t max_rows = round_up((int64_t)(total_b / (size_t)(h->ld * 6)) + kStepRows, kStepRows);
+  if (!h->vC.reserve(h->dev, (size_t)max_rows * h->ld * 4) || !h->vXh.reserve(h->dev, (size_t)max_rows * h->ld * 2) ||
+      !h->vInvc.reserve(h->dev, (size_t)max_rows * 4) || !h->vLive.reserve(h->dev, (size_t)max_rows / 8)) {
+    h->vC.release();
+    h->vXh.release();
+    h->vInvc.release();
+    h->vLive.release();
+    return false;
+  }
+  h->C = reinterpret_cast<float *>(h->vC.base);
+  h->Xh = reinterpret_cast<_Float16 *>(h->vXh.base);
+  h->invc = reinterpret_cast<float *>(h->vInvc.base);
+  h->live = reinterpret_cast<uint32_t *>(h->vLive.base);
+  return true;
+}
+
 int dense_grow(cm_dense *h, int64_t need_rows) {
   if (need_rows <= h->rows_alloc) return CM_OK;
+  if (h->vm) {
+    // in place: map (zeroed) memory behind the arrays' fixed bases; rows_alloc stays a multiple of
+    // kStepRows, the rows of the mapping slack become usable at the next growth without a map
+    const int64_t cap = round_up(std::max<int64_t>(need_rows, kStepRows), kStepRows);
+    int rc;
+    if ((rc = h->vC.ensure((size_t)cap * h->ld * 4, h->stream)) || (rc = h->vXh.ensure((size_t)cap * h->ld * 2, h->stream)) ||
+        (rc = h->vInvc.ensure((size_t)cap * 4, h->stream)) || (rc = h->vLive.ensure((size_t)cap / 8, h->stream))) {
+      if (rc != CM_EDEVICE) return rc;  // out of memory: the copy path would need even more
+      // the mapping itself failed: move to hipMalloc arrays (the copy below reads the mapped rows)
+    } else {
+      CM_HIP(hipStreamSynchronize(h->stream));
+      h->rows_alloc = cap;
+      h->mem_cur = (int64_t)(h->vC.mapped + h->vXh.mapped + h->vInvc.mapped + h->vLive.mapped);
+      h->mem_peak = std::max(h->mem_peak, h->mem_cur);
+      return CM_OK;
+    }
+  }
   int64_t cap = std::max<int64_t>(need_rows, h->rows_alloc + h->rows_alloc / 2);
   cap = round_up(std::max<int64_t>(cap, kStepRows), kStepRows);
   float *C2 = nullptr, *ic2 = nullptr;
@@ -1461,6 +1509,7 @@ int dense_grow(cm_dense *h, int64_t need_rows) {
       if (p) (void)hipFree(p);
     CM_FAIL(CM_ENOMEM, "dense: out of device memory");
   }
+  h->mem_peak = std::max(h->mem_peak, h->mem_cur + dense_row_bytes(h, cap));  // old + new at once
   CM_HIP(hipMemsetAsync(C2, 0, nel * 4, h->stream));
   CM_HIP(hipMemsetAsync(ic2, 0, (size_t)cap * 4, h->stream));
   CM_HIP(hipMemsetAsync(lv2, 0, (size_t)cap / 8, h->stream));
@@ -1474,13 +1523,22 @@ int dense_grow(cm_dense *h, int64_t need_rows) {
     CM_HIP(hipMemcpyAsync(xh2, h->Xh, old * 2, hipMemcpyDeviceToDevice, h->stream));
   }
   CM_HIP(hipStreamSynchronize(h->stream));
-  for (void *p : {(void *)h->C, (void *)h->invc, (void *)h->live, (void *)h->Xh})
-    if (p) (void)hipFree(p);
+  if (h->vm) {  // leaving the reserved ranges for good
+    h->vC.release();
+    h->vXh.release();
+    h->vInvc.release();
+    h->vLive.release();
+    h->vm = false;
+  } else {
+    for (void *p : {(void *)h->C, (void *)h->invc, (void *)h->live, (void *)h->Xh})
+      if (p) (void)hipFree(p);
+  }
   h->C = C2;
   h->invc = ic2;
   h->live = lv2;
   h->Xh = xh2;
   h->rows_alloc = cap;
+  h->mem_cur = dense_row_bytes(h, cap);
   return CM_OK;
 }
 
@@ -1798,6 +1856,7 @@ int cm_dense_create(int device, int32_t dim, int64_t capacity, cm_dense **out) {
     cm_dense_destroy(h);
     CM_FAIL(CM_ENOMEM, "dense: out of device memory");
   }
+  h->vm = dense_vm_reserve(h);
   int rc = dense_grow(h, std::max<int64_t>(capacity, kStepRows));
   if (rc) {
     cm_dense_destroy(h);
@@ -1811,10 +1870,17 @@ void cm_dense_destroy(cm_dense *h) {
   if (!h) return;
   DeviceGuard dg(h->dev);
   if (h->stream) (void)hipStreamSynchronize(h->stream);
-  if (h->C) (void)hipFree(h->C);
-  if (h->invc) (void)hipFree(h->invc);
-  if (h->live) (void)hipFree(h->live);
-  if (h->Xh) (void)hipFree(h->Xh);
+  if (h->vm) {
+    h->vC.release();
+    h->vXh.release();
+    h->vInvc.release();
+    h->vLive.release();
+  } else {
+    if (h->C) (void)hipFree(h->C);
+    if (h->invc) (void)hipFree(h->invc);
+    if (h->live) (void)hipFree(h->live);
+    if (h->Xh) (void)hipFree(h->Xh);
+  }
   if (h->rnorm) (void)hipFree(h->rnorm);
   h->timer.release();
   h->staging.release();
@@ -1910,6 +1976,14 @@ int cm_dense_reset(cm_dense *h) {
   CM_HIP(hipMemsetAsync(h->rnorm, 0, 8, h->stream));
   CM_HIP(hipStreamSynchronize(h->stream));
   h->size = 0;
+  return CM_OK;
+}
+
+int cm_dense_mem_stats(cm_dense *h, int64_t *cur_bytes, int64_t *peak_bytes, int32_t *in_place) {
+  if (!h) CM_FAIL(CM_EINVAL, "null handle");
+  if (cur_bytes) *cur_bytes = h->mem_cur;
+  if (peak_bytes) *peak_bytes = h->mem_peak;
+  if (in_place) *in_place = h->vm ? 1 : 0;
   return CM_OK;
 }
 

@@ -112,7 +112,9 @@ def test_plane_producers_match_split_rows():
     hi, lo = q.halves()
     rec = (hi.double() + lo.double()) / 2.0 ** 9
     assert float((rec - out.view(-1, D).double()).abs().max()) <= 2.0 ** -21 * float(out.abs().max())
-    qkv = torch.randn(B, S, 3 * D, device="cuda")
+    # attention: S > 32 runs the fp32 VALU kernel, whose planes are the split of its fp32 output;
+    # S <= 32 runs the split-precision MFMA kernel (held to fp64 in the test below)
+    qkv = torch.randn(B, 40, 3 * D, device="cuda")
     pa = engine.short_attention_split(qkv, H, 0.125, 2.0 ** 10)
     assert same(pa, engine.split_rows(engine.short_attention(qkv, H, 0.125), 2.0 ** 10))
     w = 0.02 * torch.randn(3072, D, device="cuda")

@@ -78,6 +78,23 @@ def _worker(rank, port, out_q):
         for k in (1, 10, 64):
             S, R = P.bm25_search_filtered_sharded(bm, qt, qo, k, allow, row0)
             res[f"filt_{k}"] = (S.cpu().numpy(), R.cpu().numpy())
+        # uneven shards: rank 0 holds every document, rank 1 an empty index -- it joins every
+        # exchange with zero statistics and empty lists (no hang, same results)
+        if rank == 0:
+            full = engine.BM25Index(device=0)
+            full.build(toks, off, vocab)
+            fm = _filter_mask(nd)
+            fw = np.zeros((nd + 31) // 32, np.uint32)
+            fi = np.nonzero(fm)[0]
+            np.bitwise_or.at(fw, fi >> 5, (np.uint32(1) << (fi & 31).astype(np.uint32)))
+            f_allow = torch.from_numpy(fw.view(np.int32)).cuda()
+        else:
+            full = engine.BM25Index(device=0)                 # never built: no documents
+            f_allow = torch.zeros(1, dtype=torch.int32, device="cuda")
+        full.prepare_filtered(nd)
+        S, R = P.bm25_search_filtered_sharded(full, qt, qo, 10, f_allow, 0)
+        res["filt_uneven_10"] = (S.cpu().numpy(), R.cpu().numpy())
+        full.close()
         emb, q = _dense_data(nd)
         dn = engine.DenseIndex(DIM, device=0, capacity=n)
         dn.upsert(emb[row0:row0 + n], np.arange(n, dtype=np.int64))
@@ -150,3 +167,7 @@ def test_sharded_hip_bm25_filtered_equals_unsharded_oracle(results, k):
         S, R = r[f"filt_{k}"]
         assert np.array_equal(R, rw)
         assert np.array_equal(S, sc)
+        if k == 10:                                  # one shard empty (no hang)
+            S, R = r["filt_uneven_10"]
+            assert np.array_equal(R, rw)
+            assert np.array_equal(S, sc)

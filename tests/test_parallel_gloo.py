@@ -131,6 +131,18 @@ def _worker(rank, port, out_q):
         # global first-occurrence order -- the exchange bm25_search_filtered_sharded runs
         for k in (1, 10, 64):
             res[f"filt_{k}"] = _filtered_shard_search(P, toks, off, vocab, queries, row0, n, k)
+        # a failure on one rank is raised on every rank (none is left blocked in a collective)
+        try:
+            P._raise_together(ValueError("shard failure") if rank == 1 else None)
+            res["raise"] = None
+        except Exception as e:  # noqa: BLE001
+            res["raise"] = type(e).__name__
+        # the epsilon exchange with an empty shard (no vocabulary): rank 0's candidates only
+        if rank == 0:
+            res["eps_uneven"] = P.filtered_eps_global(csr["df"], csr["first_key"], 0, n)
+        else:
+            res["eps_uneven"] = P.filtered_eps_global(np.zeros(0, np.int64), np.zeros(0, np.uint64), row0,
+                                                      P.shard_range(nd, 0, WS)[1])   # the global count
         out_q.put(res)
     finally:
         dist.destroy_process_group()
@@ -243,3 +255,22 @@ def test_packed_exchange_and_pool_fetch(results):
         assert np.array_equal(BR, rw) and np.array_equal(S, sc)
         blk = r[res["rank"] * bq:(res["rank"] + 1) * bq]
         np.testing.assert_array_equal(res["pool_block"], emb[blk])
+
+
+def test_errors_raise_on_every_rank_and_empty_shard_eps(results):
+    """ADVICE r2: a local failure must not leave the other ranks blocked in the next collective;
+    an empty shard (no vocabulary) joins the epsilon exchange with padded arrays."""
+    assert [r["raise"] for r in results] == ["RuntimeError", "ValueError"]
+    toks, off, vocab, _ = _corpus()
+    nd = off.shape[0] - 1
+    _, n0 = shard_range_cpu(nd, 0, WS)
+    csr0 = corc.build_csr(toks[:off[n0]], off[:n0 + 1], vocab)
+    _, eps0 = corc.bm25_idf(csr0["df"], csr0["first_key"], n0)
+    for r in results:
+        assert r["eps_uneven"] == eps0
+
+
+def shard_range_cpu(n_total, rank, ws):
+    per = (n_total + ws - 1) // ws
+    lo = min(rank * per, n_total)
+    return lo, min(lo + per, n_total) - lo
