@@ -393,23 +393,31 @@ class E5MultilingualEmbedder:
                 fwd()
         return ids, mask, out, graph
 
-    def _encode(self, texts: List[str], batch_size: int = 32) -> np.ndarray:
+    def _encode_dev(self, texts: List[str], batch_size: int = 32):
+        """(len(texts), 768) fp32 device tensor: sentence-transformers' length-sorted batches of
+        ``batch_size`` (its encode() default), each through encode_token_ids, order restored."""
         import torch
+        out = torch.empty((len(texts), self.model.config.hidden_size), dtype=torch.float32, device=self.device)
         if not texts:
-            return np.zeros((0, self.model.config.hidden_size), np.float32)
-        # sentence-transformers sorts by length for batching and restores the order
+            return out
         order = np.argsort([-len(t) for t in texts], kind="stable")
-        out = np.empty((len(texts), self.model.config.hidden_size), np.float32)
         for s in range(0, len(texts), batch_size):
             idx = order[s: s + batch_size]
             ids, mask = self._tokenize([texts[i] for i in idx])
-            emb = self.encode_token_ids(ids, mask)
-            out[idx] = emb.float().cpu().numpy()
-        torch.cuda.synchronize(self.device)
+            out[torch.from_numpy(np.ascontiguousarray(idx)).to(self.device)] = self.encode_token_ids(ids, mask).float()
         return out
+
+    def _encode(self, texts: List[str], batch_size: int = 32) -> np.ndarray:
+        if not texts:
+            return np.zeros((0, self.model.config.hidden_size), np.float32)
+        return self._encode_dev(texts, batch_size).cpu().numpy()
 
     def encode_queries(self, queries: Iterable[str]) -> np.ndarray:
         return self._encode(self._fmt_queries(queries)).astype("float32", copy=False)
+
+    def encode_queries_dev(self, queries: Iterable[str]):
+        """encode_queries, left on the device (the batched retrieval path consumes it there)."""
+        return self._encode_dev(self._fmt_queries(queries))
 
     def encode_passages(self, texts: Iterable[str]) -> np.ndarray:
         return self._encode(self._fmt_passages(texts)).astype("float32", copy=False)

@@ -145,6 +145,7 @@ class BM25Store:
     _dirty: bool = field(default=True, repr=False)
     _meta_dirty: bool = field(default=True, repr=False)
     _csr: Optional[tuple] = field(default=None, repr=False)  # persisted (term_ids, doc_off) to build from
+    _version: int = field(default=0, repr=False)   # bumped by every change of the document set
 
     # ---------- core ops ----------
     def _term_ids(self, tokens: Sequence[str]) -> np.ndarray:
@@ -155,6 +156,7 @@ class BM25Store:
         """bm25.py:140-145: the reference rebuilds BM25Okapi here; it raises ZeroDivisionError when
         entries exist but every token list is empty.  We check that and defer the device build."""
         self._id_list = list(self._entries.keys())
+        self._version += 1
         self._csr = None
         if self._entries and all(len(e.tokens) == 0 for e in self._entries.values()):
             raise ZeroDivisionError("float division by zero")
@@ -335,6 +337,7 @@ class BM25Store:
         self._entries = cat
         self._vocab = {t: i for i, t in enumerate(vocab)}
         self._id_list = list(ids)
+        self._version += 1
         self._csr = (term_ids, doc_off)
         self._dirty = self._meta_dirty = True
         return True

@@ -1,0 +1,153 @@
+"""``HybridRetriever.retrieve_batch`` with the whole batch resident on the device.
+
+The drop-in path (fusion.py) follows the reference's control flow per stage: the vector store
+returns result dicts with their embeddings, MMR runs over host copies of the pools, the BM25 store
+returns result dicts, and the merge matches items by id on the host (rag/retrieval/fusion.py:
+108-167).  For an unfiltered hybrid batch with MMR -- the configuration the reference's callers
+use (rag/pipeline/rag.py:549, tools/bench_ask.py:19-38) -- every one of those steps has a device
+form: cosine pool search (K1c/K1s), pool gather + MMR (K4), BM25 top-k (K2a/K2b/K2 + K3), pool
+preparation + RRF merge (K5).  This module chains them without a host round trip and builds result
+dicts only for the final top_k items of each query.
+
+Id matching: the merge compares integer keys.  A document's key is its vector-store row; a BM25
+document that the vector store does not hold gets ``n_vector_rows + bm25_row``.  The BM25-row ->
+key map is a device array rebuilt when either store changes (their ``_version`` counters).
+
+The result dicts equal the host path's (tests/test_gpu_dropin.py checks both on the same
+stores): same ids, documents, metadata objects, distances (fp32 -> float), BM25 scores and fused
+scores, in the same order.
+"""
+from __future__ import annotations
+
+from typing import Any, Dict, List, Optional, Sequence
+
+import numpy as np
+
+from .. import _lib as L
+from .. import engine
+
+
+class _KeyMap:
+    """BM25 rows <-> merge keys for one (vector store version, BM25 store version)."""
+
+    def __init__(self, vs, bm, device: int):
+        import torch
+        ids_bm = bm._id_list
+        nvr = len(vs._ids)
+        if len(ids_bm) == nvr and ids_bm == vs._ids:          # the common case: one corpus, same order
+            bm2key = np.arange(nvr, dtype=np.int64)
+            vs2bm = np.arange(nvr, dtype=np.int64)
+        else:
+            rowmap = vs._row
+            bm2key = np.fromiter((rowmap.get(i, -1) for i in ids_bm), dtype=np.int64, count=len(ids_bm))
+            only = bm2key < 0
+            bm2key[only] = nvr + np.nonzero(only)[0]
+            vs2bm = np.full(nvr, -1, np.int64)
+            both = ~only
+            vs2bm[bm2key[both]] = np.nonzero(both)[0]
+        self.nvr = nvr
+        self.vs2bm = vs2bm
+        self.bm2key_dev = torch.from_numpy(bm2key).to(torch.device("cuda", device))
+
+
+def applicable(retr, filters, hybrid: bool) -> bool:
+    """The device batch path covers unfiltered hybrid retrieval with MMR over this package's stores
+    (anything else takes the host path)."""
+    from .bm25 import BM25Store
+    from .vector_store import GpuVectorStore
+    vs, bm = retr.vector_store, retr.bm25_store
+    if filters or not hybrid or not retr.use_mmr:
+        return False
+    if not isinstance(vs, GpuVectorStore) or not isinstance(bm, BM25Store):
+        return False
+    vs._ensure_loaded()
+    if vs._index is None or not bm._entries:
+        return False
+    pool = max(retr.k_vector, retr.mmr_max_pool)
+    limit = L.max_topk()
+    if not (0 < retr.k_vector <= pool <= limit and 0 < retr.k_bm25 <= limit):
+        return False
+    # the host path clamps k to the candidates; the device path needs full lists
+    return vs._index.live_count() >= pool and len(bm._id_list) >= retr.k_bm25
+
+
+def _query_vectors(embedder, questions: Sequence[str], dev):
+    import torch
+    enc = getattr(embedder, "encode_queries_dev", None)
+    if enc is not None:
+        q = enc(questions)
+        if q.device == dev and q.dtype == torch.float32:
+            return q.contiguous()
+    q = np.ascontiguousarray(np.asarray(embedder.encode_queries(list(questions)), np.float32))
+    return torch.from_numpy(q).to(dev)
+
+
+def retrieve_batch(retr, questions: Sequence[str], top_k: int) -> List[List[Dict[str, Any]]]:
+    """retr.retrieve_batch(questions, filters=None, top_k, hybrid=True) on the device (see module
+    docstring); the caller checked ``applicable``."""
+    import torch
+    vs, bm = retr.vector_store, retr.bm25_store
+    index = vs._index
+    dev = torch.device("cuda", index.device)
+    nq = len(questions)
+    kv, kb = retr.k_vector, retr.k_bm25
+    pool = max(kv, retr.mmr_max_pool)
+    # BM25 query terms (host tokenizer, as the reference) while nothing else needs the host
+    bm._ensure_index()
+    key = (vs._version, bm._version)
+    km = getattr(retr, "_device_keymap", None)
+    if km is None or km[0] != key:
+        km = (key, _KeyMap(vs, bm, index.device))
+        retr._device_keymap = km
+    km = km[1]
+    blank = np.array([not q.strip() for q in questions], bool)
+    qids = [[] if blank[i] else bm._query_ids(q) for i, q in enumerate(questions)]
+    off = np.zeros(nq + 1, np.int32)
+    off[1:] = np.cumsum([len(x) for x in qids])
+    flat = np.asarray([t for x in qids for t in x] or [0], np.int32)
+    q_terms = torch.from_numpy(flat).to(dev)
+    q_off = torch.from_numpy(off).to(dev)
+    # dense pool + MMR
+    q = _query_vectors(retr.embedder, questions, dev)
+    d, r = index.search_dev(q, pool)
+    vecs = index.gather_dev(r.reshape(-1)).view(nq, pool, index.dim)
+    order = engine.mmr_dev(q, vecs, kv, float(retr.mmr_lambda))
+    # BM25 top-k (whitespace-only queries: no BM25 list, bm25.py:178)
+    bs, br = bm._index.search_dev(q_terms, q_off, kb)
+    bkeys = torch.where(br >= 0, km.bm2key_dev[br.clamp(min=0)], torch.full_like(br, -1))
+    if blank.any():
+        bkeys[torch.from_numpy(blank).to(dev)] = -1
+    vk, vd, vn, bn = engine.rrf_pool_prep_dev(r.contiguous(), d.contiguous(), order, bkeys.contiguous())
+    k_dev = top_k if top_k > 0 else kv + kb
+    ok, of, ov, ob, ofl, on = engine.rrf_merge_dev(vk, vd, vn, bkeys.contiguous(), bs.contiguous(), bn,
+                                                   w_vec=retr.weight_vector, w_bm25=retr.weight_bm25,
+                                                   rrf_k=retr.rrf_k, top_k=k_dev)
+    ok, of, ov, ob, ofl, on = (t.cpu().numpy() for t in (ok, of, ov, ob, ofl, on))
+    # result dicts of the final top_k items only (fusion.py:132-167 field rules)
+    out: List[List[Dict[str, Any]]] = []
+    nvr, vs2bm = km.nvr, km.vs2bm
+    vids, vdocs, vmetas = vs._ids, vs._docs, vs._meta.metas
+    bids, entries = bm._id_list, bm._entries
+    for i in range(nq):
+        m = len(range(int(on[i]))[:top_k])               # Python slice of the full order
+        res = []
+        for j in range(m):
+            kk, fl = int(ok[i, j]), int(ofl[i, j])
+            if kk < nvr:
+                _id = vids[kk]
+                doc, meta = vdocs[kk], vmetas[kk] or {}
+                if fl & 2 and (not doc or not meta):
+                    e = entries[bids[int(vs2bm[kk])]]
+                    if not doc and e.text:
+                        doc = e.text
+                    if not meta and e.metadata:
+                        meta = e.metadata
+            else:
+                e = entries[bids[kk - nvr]]
+                _id, doc, meta = e.id, e.text or None, e.metadata or {}
+            res.append({"id": _id, "document": doc, "metadata": meta,
+                        "scores": {"vector_distance": float(ov[i, j]) if fl & 1 else None,
+                                   "bm25_score": float(ob[i, j]) if fl & 2 else None,
+                                   "fused": float(of[i, j])}})
+        out.append(res)
+    return out

@@ -5,16 +5,20 @@
 values; the arithmetic runs in HIP kernels (K4 MMR, K5 RRF merge) instead of
 Python/numpy.  ``HybridRetriever.retrieve_batch`` is the batched form: one
 embedder call, one dense search, one MMR launch, one BM25 launch and one RRF
-launch for the whole batch (per-query semantics unchanged).
+launch for the whole batch (per-query semantics unchanged); unfiltered hybrid
+batches stay on the device end to end (``device_batch``; CM_RETRIEVE_DEVICE=0
+takes the host path).
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 from typing import Any, Dict, List, Mapping, Optional, Sequence
 
 import numpy as np
 
 from .. import engine
+from . import device_batch
 from .filters import build_where_filter
 
 
@@ -176,6 +180,8 @@ class HybridRetriever:
         if not questions:
             return []
         raw_filters = filters or {}
+        if os.environ.get("CM_RETRIEVE_DEVICE", "1") != "0" and device_batch.applicable(self, raw_filters, hybrid):
+            return device_batch.retrieve_batch(self, questions, top_k)   # whole batch on the device
         chroma_where = build_where_filter(raw_filters) if raw_filters else None
         bm_where = raw_filters or None
         k = self.k_vector if hybrid else max(top_k, self.k_vector)

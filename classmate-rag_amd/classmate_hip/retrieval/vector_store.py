@@ -54,6 +54,7 @@ class GpuVectorStore:
     _docs: List[Optional[str]] = field(default_factory=list, init=False, repr=False)
     _meta: MetaIndex = field(default_factory=MetaIndex, init=False, repr=False)
     _loaded: bool = field(default=False, init=False, repr=False)
+    _version: int = field(default=0, init=False, repr=False)   # bumped by every mutation (device key maps)
 
     def __post_init__(self):
         if self.distance != "cosine":
@@ -88,6 +89,7 @@ class GpuVectorStore:
                         recs[rec["row"]] = rec
         vecs = np.memmap(d / "vectors.f32", dtype=np.float32, mode="r", shape=(n, dim)) if n else None
         self._index = engine.DenseIndex(dim, device=self.device, capacity=max(n, 1))
+        self._version += 1
         live = []
         for r in range(n):
             rec = recs.get(r)
@@ -180,6 +182,7 @@ class GpuVectorStore:
             raise ValueError(f"Embedding dimension {emb.shape[1]} does not match collection dimensionality "
                              f"{self._index.dim}")
         rows = np.empty(len(ids), np.int64)
+        self._version += 1
         for i, _id in enumerate(ids):
             r = self._row.get(_id)
             if r is None:
@@ -200,6 +203,7 @@ class GpuVectorStore:
         rows = [self._row.pop(i) for i in ids if i in self._row]
         if not rows:
             return
+        self._version += 1
         for r in rows:
             self._ids[r] = None
             self._docs[r] = None
@@ -278,6 +282,7 @@ class GpuVectorStore:
         if self._index is not None:
             self._index.close()
         self._index = None
+        self._version += 1
         self._ids, self._row, self._docs = [], {}, []
         self._meta = MetaIndex()
         d = self._dir

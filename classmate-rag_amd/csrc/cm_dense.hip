@@ -348,7 +348,7 @@ __global__ void __launch_bounds__(256) dense_prep_planes(const float *__restrict
   for (int i = threadIdx.x; i < ld; i += 256) {
     const float v = (qi < nq && i < dim) ? src[i] * inv : 0.f;
     const _Float16 hi = (_Float16)v;
-    const float lo = (float)(_Float16)(v - (float)hi);
+    const float lo = v - (float)hi;  // exact residual (the error bound's ||ql||)
     Qh[(int64_t)qi * ld + i] = hi;
     sh += (float)hi * (float)hi;
     sl += lo * lo;
@@ -1233,8 +1233,8 @@ __global__ void __launch_bounds__(256) dense_scatter_kernel(const float *__restr
   float sh = 0.f, sl = 0.f;
   for (int c = threadIdx.x; c < ld; c += 256) {
     const float xn = (c < dim ? s[c] : 0.f) * inv;
-    const _Float16 hi = (_Float16)xn;
-    const float lo = (float)(_Float16)(xn - (float)hi);
+    const _Float16 hi = (_Float16)xn;  // subnormal halves included: the matrix cores keep them
+    const float lo = xn - (float)hi;    // exact residual (||xl|| of the bound E; tools/denorm_probe.hip)
     Xh[plane_off(r, c, ld)] = hi;
     sh += (float)hi * (float)hi;
     sl += lo * lo;

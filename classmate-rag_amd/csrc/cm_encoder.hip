@@ -386,17 +386,36 @@ __global__ void __launch_bounds__(64) short_attention_mfma_kernel(const __hip_bf
 // V^T staged split in LDS in the permuted key order of the accumulator layout.  The context is
 // written as K10 planes of o * a_scale (the O projection's operand) through an LDS image of the
 // (S x 64) head slice: 16-byte slot stores.
-__device__ inline void split_frag8(const float *p, bool ok, h16x8_t &hi, h16x8_t &lo) {
+// f16 range: a lo half below 2^-14 is subnormal, with an absolute precision of 2^-24 instead of
+// 11 significant bits (a probability of 0.05 has a lo half of ~2e-5), and the unscaled split of
+// Q, K, V and P measured 1.3e-4 context errors at S = 24 against 1e-5 for torch's fp32.  Every
+// operand is therefore split after an exact power-of-two scale that puts the wave's largest |x|
+// in [2^13, 2^14) -- Q, K and V by their per-(sequence, head) maxima, P (<= 1) by 2^14 -- so the
+// split keeps 22 significant bits, and the scales are undone exactly on the fp32 accumulators.
+__device__ inline float pow2_scale_for(float amax) {
+  if (!(amax > 0.f)) return 1.f;
+  int e;
+  (void)frexpf(amax, &e);  // amax = m 2^e, m in [0.5, 1)
+  return ldexpf(1.f, 14 - e);
+}
+__device__ inline float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+  return v;
+}
+__device__ inline void load_frag8(const float *p, bool ok, float (&x)[8]) {
   float4 u = make_float4(0.f, 0.f, 0.f, 0.f), v = u;
   if (ok) {
     u = reinterpret_cast<const float4 *>(p)[0];
     v = reinterpret_cast<const float4 *>(p)[1];
   }
-  const float x[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
+  x[0] = u.x, x[1] = u.y, x[2] = u.z, x[3] = u.w, x[4] = v.x, x[5] = v.y, x[6] = v.z, x[7] = v.w;
+}
+__device__ inline void split_frag8(const float (&x)[8], float s, h16x8_t &hi, h16x8_t &lo) {
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
     _Float16 h, l;
-    f16x3_split1(x[e], h, l);
+    f16x3_split1(x[e] * s, h, l);
     hi[e] = h;
     lo[e] = l;
   }
@@ -412,6 +431,7 @@ __global__ void __launch_bounds__(64) short_attention_f16x3_kernel(const float *
                                                                    float scale, float a_scale,
                                                                    _Float16 *__restrict__ planes) {
   constexpr int VT = 40;  // V^T row stride (keys, halves): 80 B keeps the 8-byte reads aligned
+  constexpr float kPScale = 16384.f;  // P in [0, 1] -> [0, 2^14]
   __shared__ __attribute__((aligned(16))) _Float16 vt[2][kAttnDh * VT];
   __shared__ __attribute__((aligned(16))) float oimg[32 * (kAttnDh + 4)];
   const int lane = threadIdx.x;
@@ -422,17 +442,46 @@ __global__ void __launch_bounds__(64) short_attention_f16x3_kernel(const float *
   const float *base = qkv + b * S * tok + (int64_t)h * kAttnDh;
   const float *kb = base + (int64_t)H * kAttnDh;
   const float *vb = base + 2LL * H * kAttnDh;
-  // V (S x 64 fp32) -> split V^T in LDS: lane handles key kk = t >> 4, dims 4 (t & 15) .. + 3
+  // every load of the wave first: V (lane: key kk = t >> 4, dims 4 (t & 15) .. + 3), Q and K fragments
+  float4 vv[8];
 #pragma unroll
   for (int u = 0; u < 8; ++u) {
     const int t = lane + 64 * u, kk = t >> 4, d0 = 4 * (t & 15);
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (kk < S) v = *reinterpret_cast<const float4 *>(vb + kk * tok + d0);
-    const float x[4] = {v.x, v.y, v.z, v.w};
+    vv[u] = kk < S ? *reinterpret_cast<const float4 *>(vb + kk * tok + d0) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  float qx[2][2][8], kx[2][2][8];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+      const int r = 16 * t + c;
+      const int d0 = 32 * st + 8 * g;
+      load_frag8(base + r * tok + d0, r < S, qx[t][st]);
+      load_frag8(kb + r * tok + d0, r < S, kx[t][st]);
+    }
+  float mq = 0.f, mk = 0.f, mv = 0.f;
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int st = 0; st < 2; ++st)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        mq = fmaxf(mq, fabsf(qx[t][st][e]));
+        mk = fmaxf(mk, fabsf(kx[t][st][e]));
+      }
+#pragma unroll
+  for (int u = 0; u < 8; ++u)
+    mv = fmaxf(mv, fmaxf(fmaxf(fabsf(vv[u].x), fabsf(vv[u].y)), fmaxf(fabsf(vv[u].z), fabsf(vv[u].w))));
+  const float sq = pow2_scale_for(wave_max(mq)), sk = pow2_scale_for(wave_max(mk)), sv = pow2_scale_for(wave_max(mv));
+  // split V^T into LDS
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const int t = lane + 64 * u, kk = t >> 4, d0 = 4 * (t & 15);
+    const float x[4] = {vv[u].x, vv[u].y, vv[u].z, vv[u].w};
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       _Float16 hh, ll;
-      f16x3_split1(x[e], hh, ll);
+      f16x3_split1(x[e] * sv, hh, ll);
       vt[0][(d0 + e) * VT + kk] = hh;
       vt[1][(d0 + e) * VT + kk] = ll;
     }
@@ -442,12 +491,10 @@ __global__ void __launch_bounds__(64) short_attention_f16x3_kernel(const float *
   for (int t = 0; t < 2; ++t)
 #pragma unroll
     for (int st = 0; st < 2; ++st) {
-      const int r = 16 * t + c;
-      const int d0 = 32 * st + 8 * g;
-      split_frag8(base + r * tok + d0, r < S, qh[t][st], ql[t][st]);
-      split_frag8(kb + r * tok + d0, r < S, kh[t][st], kl[t][st]);
+      split_frag8(qx[t][st], sq, qh[t][st], ql[t][st]);
+      split_frag8(kx[t][st], sk, kh[t][st], kl[t][st]);
     }
-  f32x4_t sc[2][2];  // [key tile][query tile]: S^T
+  f32x4_t sc[2][2];  // [key tile][query tile]: S^T (times sq sk)
 #pragma unroll
   for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
@@ -457,6 +504,7 @@ __global__ void __launch_bounds__(64) short_attention_f16x3_kernel(const float *
       a = mfma3(kh[kt][1], kl[kt][1], qh[it][1], ql[it][1], a);
       sc[kt][it] = a;
     }
+  const float lscale = scale / (sq * sk);  // exact: sq sk is a power of two
   h16x8_t ph[2], pl[2];
 #pragma unroll
   for (int it = 0; it < 2; ++it) {
@@ -466,7 +514,7 @@ __global__ void __launch_bounds__(64) short_attention_f16x3_kernel(const float *
     for (int j = 0; j < 8; ++j) {
       const int kt = j >> 2, r = j & 3;
       const int kk = 16 * kt + 4 * g + r;
-      v[j] = kk < S ? sc[kt][it][r] * scale : -INFINITY;
+      v[j] = kk < S ? sc[kt][it][r] * lscale : -INFINITY;
       m = fmaxf(m, v[j]);
     }
     m = fmaxf(m, __shfl_xor(m, 16));
@@ -483,12 +531,13 @@ __global__ void __launch_bounds__(64) short_attention_f16x3_kernel(const float *
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       _Float16 hh, ll;
-      f16x3_split1(v[j] * inv, hh, ll);
+      f16x3_split1(v[j] * inv * kPScale, hh, ll);
       ph[it][j] = hh;
       pl[it][j] = ll;
     }
   }
   __syncthreads();  // V^T staged
+  const float oscale = a_scale / (kPScale * sv);  // exact power-of-two ratio
 #pragma unroll
   for (int dt = 0; dt < kAttnDh / 16; ++dt) {
     const int d = 16 * dt + c;
@@ -504,7 +553,7 @@ __global__ void __launch_bounds__(64) short_attention_f16x3_kernel(const float *
       f32x4_t o = {0.f, 0.f, 0.f, 0.f};
       o = mfma3(ph[it], pl[it], vh, vl, o);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) oimg[(16 * it + 4 * g + r) * (kAttnDh + 4) + d] = o[r] * a_scale;
+      for (int r = 0; r < 4; ++r) oimg[(16 * it + 4 * g + r) * (kAttnDh + 4) + d] = o[r] * oscale;
     }
   }
   __syncthreads();

@@ -319,3 +319,35 @@ def test_top_k_beyond_fused_lists(stores, corpus, top_k):
                     assert g["id"] == w["id"]
             idx = {i: n for n, i in enumerate(corpus["ids"])}
             assert all(np.array_equal(r["embedding"], corpus["emb"][idx[r["id"]]]) for r in got[:50])
+
+
+@pytest.mark.parametrize("top_k", [10, 3, 0, -4])
+def test_retrieve_batch_device_path_equals_host_path(corpus, monkeypatch, top_k):
+    """The device-resident retrieve_batch (retrieval/device_batch.py) returns the same result dicts
+    as the host path (CM_RETRIEVE_DEVICE=0), field by field, on stores that do not hold the same
+    documents: ids only in the vector store, ids only in the BM25 store, a deleted vector row,
+    documents / metadata present in one store only; plus a whitespace-only query (no BM25 list)."""
+    from classmate_hip.retrieval import BM25Store, GpuVectorStore, HybridRetriever
+    ids, texts, metas, emb = corpus["ids"], corpus["texts"], corpus["metas"], corpus["emb"]
+    vs = GpuVectorStore(persist_dir=None)
+    vs.upsert(ids=ids[:250], documents=[t if i % 7 else "" for i, t in enumerate(texts[:250])],
+              metadatas=[m if i % 5 else {} for i, m in enumerate(metas[:250])], embeddings=emb[:250])
+    vs.delete([ids[3], ids[120]])
+    bm = BM25Store(index_dir=None)
+    bm.upsert_many(ids=ids[40:], texts=texts[40:], metadatas=metas[40:])
+    qtexts = list(corpus["qtexts"]) + ["   "]
+    qvecs = np.concatenate([corpus["qvecs"], corpus["qvecs"][:1]])
+    retr = HybridRetriever(vector_store=vs, bm25_store=bm, embedder=PresetEmbedder(qtexts, qvecs),
+                           k_vector=8, k_bm25=8)
+    from classmate_hip.retrieval import device_batch
+    assert device_batch.applicable(retr, {}, True)
+    got = retr.retrieve_batch(questions=qtexts, top_k=top_k)
+    monkeypatch.setenv("CM_RETRIEVE_DEVICE", "0")
+    want = retr.retrieve_batch(questions=qtexts, top_k=top_k)
+    assert got == want
+    # after a mutation the key map follows the stores
+    monkeypatch.delenv("CM_RETRIEVE_DEVICE")
+    bm.upsert_many(ids=[ids[0]], texts=["an extra lexical document " + texts[1]], metadatas=[{"course": "x"}])
+    got = retr.retrieve_batch(questions=qtexts, top_k=top_k)
+    monkeypatch.setenv("CM_RETRIEVE_DEVICE", "0")
+    assert got == retr.retrieve_batch(questions=qtexts, top_k=top_k)

@@ -63,7 +63,7 @@ def test_dense_grows_in_place_within_10pct():
     assert final["peak_bytes"] <= 1.1 * final["bytes"]
     assert final["bytes"] <= 1.1 * _row_bytes(n)
     assert used <= 1.15 * _row_bytes(n)
-    assert idx.size() == n and idx.live_count() == n
+    assert idx.size == n and idx.live_count() == n
     _check_search(idx, probes)
     # a reserve() past the current size maps the rest without moving anything
     idx.reserve(3 * n)
