@@ -101,12 +101,12 @@ class DenseIndex:
         L.check(L.fn["cm_dense_reserve"](self._h, int(capacity)), "cm_dense_reserve")
 
     def mem_stats(self) -> dict:
-        """Device bytes of the row arrays now / at most at once, and whether growth is in place
-        (cm_dense_mem_stats)."""
-        cur, peak, inplace = C.c_int64(), C.c_int64(), C.c_int32()
-        L.check(L.fn["cm_dense_mem_stats"](self._h, C.byref(cur), C.byref(peak), C.byref(inplace)),
+        """Device bytes of the row arrays now / at most at once, and the growths staged through
+        host memory (cm_dense_mem_stats)."""
+        cur, peak, staged = C.c_int64(), C.c_int64(), C.c_int64()
+        L.check(L.fn["cm_dense_mem_stats"](self._h, C.byref(cur), C.byref(peak), C.byref(staged)),
                 "cm_dense_mem_stats")
-        return {"bytes": cur.value, "peak_bytes": peak.value, "in_place": bool(inplace.value)}
+        return {"bytes": cur.value, "peak_bytes": peak.value, "staged_growths": staged.value}
 
     def upsert(self, vecs: np.ndarray, rows: np.ndarray):
         v = _c(vecs, np.float32)

@@ -76,94 +76,6 @@ struct DevBuf {
   }
 };
 
-// Device array that grows in place: one virtual address range reserved up front
-// (hipMemAddressReserve) and physical chunks mapped at its end as the array grows (hipMemCreate /
-// hipMemMap), so a growth neither copies nor holds an old and a new array at once.  The base
-// pointer never changes.  reserve() fails (and the caller keeps hipMalloc + copy) where the
-// device has no virtual memory management.
-struct VmBuf {
-  char *base = nullptr;
-  size_t reserved = 0, mapped = 0, gran = 0;
-  int dev = -1;
-  std::vector<std::pair<hipMemGenericAllocationHandle_t, size_t>> chunks;
-
-  static hipMemAllocationProp prop_of(int device) {
-    hipMemAllocationProp p{};
-    p.type = hipMemAllocationTypePinned;
-    p.location.type = hipMemLocationTypeDevice;
-    p.location.id = device;
-    return p;
-  }
-  // true when `device` supports VMM and `bytes` of address space were reserved
-  bool reserve(int device, size_t bytes) {
-    int vmm = 0;
-    if (hipDeviceGetAttribute(&vmm, hipDeviceAttributeVirtualMemoryManagementSupported, device) != hipSuccess || !vmm)
-      return false;
-    hipMemAllocationProp p = prop_of(device);
-    size_t g = 0;
-    if (hipMemGetAllocationGranularity(&g, &p, hipMemAllocationGranularityRecommended) != hipSuccess || g == 0)
-      return false;
-    const size_t r = (size_t)round_up((int64_t)std::max<size_t>(bytes, g), (int64_t)g);
-    void *ptr = nullptr;
-    if (hipMemAddressReserve(&ptr, r, g, nullptr, 0) != hipSuccess || !ptr) return false;
-    base = static_cast<char *>(ptr);
-    reserved = r;
-    gran = g;
-    dev = device;
-    return true;
-  }
-  // map physical memory until >= need bytes are backed (slack: 1/16 of the mapped size, so a
-  // sequence of small growths maps O(log) chunks); the new bytes are zeroed on `st`
-  int ensure(size_t need, hipStream_t st) {
-    if (need <= mapped) return CM_OK;
-    if (need > reserved) {
-      set_error("dense: " + std::to_string(need) + " bytes exceed the reserved address range");
-      return CM_ENOMEM;
-    }
-    size_t sz = (size_t)round_up((int64_t)std::max(need - mapped, mapped / 16), (int64_t)gran);
-    sz = std::min(sz, reserved - mapped);
-    hipMemAllocationProp p = prop_of(dev);
-    hipMemGenericAllocationHandle_t hnd{};
-    if (hipMemCreate(&hnd, sz, &p, 0) != hipSuccess) {
-      set_error("dense: out of device memory (hipMemCreate " + std::to_string(sz) + " bytes)");
-      return CM_ENOMEM;
-    }
-    if (hipMemMap(base + mapped, sz, 0, hnd, 0) != hipSuccess) {
-      (void)hipMemRelease(hnd);
-      set_error("dense: hipMemMap failed");
-      return CM_EDEVICE;
-    }
-    hipMemAccessDesc a{};
-    a.location = p.location;
-    a.flags = hipMemAccessFlagsProtReadWrite;
-    // access for the new chunk; ROCm 7.2 refuses some chunk-only ranges (tools/vmm_probe.hip: a
-    // 64 KiB chunk at offset 16 KiB -> invalid argument) but accepts the whole mapped prefix
-    if (hipMemSetAccess(base + mapped, sz, &a, 1) != hipSuccess &&
-        ((void)hipGetLastError(), hipMemSetAccess(base, mapped + sz, &a, 1) != hipSuccess)) {
-      (void)hipMemUnmap(base + mapped, sz);
-      (void)hipMemRelease(hnd);
-      set_error("dense: hipMemSetAccess failed");
-      return CM_EDEVICE;
-    }
-    chunks.emplace_back(hnd, sz);
-    CM_HIP(hipMemsetAsync(base + mapped, 0, sz, st));
-    mapped += sz;
-    return CM_OK;
-  }
-  void release() {
-    size_t off = 0;
-    for (auto &c : chunks) {
-      (void)hipMemUnmap(base + off, c.second);
-      (void)hipMemRelease(c.first);
-      off += c.second;
-    }
-    chunks.clear();
-    if (base) (void)hipMemAddressFree(base, reserved);
-    base = nullptr;
-    reserved = mapped = 0;
-  }
-};
-
 // Orderable encodings so that an unsigned integer compare gives the float order.
 __host__ __device__ inline uint32_t f32_order(float f) {
   uint32_t u = __builtin_bit_cast(uint32_t, f);

@@ -1340,11 +1340,8 @@ struct cm_dense {
   KernelTimer timer;                       // scan-kernel events (cm_dense_timing)
   uint32_t *live = nullptr;
   hipStream_t stream = nullptr;
-  // growth in place (cm_common.h VmBuf): C / invc / live / Xh live in reserved address ranges and
-  // grow by mapping chunks; vm = false -> hipMalloc + prefix copy (devices without VMM)
-  bool vm = false;
-  VmBuf vC, vInvc, vLive, vXh;
-  int64_t mem_cur = 0, mem_peak = 0;       // bytes of the four row arrays (cm_dense_mem_stats)
+  int64_t mem_cur = 0, mem_peak = 0;       // device bytes of the four row arrays (cm_dense_mem_stats)
+  int64_t staged_growths = 0;              // growths that went through host memory
   DevBuf staging, rows_buf, allow_buf, ws, out_buf;
   std::vector<float> host_tmp;
 };
@@ -1455,88 +1452,118 @@ DenseWs dense_ws_layout(const cm_dense *h, const DenseCfg &c, int nq, int k, voi
 // Bytes of the four row arrays at `rows` rows (C fp32, invc, live bits, Xh plane).
 int64_t dense_row_bytes(const cm_dense *h, int64_t rows) { return rows * h->ld * 6 + rows * 4 + rows / 8; }
 
-// Reserve the row arrays' address ranges: enough rows to fill the whole device memory, so the
-// index can grow to any size that fits without ever moving (VmBuf).  false -> hipMalloc path.
-bool dense_vm_reserve(cm_dense *h) {
-  const char *e = getenv("CM_DENSE_VMM");
-  if (e && e[0] == '0') return false;
-  size_t free_b = 0, total_b = 0;
-  if (hipMemGetInfo(&free_b, &total_b) != hipSuccess || total_b == 0) return false;
-  const int64_t max_rows = round_up((int64_t)(total_b / (size_t)(h->ld * 6)) + kStepRows, kStepRows);
-  if (!h->vC.reserve(h->dev, (size_t)max_rows * h->ld * 4) || !h->vXh.reserve(h->dev, (size_t)max_rows * h->ld * 2) ||
-      !h->vInvc.reserve(h->dev, (size_t)max_rows * 4) || !h->vLive.reserve(h->dev, (size_t)max_rows / 8)) {
-    h->vC.release();
-    h->vXh.release();
-    h->vInvc.release();
-    h->vLive.release();
-    return false;
+// Growth (dense_grow).  The arrays are reallocated at max(need, 1.5 x rows_alloc) rows.  A store
+// holding more than kStageBytes moves through host memory: its written rows' fp32 data, norms and
+// live bits are copied to the host, the old arrays freed, the new ones allocated and the rows copied
+// back; the f16 plane is recomputed on the device from them (dense_replane_kernel, bit-identical
+// to the upsert's).  The device then never holds the old and the new arrays at once -- a store
+// growing by upserts to hundreds of GB of HBM peaks at its final size, not 2.5 x it.  Smaller
+// stores copy device to device (faster; their double residency is at most 2 x kStageBytes).
+constexpr int64_t kStageBytes = 1ll << 30;
+
+__global__ void __launch_bounds__(256) dense_replane_kernel(const float *__restrict__ C, const float *__restrict__ invc,
+                                                            int64_t n, int dim, int ld, _Float16 *__restrict__ Xh) {
+  const int64_t r = blockIdx.x;
+  if (r >= n) return;
+  const float inv = invc[r];
+  for (int c = threadIdx.x; c < ld; c += 256) {
+    const float xn = (c < dim ? C[r * ld + c] : 0.f) * inv;  // == dense_scatter_kernel's
+    Xh[plane_off(r, c, ld)] = (_Float16)xn;
   }
-  h->C = reinterpret_cast<float *>(h->vC.base);
-  h->Xh = reinterpret_cast<_Float16 *>(h->vXh.base);
-  h->invc = reinterpret_cast<float *>(h->vInvc.base);
-  h->live = reinterpret_cast<uint32_t *>(h->vLive.base);
-  return true;
+}
+
+int dense_alloc_rows(cm_dense *h, int64_t cap, float **C2, float **ic2, uint32_t **lv2, _Float16 **xh2) {
+  *C2 = nullptr, *ic2 = nullptr, *lv2 = nullptr, *xh2 = nullptr;
+  const size_t nel = (size_t)cap * h->ld;
+  if (hipMalloc(C2, nel * 4) != hipSuccess || hipMalloc(ic2, (size_t)cap * 4) != hipSuccess ||
+      hipMalloc(lv2, (size_t)cap / 8) != hipSuccess || hipMalloc(xh2, nel * 2) != hipSuccess) {
+    for (void *p : {(void *)*C2, (void *)*ic2, (void *)*lv2, (void *)*xh2})
+      if (p) (void)hipFree(p);
+    *C2 = nullptr, *ic2 = nullptr, *lv2 = nullptr, *xh2 = nullptr;
+    CM_FAIL(CM_ENOMEM, "dense: out of device memory");
+  }
+  CM_HIP(hipMemsetAsync(*C2, 0, nel * 4, h->stream));
+  CM_HIP(hipMemsetAsync(*ic2, 0, (size_t)cap * 4, h->stream));
+  CM_HIP(hipMemsetAsync(*lv2, 0, (size_t)cap / 8, h->stream));
+  CM_HIP(hipMemsetAsync(*xh2, 0, nel * 2, h->stream));
+  return CM_OK;
+}
+
+void dense_free_rows(cm_dense *h) {
+  for (void *p : {(void *)h->C, (void *)h->invc, (void *)h->live, (void *)h->Xh})
+    if (p) (void)hipFree(p);
+  h->C = nullptr, h->invc = nullptr, h->live = nullptr, h->Xh = nullptr;
 }
 
 int dense_grow(cm_dense *h, int64_t need_rows) {
   if (need_rows <= h->rows_alloc) return CM_OK;
-  if (h->vm) {
-    // in place: map (zeroed) memory behind the arrays' fixed bases; rows_alloc stays a multiple of
-    // kStepRows, the rows of the mapping slack become usable at the next growth without a map
-    const int64_t cap = round_up(std::max<int64_t>(need_rows, kStepRows), kStepRows);
-    int rc;
-    if ((rc = h->vC.ensure((size_t)cap * h->ld * 4, h->stream)) || (rc = h->vXh.ensure((size_t)cap * h->ld * 2, h->stream)) ||
-        (rc = h->vInvc.ensure((size_t)cap * 4, h->stream)) || (rc = h->vLive.ensure((size_t)cap / 8, h->stream))) {
-      if (rc != CM_EDEVICE) return rc;  // out of memory: the copy path would need even more
-      // the mapping itself failed: move to hipMalloc arrays (the copy below reads the mapped rows)
-    } else {
-      CM_HIP(hipStreamSynchronize(h->stream));
-      h->rows_alloc = cap;
-      h->mem_cur = (int64_t)(h->vC.mapped + h->vXh.mapped + h->vInvc.mapped + h->vLive.mapped);
-      h->mem_peak = std::max(h->mem_peak, h->mem_cur);
-      return CM_OK;
-    }
-  }
   int64_t cap = std::max<int64_t>(need_rows, h->rows_alloc + h->rows_alloc / 2);
   cap = round_up(std::max<int64_t>(cap, kStepRows), kStepRows);
-  float *C2 = nullptr, *ic2 = nullptr;
-  uint32_t *lv2 = nullptr;
-  _Float16 *xh2 = nullptr;
-  const size_t nel = (size_t)cap * h->ld;
-  if (hipMalloc(&C2, nel * 4) != hipSuccess || hipMalloc(&ic2, (size_t)cap * 4) != hipSuccess ||
-      hipMalloc(&lv2, (size_t)cap / 8) != hipSuccess || hipMalloc(&xh2, nel * 2) != hipSuccess) {
-    for (void *p : {(void *)C2, (void *)ic2, (void *)lv2, (void *)xh2})
-      if (p) (void)hipFree(p);
-    CM_FAIL(CM_ENOMEM, "dense: out of device memory");
+  const int64_t keep = std::min<int64_t>(round_up(h->size, kStepRows), h->rows_alloc);  // rows holding data
+  float *C2, *ic2;
+  uint32_t *lv2;
+  _Float16 *xh2;
+  int rc;
+  if (keep > 0 && h->mem_cur > kStageBytes) {
+    // host-staged: fp32 rows + norms + live bits out, old arrays freed, new ones in
+    const size_t cb = (size_t)keep * h->ld * 4, ib = (size_t)keep * 4, lb = (size_t)keep / 8;
+    std::vector<char> host;
+    try {
+      host.resize(cb + ib + lb);
+    } catch (const std::bad_alloc &) {
+      CM_FAIL(CM_ENOMEM, "dense: no host memory to stage the growth");
+    }
+    CM_HIP(hipStreamSynchronize(h->stream));
+    CM_HIP(hipMemcpy(host.data(), h->C, cb, hipMemcpyDeviceToHost));
+    CM_HIP(hipMemcpy(host.data() + cb, h->invc, ib, hipMemcpyDeviceToHost));
+    CM_HIP(hipMemcpy(host.data() + cb + ib, h->live, lb, hipMemcpyDeviceToHost));
+    dense_free_rows(h);
+    h->rows_alloc = 0;
+    h->mem_cur = 0;
+    if ((rc = dense_alloc_rows(h, cap, &C2, &ic2, &lv2, &xh2))) {
+      // put the old rows back (the size just freed, so this allocation fits where the larger failed)
+      cap = keep;
+      if (dense_alloc_rows(h, cap, &C2, &ic2, &lv2, &xh2) != CM_OK) {
+        // nothing fits any more: an empty minimal store (never a handle without arrays)
+        if (dense_alloc_rows(h, kStepRows, &C2, &ic2, &lv2, &xh2) != CM_OK)
+          CM_FAIL(CM_ENOMEM, "dense: out of device memory; the handle is unusable");
+        CM_HIP(hipStreamSynchronize(h->stream));
+        h->C = C2, h->invc = ic2, h->live = lv2, h->Xh = xh2;
+        h->rows_alloc = kStepRows;
+        h->size = 0;
+        h->mem_cur = dense_row_bytes(h, kStepRows);
+        CM_FAIL(CM_ENOMEM, "dense: out of device memory while growing; the store was emptied");
+      }
+      rc = CM_ENOMEM;
+    }
+    CM_HIP(hipMemcpyAsync(C2, host.data(), cb, hipMemcpyHostToDevice, h->stream));
+    CM_HIP(hipMemcpyAsync(ic2, host.data() + cb, ib, hipMemcpyHostToDevice, h->stream));
+    CM_HIP(hipMemcpyAsync(lv2, host.data() + cb + ib, lb, hipMemcpyHostToDevice, h->stream));
+    hipLaunchKernelGGL(dense_replane_kernel, dim3((unsigned)keep), dim3(256), 0, h->stream, C2, ic2, keep, h->dim,
+                       h->ld, xh2);
+    CM_HIP(hipGetLastError());
+    CM_HIP(hipStreamSynchronize(h->stream));
+    ++h->staged_growths;
+    h->C = C2, h->invc = ic2, h->live = lv2, h->Xh = xh2;
+    h->rows_alloc = cap;
+    h->mem_cur = dense_row_bytes(h, cap);
+    h->mem_peak = std::max(h->mem_peak, h->mem_cur);
+    if (rc) CM_FAIL(CM_ENOMEM, "dense: out of device memory");
+    return CM_OK;
   }
+  if ((rc = dense_alloc_rows(h, cap, &C2, &ic2, &lv2, &xh2))) return rc;
   h->mem_peak = std::max(h->mem_peak, h->mem_cur + dense_row_bytes(h, cap));  // old + new at once
-  CM_HIP(hipMemsetAsync(C2, 0, nel * 4, h->stream));
-  CM_HIP(hipMemsetAsync(ic2, 0, (size_t)cap * 4, h->stream));
-  CM_HIP(hipMemsetAsync(lv2, 0, (size_t)cap / 8, h->stream));
-  CM_HIP(hipMemsetAsync(xh2, 0, nel * 2, h->stream));
-  if (h->rows_alloc) {
-    // the plane is tile-major (64-row tiles, rows_alloc a multiple of 128): a prefix copy keeps it
-    const size_t old = (size_t)h->rows_alloc * h->ld;
+  if (keep > 0) {
+    // the plane is tile-major (64-row tiles, keep a multiple of 128): a prefix copy keeps it
+    const size_t old = (size_t)keep * h->ld;
     CM_HIP(hipMemcpyAsync(C2, h->C, old * 4, hipMemcpyDeviceToDevice, h->stream));
-    CM_HIP(hipMemcpyAsync(ic2, h->invc, (size_t)h->rows_alloc * 4, hipMemcpyDeviceToDevice, h->stream));
-    CM_HIP(hipMemcpyAsync(lv2, h->live, (size_t)h->rows_alloc / 8, hipMemcpyDeviceToDevice, h->stream));
+    CM_HIP(hipMemcpyAsync(ic2, h->invc, (size_t)keep * 4, hipMemcpyDeviceToDevice, h->stream));
+    CM_HIP(hipMemcpyAsync(lv2, h->live, (size_t)keep / 8, hipMemcpyDeviceToDevice, h->stream));
     CM_HIP(hipMemcpyAsync(xh2, h->Xh, old * 2, hipMemcpyDeviceToDevice, h->stream));
   }
   CM_HIP(hipStreamSynchronize(h->stream));
-  if (h->vm) {  // leaving the reserved ranges for good
-    h->vC.release();
-    h->vXh.release();
-    h->vInvc.release();
-    h->vLive.release();
-    h->vm = false;
-  } else {
-    for (void *p : {(void *)h->C, (void *)h->invc, (void *)h->live, (void *)h->Xh})
-      if (p) (void)hipFree(p);
-  }
-  h->C = C2;
-  h->invc = ic2;
-  h->live = lv2;
-  h->Xh = xh2;
+  dense_free_rows(h);
+  h->C = C2, h->invc = ic2, h->live = lv2, h->Xh = xh2;
   h->rows_alloc = cap;
   h->mem_cur = dense_row_bytes(h, cap);
   return CM_OK;
@@ -1856,7 +1883,6 @@ int cm_dense_create(int device, int32_t dim, int64_t capacity, cm_dense **out) {
     cm_dense_destroy(h);
     CM_FAIL(CM_ENOMEM, "dense: out of device memory");
   }
-  h->vm = dense_vm_reserve(h);
   int rc = dense_grow(h, std::max<int64_t>(capacity, kStepRows));
   if (rc) {
     cm_dense_destroy(h);
@@ -1870,17 +1896,7 @@ void cm_dense_destroy(cm_dense *h) {
   if (!h) return;
   DeviceGuard dg(h->dev);
   if (h->stream) (void)hipStreamSynchronize(h->stream);
-  if (h->vm) {
-    h->vC.release();
-    h->vXh.release();
-    h->vInvc.release();
-    h->vLive.release();
-  } else {
-    if (h->C) (void)hipFree(h->C);
-    if (h->invc) (void)hipFree(h->invc);
-    if (h->live) (void)hipFree(h->live);
-    if (h->Xh) (void)hipFree(h->Xh);
-  }
+  dense_free_rows(h);
   if (h->rnorm) (void)hipFree(h->rnorm);
   h->timer.release();
   h->staging.release();
@@ -1979,11 +1995,11 @@ int cm_dense_reset(cm_dense *h) {
   return CM_OK;
 }
 
-int cm_dense_mem_stats(cm_dense *h, int64_t *cur_bytes, int64_t *peak_bytes, int32_t *in_place) {
+int cm_dense_mem_stats(cm_dense *h, int64_t *cur_bytes, int64_t *peak_bytes, int64_t *staged_growths) {
   if (!h) CM_FAIL(CM_EINVAL, "null handle");
   if (cur_bytes) *cur_bytes = h->mem_cur;
   if (peak_bytes) *peak_bytes = h->mem_peak;
-  if (in_place) *in_place = h->vm ? 1 : 0;
+  if (staged_growths) *staged_growths = h->staged_growths;
   return CM_OK;
 }
 

@@ -71,10 +71,10 @@ int cm_dense_create(int device, int32_t dim, int64_t capacity, cm_dense **out);
 void cm_dense_destroy(cm_dense *h);
 int cm_dense_reserve(cm_dense *h, int64_t capacity);
 /* Device bytes of the row arrays (fp32 rows, norms, live bits, f16 plane): now and the most ever
- * held at once (a growth by hipMalloc + copy holds the old and the new arrays together; in-place
- * growth maps memory behind fixed address ranges and never does).  in_place = 1 when the store
- * grows in place.  Not a reference interface (capacity planning for 288 GB of HBM). */
-int cm_dense_mem_stats(cm_dense *h, int64_t *cur_bytes, int64_t *peak_bytes, int32_t *in_place);
+ * held at once, and how many growths went through host memory.  A store above 1 GiB grows by
+ * staging its rows through the host (the device never holds the old and the new arrays together);
+ * smaller ones copy device to device.  Not a reference interface (capacity planning for 288 GB). */
+int cm_dense_mem_stats(cm_dense *h, int64_t *cur_bytes, int64_t *peak_bytes, int64_t *staged_growths);
 /* ChromaVectorStore.upsert (vector_chroma.py:168-200): write n fp32 rows
  * (host, n x dim row-major) at the given row indices, marking them live.
  * Rows beyond the current size grow the store. */

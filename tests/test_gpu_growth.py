@@ -1,13 +1,13 @@
 """Ingest growth without double residency (VERDICT r2 "next" 8).
 
 ChromaVectorStore.upsert (rag/retrieval/vector_chroma.py:168-200) grows the collection one batch at
-a time.  The HBM store grows in place: its row arrays sit in reserved address ranges and a growth
-maps more memory behind them (cm_common.h VmBuf), so the footprint never exceeds the final size by
-more than the mapping slack, and the rows written earlier never move.  The hipMalloc + copy path
-(CM_DENSE_VMM=0, kept for devices without virtual memory management) holds old + new at once.
+a time.  Above 1 GiB the HBM store grows through host memory (cm_dense.hip dense_grow): its rows go
+to the host, the old arrays are freed, the new ones allocated and the rows copied back with the f16
+plane recomputed on the device -- so the device never holds the old and the new arrays together
+and the peak footprint is the final allocation.  Smaller stores copy device to device.
+(An in-place growth through reserved address ranges, hipMemAddressReserve + hipMemMap, was tried
+first and dropped: hipMemSetAccess rejects some chunk ranges on this ROCm, tools/vmm_probe.hip.)
 """
-import os
-
 import numpy as np
 import pytest
 
@@ -46,44 +46,47 @@ def _check_search(index, probes):
     assert np.abs(dist[:, 0]).max() < 1e-5
 
 
-def test_dense_grows_in_place_within_10pct():
+def test_dense_growth_peak_is_final_size():
     import torch
     from classmate_hip import engine
-    os.environ.pop("CM_DENSE_VMM", None)
     nb, per = 16, 125_000                                 # 0 -> 2M rows (9.2 GB) in 16 upserts
     idx = engine.DenseIndex(D, capacity=0)
-    assert idx.mem_stats()["in_place"], "MI355X supports virtual memory management"
-    free0 = torch.cuda.mem_get_info()[0]
     stats, probes = _grow(idx, nb, per, seed=3)
     final = stats[-1]
-    used = free0 - torch.cuda.mem_get_info()[0]
     n = nb * per
-    print(f"\nin place: {final['bytes'] / 1e9:.2f} GB mapped for {n} rows ({_row_bytes(n) / 1e9:.2f} GB), "
-          f"peak {final['peak_bytes'] / 1e9:.2f} GB, device memory used {used / 1e9:.2f} GB")
+    print(f"\nstaged growth: {final['bytes'] / 1e9:.2f} GB for {n} rows ({_row_bytes(n) / 1e9:.2f} GB of rows), "
+          f"peak {final['peak_bytes'] / 1e9:.2f} GB, {final['staged_growths']} growths through the host")
+    assert final["staged_growths"] >= 1
     assert final["peak_bytes"] <= 1.1 * final["bytes"]
-    assert final["bytes"] <= 1.1 * _row_bytes(n)
-    assert used <= 1.15 * _row_bytes(n)
+    assert final["bytes"] <= 1.6 * _row_bytes(n)              # 1.5x growth steps
     assert idx.size == n and idx.live_count() == n
     _check_search(idx, probes)
-    # a reserve() past the current size maps the rest without moving anything
+    # searches after a staged growth: the recomputed f16 plane equals the upsert-written one
+    # (K1c at B = 256 and K1s at B = 16 on the coarse plane, ids identical to the fp32 path)
+    g = torch.Generator(device="cuda").manual_seed(9)
+    q = torch.randn(256, D, device="cuda", generator=g)
+    for nq in (256, 16):
+        d1, r1 = idx.search_dev(q[:nq].contiguous(), 10)
+        idx.set_path(1)
+        d2, r2 = idx.search_dev(q[:nq].contiguous(), 10)
+        idx.set_path(0)
+        assert float((d1 - d2).abs().max()) < 1e-5          # a wrong plane would lose true neighbours
+        assert float((r1 == r2).float().mean()) > 0.99
+    # reserve() past the size: one more staged growth, nothing lost
     idx.reserve(3 * n)
-    assert idx.mem_stats()["bytes"] >= _row_bytes(3 * n)
+    st = idx.mem_stats()
+    assert st["peak_bytes"] <= 1.1 * st["bytes"] and st["bytes"] >= _row_bytes(3 * n)
     _check_search(idx, probes)
     idx.close()
 
 
-def test_dense_copy_growth_path_same_results():
-    """CM_DENSE_VMM=0: the hipMalloc + copy growth (1.5x) gives the same rows and search results;
-    its recorded peak holds the old and the new arrays together."""
+def test_dense_small_store_copies_on_device():
+    """Below 1 GiB the growth copies device to device (old + new together, at most ~2 GiB)."""
     from classmate_hip import engine
-    os.environ["CM_DENSE_VMM"] = "0"
-    try:
-        idx = engine.DenseIndex(D, capacity=0)
-    finally:
-        os.environ.pop("CM_DENSE_VMM", None)
-    assert not idx.mem_stats()["in_place"]
-    stats, probes = _grow(idx, 6, 50_000, seed=4)
+    idx = engine.DenseIndex(D, capacity=0)
+    stats, probes = _grow(idx, 4, 50_000, seed=4)
     final = stats[-1]
-    assert final["peak_bytes"] >= 1.5 * final["bytes"]              # old + new coexisted (1.5x steps)
+    assert final["staged_growths"] == 0
+    assert final["peak_bytes"] >= 1.5 * final["bytes"]              # old + new coexisted
     _check_search(idx, probes)
     idx.close()
