@@ -717,10 +717,23 @@ def run_e2e(args, rank, ws, dev):
     p = 1.0 / np.arange(1, V + 1) ** args.zipf
     cdf = np.cumsum(p)
     cdf /= cdf[-1]
-    words = np.minimum(np.searchsorted(cdf, rng.random(N * args.e2e_words)), V - 1).reshape(N, args.e2e_words)
-    alpha = np.array(list("abcdefghijklmnopqrstuvwxyz"))
-    vocab = ["zq" + "".join(alpha[(w // 26 ** i) % 26] for i in range(4)) for w in range(V)]  # letters only
-    texts = [" ".join(vocab[w] for w in row) for row in words]
+    W = args.e2e_words
+    # word w = "zq" + 4 letters (letters only, as the BM25 tokenizer keeps letters only); texts are
+    # cut from one byte image of N x W words (7 bytes with the separator) instead of a join per word
+    alpha = np.frombuffer(b"abcdefghijklmnopqrstuvwxyz", np.uint8)
+    wv = np.arange(V)
+    vb = np.empty((V, 7), np.uint8)
+    vb[:, 0], vb[:, 1], vb[:, 6] = ord("z"), ord("q"), ord(" ")
+    for i in range(4):
+        vb[:, 2 + i] = alpha[(wv // 26 ** i) % 26]
+    texts = []
+    for c0 in range(0, N, 1 << 20):
+        c1 = min(N, c0 + (1 << 20))
+        words = np.minimum(np.searchsorted(cdf, rng.random((c1 - c0) * W)), V - 1).astype(np.int32)
+        blob = vb[words].tobytes()
+        L = 7 * W
+        texts.extend(blob[i * L:(i + 1) * L - 1].decode("ascii") for i in range(c1 - c0))
+        del words, blob
     ids = [f"c{i}" for i in range(N)]
     metas = [{"course": f"C{i % 16}", "week": int(i % 12), "language": "en"} for i in range(N)]
     log(f"e2e corpus: {N} chunks x {args.e2e_words} words ({time.perf_counter() - t_setup:.1f}s)")

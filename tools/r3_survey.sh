@@ -11,3 +11,5 @@ VARIANTS=" " bash tools/k2_kprof.sh > gpurun_out/r3s_bm25.txt 2>&1 || { tail -20
 cat gpurun_out/r3s_bm25.txt
 ONLY="bm25_B256 bm25b_B256" ROUND=r03 bash tools/pmc_traffic.sh > gpurun_out/r3s_pmc.txt 2>&1 || { tail -20 gpurun_out/r3s_pmc.txt; exit 1; }
 cat gpurun_out/pmc_traffic_r03.txt
+DOCS=1000000 bash tools/mgpu_rehearsal.sh > gpurun_out/r3s_mgpu.txt 2>&1 || { tail -20 gpurun_out/r3s_mgpu.txt; exit 1; }
+cat gpurun_out/r3s_mgpu.txt
