@@ -280,6 +280,8 @@ def main():
             return q_local
         return parallel.all_gather_into(qfull, q_local)
 
+    last_lists = {}      # the last step's merged lists (recall diagnostics)
+
     def step(record=False):
         e = {n: torch.cuda.Event(enable_timing=True) for n in ("e0", "e1", "d0", "d1", "b0", "b1")} if record else None
         if bm25 is not None and not args.bm25_after_e5:
@@ -314,6 +316,7 @@ def main():
             order = engine.mmr_dev(q[blk].contiguous(), vecs, K, 0.5, out=obuf)
         if record:
             ev.append(e)
+        last_lists["pool"] = (rg, dm, brg, bsm, order)
         # MMR-ordered vector list + list counts in one device pass, then the fused merge
         vk, vd, vn, bn = engine.rrf_pool_prep_dev(rg[blk].contiguous(), dm[blk].contiguous(), order,
                                                   brg[blk].contiguous(), out=pbuf)
@@ -426,7 +429,8 @@ def main():
     }
     if args.cpu_baseline and args.mode == "hybrid":
         q_emb = ((qfull if ws > 1 else e5["qbuf"]) if use_e5 else qfix)   # the last step's embeddings
-        cpu, recall = cpu_baseline_and_recall(args, dense, bm25, res, q_terms, q_emb, rank, ws, row0, N)
+        cpu, recall = cpu_baseline_and_recall(args, dense, bm25, res, q_terms, q_emb, rank, ws, row0, N,
+                                              last_lists.get("pool"))
         out["cpu_baseline"] = cpu
         out["recall_at_10"] = recall
     else:
@@ -577,7 +581,7 @@ def _pmc_traffic(args, which):
 
 
 # ---------------------------------------------------------------------------
-def cpu_baseline_and_recall(args, dense, bm25, res, q_terms, q_dev, rank, ws, row0, N):
+def cpu_baseline_and_recall(args, dense, bm25, res, q_terms, q_dev, rank, ws, row0, N, gpu_lists=None):
     """Time the CPU oracle on a bounded sample of the step's queries (its query embeddings) over
     every rank's shard (each rank scans its own, in parallel), merge the per-shard exact lists
     (a merge of exact per-shard top lists is the exact global list), run MMR + RRF on the merged
@@ -677,6 +681,17 @@ def cpu_baseline_and_recall(args, dense, bm25, res, q_terms, q_dev, rank, ws, ro
     t_fuse = time.perf_counter() - t2
     recall = float(np.mean([len(set(cpu_keys[i]) & set(int(x) for x in gpu_keys[i] if x >= 0)) / K
                             for i in range(Qc)]))
+    shown = 0
+    for i in range(Qc):          # the first mismatching queries, for diagnosis
+        g = [int(x) for x in gpu_keys[i] if x >= 0]
+        if g != cpu_keys[i] and shown < 3:
+            shown += 1
+            log(f"recall mismatch q{i}: gpu {g} cpu {cpu_keys[i]}; pool rows {dense_rows[i][:P].tolist()} "
+                f"dist {[round(float(x), 7) for x in dense_dist[i][:P]]}; bm25 {BR[i].tolist()} {BS[i].tolist()}")
+            if gpu_lists is not None:
+                rg, dm, brg, bsm, order = (t.cpu().numpy() for t in gpu_lists)
+                log(f"  gpu lists q{i}: pool rows {rg[i].tolist()} dist {[round(float(x), 7) for x in dm[i]]}; "
+                    f"bm25 {brg[i].tolist()} {bsm[i].tolist()}" + (f"; mmr order {order[i].tolist()}" if ws == 1 else ""))
     shard_s = [x["t_dense"] + x["t_bm25"] for x in allv]
     total = sum(shard_s) + t_fuse
     cpu = dict(value=Qc / total, unit="queries/s", cores=int(threads), kind="port",
@@ -746,13 +761,19 @@ def run_e2e(args, rank, ws, dev):
     for i in range(0, N, step):
         vs.upsert(ids=ids[i:i + step], documents=texts[i:i + step], metadatas=metas[i:i + step],
                   embeddings=emb[i:i + step])
+        if (i // step) % 8 == 7:
+            log(f"vector store: {i + step} chunks ({time.perf_counter() - t_setup:.1f}s)")
     del emb
     bm = BM25Store(index_dir=None, device=dev.index)
-    bm.upsert_many(ids=ids, texts=texts, metadatas=metas)
+    step = 1 << 20
+    for i in range(0, N, step):       # one upsert_many per 1M chunks (progress lines; same store)
+        bm.upsert_many(ids=ids[i:i + step], texts=texts[i:i + step], metadatas=metas[i:i + step])
+        log(f"bm25 store: {min(N, i + step)} chunks tokenized ({time.perf_counter() - t_setup:.1f}s)")
     embedder = E5MultilingualEmbedder.random_init(seed=0, device=str(dev), num_layers=args.e5_layers)
     retr = HybridRetriever(vector_store=vs, bm25_store=bm, embedder=embedder)
     qsrc = rng.integers(0, N, B * (args.steps + args.warmup + 1))
     qs = [" ".join(texts[i].split()[j:j + 6]) for i, j in zip(qsrc, rng.integers(0, args.e2e_words - 6, qsrc.size))]
+    log("first retrieve_batch: builds the BM25 device index")
     retr.retrieve_batch(questions=qs[:B], top_k=K)     # builds the BM25 index, first graph/kernels
     torch.cuda.synchronize()
     log(f"e2e stores ready: {vs.count()} vectors, {len(bm._id_list)} BM25 docs ({time.perf_counter() - t_setup:.1f}s)")

@@ -49,6 +49,8 @@
 #include "cm_common.h"
 
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 
 namespace cm {
 
@@ -357,6 +359,16 @@ struct TileCfg {
 // the 96 x 192 tile divides M = 6144 (the 256 x 24 query batch) x N in {768, 2304, 3072} into
 // exact multiples of 256 tiles; 128 x 128, 64 x 128 and 64 x 64 cover the other shapes.
 static TileCfg pick_tile(int64_t M, int N, int n_cu) {
+  // CM_K10_TILE=RxC (fragment blocks, e.g. 12x12) forces a tile for A/B timing
+  static const TileCfg forced = [] {
+    TileCfg f{0, 0};
+    if (const char *e = getenv("CM_K10_TILE")) (void)sscanf(e, "%dx%d", &f.bmb, &f.bnb);
+    return f;
+  }();
+  if (forced.bmb && N % (16 * forced.bnb) == 0) return forced;
+  // FFN-up (N = 3072): 192 x 192 measured 98.3 -> 90.5 us at M = 6144 (tools/k10_tiles.sh); the
+  // other E5 shapes are faster at 96 x 192 (qkv 67 vs 75 us, o 25 vs 34, down 73 vs 95)
+  if (N >= 3072 && N % 192 == 0 && M >= 192 * (int64_t)n_cu / 2) return TileCfg{12, 12};
   const TileCfg cands[4] = {{6, 12}, {8, 8}, {4, 8}, {4, 4}};
   TileCfg best = {0, 0};
   double best_cost = 0;
@@ -451,6 +463,10 @@ extern "C" int cm_linear_f16x3(const void *a_planes, int64_t M, int32_t K, const
   _Float16 *Cp = (_Float16 *)c_planes;
   hipStream_t st = (hipStream_t)stream;
   // waves per workgroup: two or three per SIMD, so one wave's MFMAs cover another's waits
+  if (t.bmb == 12 && t.bnb == 12)  // 192 x 192: half the operand bytes per MFMA of 96 x 192 (L2 -> LDS bound)
+    return launch_tile<12, 12, 3, 8>(A, M, K, W, bias_dev, out_scale, N, epilogue, c_dev, next_scale, Cp, g_n_cu, st);
+  if (t.bmb == 8 && t.bnb == 16)
+    return launch_tile<8, 16, 3, 8>(A, M, K, W, bias_dev, out_scale, N, epilogue, c_dev, next_scale, Cp, g_n_cu, st);
   if (t.bmb == 6)
     return launch_tile<6, 12, K10_W6 == 8 ? 3 : 4, K10_W6>(A, M, K, W, bias_dev, out_scale, N, epilogue, c_dev,
                                                            next_scale, Cp, g_n_cu, st);
