@@ -316,7 +316,7 @@ def main():
             order = engine.mmr_dev(q[blk].contiguous(), vecs, K, 0.5, out=obuf)
         if record:
             ev.append(e)
-        last_lists["pool"] = (rg, dm, brg, bsm, order)
+        last_lists["pool"] = (rg, dm, brg, bsm, order, vecs)
         # MMR-ordered vector list + list counts in one device pass, then the fused merge
         vk, vd, vn, bn = engine.rrf_pool_prep_dev(rg[blk].contiguous(), dm[blk].contiguous(), order,
                                                   brg[blk].contiguous(), out=pbuf)
@@ -689,9 +689,14 @@ def cpu_baseline_and_recall(args, dense, bm25, res, q_terms, q_dev, rank, ws, ro
             log(f"recall mismatch q{i}: gpu {g} cpu {cpu_keys[i]}; pool rows {dense_rows[i][:P].tolist()} "
                 f"dist {[round(float(x), 7) for x in dense_dist[i][:P]]}; bm25 {BR[i].tolist()} {BS[i].tolist()}")
             if gpu_lists is not None:
-                rg, dm, brg, bsm, order = (t.cpu().numpy() for t in gpu_lists)
+                rg, dm, brg, bsm, order, gv = (t.cpu().numpy() for t in gpu_lists)
                 log(f"  gpu lists q{i}: pool rows {rg[i].tolist()} dist {[round(float(x), 7) for x in dm[i]]}; "
-                    f"bm25 {brg[i].tolist()} {bsm[i].tolist()}" + (f"; mmr order {order[i].tolist()}" if ws == 1 else ""))
+                    f"bm25 {brg[i].tolist()} {bsm[i].tolist()}")
+                if i < order.shape[0]:   # rank 0's query block (rows of its MMR launch)
+                    o_cpu = orc.mmr_order(qh[i], pool_v[i], list(range(P)), K, 0.5)
+                    o_gv = orc.mmr_order(qh[i], gv[i], list(range(P)), K, 0.5)
+                    log(f"  mmr q{i}: gpu {order[i].tolist()} oracle {o_cpu} oracle-on-gpu-pool {o_gv}; "
+                        f"max |gpu pool - oracle pool| {float(np.abs(gv[i] - pool_v[i]).max()):.3e}")
     shard_s = [x["t_dense"] + x["t_bm25"] for x in allv]
     total = sum(shard_s) + t_fuse
     cpu = dict(value=Qc / total, unit="queries/s", cores=int(threads), kind="port",
