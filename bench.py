@@ -348,6 +348,10 @@ def main():
     if bm25 is not None:
         bm25.timing(True)
     elapsed, res = timed(args.steps)
+    # the recall check compares `res` with the oracle on the SAME step's inputs: keep this run's
+    # query embeddings and merged lists before the side legs reuse the buffers (qfull at N > 1)
+    q_main = ((qfull if ws > 1 else e5["qbuf"]) if use_e5 else qfix).clone()
+    lists_main = tuple(t.clone() for t in last_lists["pool"]) if "pool" in last_lists else None
     mean_ms = lambda a, b: sum(x[a].elapsed_time(x[b]) for x in ev) / len(ev)   # noqa: E731
     search_ms = mean_ms("d0", "d1")
     bsearch_ms = mean_ms("b0", "b1") if bm25 is not None else None
@@ -428,9 +432,8 @@ def main():
         "env": {e: os.environ[e] for e in KNOB_ENV if e in os.environ},
     }
     if args.cpu_baseline and args.mode == "hybrid":
-        q_emb = ((qfull if ws > 1 else e5["qbuf"]) if use_e5 else qfix)   # the last step's embeddings
-        cpu, recall = cpu_baseline_and_recall(args, dense, bm25, res, q_terms, q_emb, rank, ws, row0, N,
-                                              last_lists.get("pool"))
+        cpu, recall = cpu_baseline_and_recall(args, dense, bm25, res, q_terms, q_main, rank, ws, row0, N,
+                                              lists_main)
         out["cpu_baseline"] = cpu
         out["recall_at_10"] = recall
     else:
