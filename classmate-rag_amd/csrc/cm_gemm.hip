@@ -71,10 +71,7 @@ __device__ __forceinline__ h16x8 as_h8(i32x4 v) { return __builtin_bit_cast(h16x
 #ifndef K10_ABL
 #define K10_ABL 0
 #endif
-// 1: one barrier per two k-steps (4-stage ring, two stages in flight) instead of one per k-step
-#ifndef K10_PAIR
-#define K10_PAIR 0
-#endif
+
 
 __device__ inline float gelu_erf(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
 
@@ -289,11 +286,7 @@ __global__ void __launch_bounds__(64 * NW)
     K10_ISSUE(p);
     K10_ADVANCE();
   }
-  constexpr bool PAIR = K10_PAIR && S == 4;
-  if constexpr (PAIR)
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PCS * (S - 2)) : "memory");  // stages 0 and 1 landed
-  else
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PCS * (S - 1)) : "memory");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PCS * (S - 1)) : "memory");
   __builtin_amdgcn_s_barrier();
   K10_READ(0, ah0, al0, bh0, bl0);
 
@@ -325,33 +318,8 @@ __global__ void __launch_bounds__(64 * NW)
   for (int ti = 0; ti < my_n; ++ti) {
     for (int kt = 0; kt < nk; kt += 2) {              // nk is even (K % 64 == 0)
       const int g = ti * nk + kt;
-      if constexpr (PAIR) {
-      // Two k-steps per barrier (S = 4): stages g, g+1 were published by the previous barrier and
-      // g+2, g+3 are in flight.  All MFMAs of step g (its fragments are in set 0) with step g+1's
-      // fragment reads; the first H1 row tiles of step g+1; then wait for g+2, g+3 (the only DMAs
-      // in flight) and for every read of slots g, g+1; one barrier publishes g+2, g+3 and frees
-      // those slots; stages g+4, g+5 are issued into them, step g+2's fragments read into set 0,
-      // and step g+1's remaining MFMAs run.
-      {
-        const int s1 = (g + 1) % S, s2 = (g + 2) % S;
-        K10_READ(s1, ah1, al1, bh1, bl1);
-        K10_MFMA(0, WMT, ah0, al0, bh0, bl0)
-        K10_MFMA(0, H1, ah1, al1, bh1, bl1)
-        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_waitcnt vmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        __builtin_amdgcn_sched_barrier(0);
-        K10_ISSUE(g % S);
-        K10_ADVANCE();
-        K10_ISSUE(s1);
-        K10_ADVANCE();
-        K10_READ(s2, ah0, al0, bh0, bl0);
-        K10_MFMA(H1, WMT, ah1, al1, bh1, bl1)
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      } else {
-        K10_STEP(g, ah0, al0, bh0, bl0, ah1, al1, bh1, bl1);
-        K10_STEP(g + 1, ah1, al1, bh1, bl1, ah0, al0, bh0, bl0);
-      }
+      K10_STEP(g, ah0, al0, bh0, bl0, ah1, al1, bh1, bl1);
+      K10_STEP(g + 1, ah1, al1, bh1, bl1, ah0, al0, bh0, bl0);
     }
     int tm, tn;
     k10_tile(c0 + ti * sx, tiles_m, tiles_n, tm, tn);
@@ -401,7 +369,7 @@ static TileCfg pick_tile(int64_t M, int N, int n_cu) {
   if (forced.bmb && N % (16 * forced.bnb) == 0) return forced;
   // FFN-up (N = 3072): 192 x 192 measured 98.3 -> 90.5 us at M = 6144 (tools/k10_tiles.sh); the
   // other E5 shapes are faster at 96 x 192 (qkv 67 vs 75 us, o 25 vs 34, down 73 vs 95)
-  if (N >= 3072 && N % 192 == 0 && M >= 192 * (int64_t)n_cu / 2) return TileCfg{12, 12};
+  if (N >= 3072 && N % 192 == 0 && ceil_div(M, 192) * (N / 192) >= n_cu) return TileCfg{12, 12};
   const TileCfg cands[4] = {{6, 12}, {8, 8}, {4, 8}, {4, 4}};
   TileCfg best = {0, 0};
   double best_cost = 0;
