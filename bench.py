@@ -728,6 +728,7 @@ def run_e2e(args, rank, ws, dev):
     import numpy as np
     import torch
     from classmate_hip.embeddings import E5MultilingualEmbedder
+    from classmate_hip.retrieval import device_batch
     from classmate_hip.retrieval.bm25 import BM25Store
     from classmate_hip.retrieval.fusion import HybridRetriever
     from classmate_hip.retrieval.vector_store import GpuVectorStore
@@ -827,6 +828,9 @@ def run_e2e(args, rank, ws, dev):
         "retrieve_latency_ms": {"p50": lat[len(lat) // 2], "p99": lat[min(len(lat) - 1, int(len(lat) * 0.99))],
                                 "n": len(lat)},
         "results_returned": n_res, "setup_s": time.perf_counter() - t_setup,
+        "retrieve_batch_path": ("device-resident (retrieval/device_batch.py)"
+                                if os.environ.get("CM_RETRIEVE_DEVICE", "1") != "0" and device_batch.applicable(retr, {}, True)
+                                else "host (per-stage dicts)"),
     }
     line = json.dumps(out)
     print(line, flush=True)

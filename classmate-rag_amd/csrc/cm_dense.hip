@@ -403,10 +403,6 @@ constexpr int kRRing = K1C_RING;  // LDS ring slots (8 KB each): kRRing - 1 chun
 #ifndef K1S_NT
 #define K1S_NT 1
 #endif
-// 1: K1c pairs its chunks -- one counted wait + barrier per two chunks instead of one per chunk
-#ifndef K1C_PAIR
-#define K1C_PAIR 0
-#endif
 // query chunks whose resident fragments are pinned to AGPRs (see the K1c prologue)
 #ifndef K1C_QAGPR
 #define K1C_QAGPR 8
@@ -667,15 +663,11 @@ __global__ void __launch_bounds__(64 * W, 1)
       const unsigned char *slot = lds + LL::ring + (gc % RING) * 8192;
       return *reinterpret_cast<const f16x8 *>(slot + (rt * 2 + sb) * 1024 + lane * 16);
     };
-    // K1C_PAIR: one counted wait + barrier per two chunks (even chunks), publishing the next two
-    // and refilling the two slots consumed before them; the prologue leaves chunk RING - 1 to the
-    // first barrier
-    constexpr bool PAIRK = K1C_PAIR && K1C_SCHED && RING == 8 && (KC % 2) == 0;
 #pragma unroll
     for (int p = 0; p < RING - 1; ++p) issue(p);
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PCS * (RING - 2)) : "memory");
     __builtin_amdgcn_s_barrier();
-    if (!PAIRK) issue(RING - 1);
+    issue(RING - 1);
     f16x8 xf[4][2];
 #pragma unroll
     for (int rt = 0; rt < (K1C_SCHED ? 2 : 4); ++rt) {  // interleaved schedule: chunk 0 reads its own 2-3
@@ -736,29 +728,13 @@ __global__ void __launch_bounds__(64 * W, 1)
             mf(0, m);
             __builtin_amdgcn_sched_barrier(0);
             if (m < 4 && !(dbg & 2048)) xf[2 + m / 2][m % 2] = frag(gc, 2 + m / 2, m % 2);  // bit 11: ablation
-            if constexpr (PAIRK) {
-              // even chunk: chunks gc+1, gc+2 landed (RING - 4 younger stay in flight), slots gc-1
-              // and gc fully read -> barrier -> chunks gc+RING-1, gc+RING into those slots
-              const int w0 = MH - 2 * PCS - 2;
-              if ((c % 2) == 0) {
-                if (m == w0) {
-                  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(PCS * (RING - 4)) : "memory");
-                  __builtin_amdgcn_s_barrier();
-                }
-                if (m > w0 && m <= w0 + 2 * PCS) {
-                  const int j = m - w0 - 1;
-                  issue_piece(j < PCS ? gc + RING - 1 : gc + RING, j % PCS);
-                }
-              }
-            } else {
-              const int w0 = MH - PCS - 2;
-              if (m == w0) {
-                asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(PCS * (RING - 2)) : "memory");
-                if (!(dbg & 512)) __builtin_amdgcn_s_barrier();  // bit 9: ablation only (races)
-              }
-              if (m > w0 && m <= w0 + PCS && !(dbg & 1024))  // bit 10: ablation only (stale data)
-                issue_piece(gc + RING, m - w0 - 1);
+            const int w0 = MH - PCS - 2;
+            if (m == w0) {
+              asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(PCS * (RING - 2)) : "memory");
+              if (!(dbg & 512)) __builtin_amdgcn_s_barrier();  // bit 9: ablation only (races)
             }
+            if (m > w0 && m <= w0 + PCS && !(dbg & 1024))  // bit 10: ablation only (stale data)
+              issue_piece(gc + RING, m - w0 - 1);
             __builtin_amdgcn_sched_barrier(0);
           }
 #pragma unroll
