@@ -47,8 +47,25 @@ constexpr int kTermLanesQd = 16;             // K2b descriptor slots per query (
 // a list contiguous after the heads, at nl + (q * nr + r) * (k - 1) + j - 1 (nl = nq * nr lists).
 // A list holds its entries in slots 0..c-1 and, when c < k, the sentinel (kEmptyKey, ~0u) in slot
 // c; slots past the sentinel are never written or read (most lists are empty: one 12-B write).
-__device__ inline int64_t lslot(int64_t list, int64_t nl, int k, int j) {
-  return j == 0 ? list : nl + list * (int64_t)(k - 1) + (j - 1);
+// CM_HEADS_QG: heads in wave order instead, [q / 4][r][q % 4] -- the 4 queries x 4 ranges of a K2a
+// wave write one whole 128-B line of keys (and 64 B of rows), the merge reads its query's heads at
+// a 32-B stride.
+#ifndef CM_HEADS_QG
+#define CM_HEADS_QG 0
+#endif
+__device__ inline int64_t lhead(int q, int64_t r, int64_t nr) {
+#if CM_HEADS_QG
+  return ((int64_t)(q >> 2) * nr + r) * 4 + (q & 3);
+#else
+  return (int64_t)q * nr + r;
+#endif
+}
+// entries of the head region (slots 1..k-1 follow it)
+__host__ __device__ inline int64_t lheads_total(int nq, int64_t nr) {
+  return CM_HEADS_QG ? (int64_t)((nq + 3) / 4 * 4) * nr : (int64_t)nq * nr;
+}
+__device__ inline int64_t lslot(int q, int64_t r, int64_t nr, int64_t nl, int k, int j) {
+  return j == 0 ? lhead(q, r, nr) : nl + ((int64_t)q * nr + r) * (k - 1) + (j - 1);
 }
 
 struct PairKey {  // (k, r) lexicographic; smaller is better
@@ -639,7 +656,7 @@ __global__ void __launch_bounds__(kBmThreads) __attribute__((amdgpu_waves_per_eu
         wave_min_pair(mk, mr);
         if (mr == 0xffffffffu || mk > T) break;  // nothing left that can enter the global top-k
         if (lane == 0) {
-          const int64_t o = lslot((int64_t)qi * nr + r, (int64_t)nq * nr, k, i);
+          const int64_t o = lslot(qi, r, nr, lheads_total(nq, nr), k, i);
           cand_key[o] = mk;
           cand_row[o] = mr;
         }
@@ -659,7 +676,7 @@ __global__ void __launch_bounds__(kBmThreads) __attribute__((amdgpu_waves_per_eu
         }
       }
       if (lane == 0 && i < k) {  // list terminator (readers stop at the first empty slot)
-        const int64_t o = lslot((int64_t)qi * nr + r, (int64_t)nq * nr, k, i);
+        const int64_t o = lslot(qi, r, nr, lheads_total(nq, nr), k, i);
         cand_key[o] = kEmptyKey;
         cand_row[o] = 0xffffffffu;
       }
@@ -720,8 +737,7 @@ __global__ void __launch_bounds__(kMergeThreads) bm25_merge_kernel(const uint64_
   int head[kMergePer];
   uint64_t hk[kMergePer];
   uint32_t hr[kMergePer];
-  const int64_t base = (int64_t)qi * nr;  // list id of (qi, range 0)
-  const int64_t nl = (int64_t)gridDim.x * nr;
+  const int64_t nl = lheads_total((int)gridDim.x, nr);
 #pragma unroll
   for (int s = 0; s < kMergePer; ++s) {
     const int l = threadIdx.x + kMergeThreads * s;
@@ -729,8 +745,8 @@ __global__ void __launch_bounds__(kMergeThreads) bm25_merge_kernel(const uint64_
     hk[s] = kEmptyKey;
     hr[s] = 0xffffffffu;
     if (l < nr) {
-      hk[s] = cand_key[base + l];
-      hr[s] = cand_row[base + l];
+      hk[s] = cand_key[lhead(qi, l, nr)];
+      hr[s] = cand_row[lhead(qi, l, nr)];
     }
   }
   for (int i = 0; i < k; ++i) {
@@ -760,8 +776,8 @@ __global__ void __launch_bounds__(kMergeThreads) bm25_merge_kernel(const uint64_
         const int l = threadIdx.x + kMergeThreads * s;
         head[s] += 1;
         if (head[s] < k) {
-          hk[s] = cand_key[lslot(base + l, nl, k, head[s])];
-          hr[s] = cand_row[lslot(base + l, nl, k, head[s])];
+          hk[s] = cand_key[lslot(qi, l, nr, nl, k, head[s])];
+          hr[s] = cand_row[lslot(qi, l, nr, nl, k, head[s])];
         } else {
           hk[s] = kEmptyKey;
           hr[s] = 0xffffffffu;
@@ -1197,10 +1213,11 @@ BmWs bm_ws_layout(const cm_bm25 *h, int nq, int total_terms, int k, void *base) 
   off += round_up((int64_t)std::max(total_terms, 1) * 8, 256);
   w.bounds = reinterpret_cast<int64_t *>(p + off);
   off += round_up((int64_t)std::max(total_terms, 1) * (nr + 1) * 8, 256);
+  const int64_t n_slots = lheads_total(nq, nr) + (int64_t)nq * nr * (k - 1);
   w.cand_key = reinterpret_cast<uint64_t *>(p + off);
-  off += round_up((int64_t)nq * nr * k * 8, 256);
+  off += round_up(n_slots * 8, 256);
   w.cand_row = reinterpret_cast<uint32_t *>(p + off);
-  off += round_up((int64_t)nq * nr * k * 4, 256);
+  off += round_up(n_slots * 4, 256);
   w.need = reinterpret_cast<uint8_t *>(p + off);
   off += round_up(ceil_div(std::max(nq, 1), kQPerWave) * nr, 256);
   w.items = reinterpret_cast<uint64_t *>(p + off);  // at most one item per (query, range)
