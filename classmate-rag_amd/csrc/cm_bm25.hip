@@ -47,23 +47,12 @@ constexpr int kTermLanesQd = 16;             // K2b descriptor slots per query (
 // a list contiguous after the heads, at nl + (q * nr + r) * (k - 1) + j - 1 (nl = nq * nr lists).
 // A list holds its entries in slots 0..c-1 and, when c < k, the sentinel (kEmptyKey, ~0u) in slot
 // c; slots past the sentinel are never written or read (most lists are empty: one 12-B write).
-// CM_HEADS_QG: heads in wave order instead, [q / 4][r][q % 4] -- the 4 queries x 4 ranges of a K2a
-// wave write one whole 128-B line of keys (and 64 B of rows), the merge reads its query's heads at
-// a 32-B stride.
-#ifndef CM_HEADS_QG
-#define CM_HEADS_QG 0
-#endif
-__device__ inline int64_t lhead(int q, int64_t r, int64_t nr) {
-#if CM_HEADS_QG
-  return ((int64_t)(q >> 2) * nr + r) * 4 + (q & 3);
-#else
-  return (int64_t)q * nr + r;
-#endif
-}
+// (Heads in K2a wave order, [q / 4][r][q % 4], so that a wave writes whole lines, measured slower --
+// 2.44 vs 2.38 ms per search -- and raised K2a's PMC WRITE_SIZE 0.29 -> 0.34 GB: the list writes
+// that count are the entries, not the heads.)
+__device__ inline int64_t lhead(int q, int64_t r, int64_t nr) { return (int64_t)q * nr + r; }
 // entries of the head region (slots 1..k-1 follow it)
-__host__ __device__ inline int64_t lheads_total(int nq, int64_t nr) {
-  return CM_HEADS_QG ? (int64_t)((nq + 3) / 4 * 4) * nr : (int64_t)nq * nr;
-}
+__host__ __device__ inline int64_t lheads_total(int nq, int64_t nr) { return (int64_t)nq * nr; }
 __device__ inline int64_t lslot(int q, int64_t r, int64_t nr, int64_t nl, int k, int j) {
   return j == 0 ? lhead(q, r, nr) : nl + ((int64_t)q * nr + r) * (k - 1) + (j - 1);
 }
