@@ -1155,8 +1155,7 @@ int build_head_tiles(cm_bm25 *h, const std::vector<int32_t> &df) {
 
 // CM_BM25_DEBUG (ablation only): K2 bit0 skip scoring, bit1 skip the per-range top-k; bit2 full
 // scan instead of the pruned search; K2a bit4 skip candidate scoring, bit5 skip the ranking,
-// bit6 no head tf gathers, bit7 no ownership searches, bit8 no tail tf searches, bit9 no dl/live,
-// bit10 no list sentinels, bit11 no list entries, bit12 no need bytes (write-traffic split).
+// bit6 no head tf gathers, bit7 no ownership searches, bit8 no tail tf searches, bit9 no dl/live.
 // Timing ablations are compiled only into -DCM_ABLATION builds (tools/build_variant.sh); the
 // product library ignores CM_BM25_DEBUG, so no bench line can come from a disabled kernel.
 #ifdef CM_ABLATION
