@@ -23,7 +23,8 @@ def _case(M, K, N, seed, xs=1.0, ws=0.02):
 
 
 @pytest.mark.parametrize("M,K,N", [(6144, 768, 2304), (6144, 768, 768), (1000, 768, 3072), (37, 3072, 768),
-                                   (1, 768, 64), (129, 64, 192), (20000, 768, 3072), (8192, 3072, 768)])
+                                   (1, 768, 64), (129, 64, 192), (20000, 768, 3072), (8192, 3072, 768),
+                                   (9216, 768, 3072), (12288, 3072, 768)])
 def test_linear_f16x3_fp32_accuracy(M, K, N):
     import torch
     from classmate_hip import engine
