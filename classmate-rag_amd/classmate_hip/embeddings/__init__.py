@@ -56,15 +56,27 @@ class HashTokenizer:
     Words -> stable ids in [5, vocab) via blake2b; <s>=0, </s>=2, <pad>=1.
     Only used with random-init weights (no real vocabulary is available)."""
 
+    _MEMO_MAX = 1 << 20   # word -> id memo (cleared when full): a query batch repeats words
+
     def __init__(self, vocab_size: int = 250002):
         self.vocab_size = vocab_size
         self._re = re.compile(r"\w+|[^\w\s]", re.UNICODE)
+        self._memo = {}
+
+    def _word_id(self, w: str) -> int:
+        h = int.from_bytes(hashlib.blake2b(w.encode("utf-8"), digest_size=8).digest(), "little")
+        i = 5 + h % (self.vocab_size - 5)
+        if len(self._memo) >= self._MEMO_MAX:
+            self._memo.clear()
+        self._memo[w] = i
+        return i
 
     def encode(self, text: str, max_len: int = MAX_SEQ_LEN) -> List[int]:
+        memo = self._memo
         ids = [0]
         for w in self._re.findall(text or ""):
-            h = int.from_bytes(hashlib.blake2b(w.encode("utf-8"), digest_size=8).digest(), "little")
-            ids.append(5 + h % (self.vocab_size - 5))
+            i = memo.get(w)
+            ids.append(i if i is not None else self._word_id(w))
         ids = ids[: max_len - 1] + [2]
         return ids
 
@@ -288,10 +300,15 @@ class E5MultilingualEmbedder:
             w0, pt, keep = embed(ids, mask)
             x, xp = engine.add_layernorm_split(w0, pt, emb.LayerNorm.weight, emb.LayerNorm.bias, eps, layers[0][1])
             short = fused_attn and S <= 64 and keep is None
+            # padded batches (S <= 32): the same HIP attention with the key mask (CM_E5_MASKED_ATTN=0:
+            # key-masked SDPA)
+            masked = (fused_attn and keep is not None and S <= 32
+                      and os.environ.get("CM_E5_MASKED_ATTN", "1") != "0")
+            km = mask.to(torch.int32).contiguous() if masked else None
             for li, (wqkv, a_qkv, wo, a_o, g1, b1, wi, a_i, w2, a_2, g2, bb2) in enumerate(layers):
                 qkv = engine.linear_f16x3(xp, wqkv)
-                if short:   # HIP attention reads the QKV output in place and writes the O operand planes
-                    op = engine.short_attention_split(qkv.view(B, S, 3 * D), H, scale, a_o)
+                if short or masked:   # HIP attention reads the QKV output in place and writes the O operand planes
+                    op = engine.short_attention_split(qkv.view(B, S, 3 * D), H, scale, a_o, key_mask=km)
                 else:
                     op = engine.split_rows(sdpa(qkv, B, S, keep), a_o)
                 x, xp = engine.add_layernorm_split(x, engine.linear_f16x3(op, wo), g1, b1, eps, a_i)
@@ -404,7 +421,9 @@ class E5MultilingualEmbedder:
         for s in range(0, len(texts), batch_size):
             idx = order[s: s + batch_size]
             ids, mask = self._tokenize([texts[i] for i in idx])
-            out[torch.from_numpy(np.ascontiguousarray(idx)).to(self.device)] = self.encode_token_ids(ids, mask).float()
+            # the order's device copy before the launches (a pageable copy waits for the stream)
+            idx_dev = torch.from_numpy(np.ascontiguousarray(idx)).to(self.device)
+            out[idx_dev] = self.encode_token_ids(ids, mask).float()
         return out
 
     def _encode(self, texts: List[str], batch_size: int = 32) -> np.ndarray:

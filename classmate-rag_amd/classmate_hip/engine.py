@@ -764,15 +764,25 @@ def add_layernorm_split(x, r, weight, bias, eps: float, a_scale: float, out=None
     return out, p
 
 
-def short_attention_split(qkv, heads: int, scale: float, a_scale: float) -> Planes:
-    """cm_short_attention (fp32) writing the context * a_scale as K10 Planes (B*S x heads*64)."""
+def short_attention_split(qkv, heads: int, scale: float, a_scale: float, key_mask=None) -> Planes:
+    """cm_short_attention (fp32) writing the context * a_scale as K10 Planes (B*S x heads*64).
+    key_mask (B, S) int32 on the device, nonzero = attend (padded batches, S <= 32): padded keys
+    leave the softmax (cm_short_attention_split_masked)."""
     B, S, F3 = qkv.shape
     if F3 != 3 * heads * 64 or not 0 < S <= 64 or qkv.dtype != torch.float32:
         raise ValueError("qkv must be fp32 (B, S<=64, 3*heads*64)")
     qkv = qkv.contiguous()
     p = Planes(B * S, heads * 64, a_scale, qkv.device)
-    L.check(L.fn["cm_short_attention_split"](L.ptr(qkv), B, S, heads, 64, float(scale), p.scale, L.ptr(p.data),
-                                             _stream(qkv.device.index)), "cm_short_attention_split")
+    if key_mask is None:
+        L.check(L.fn["cm_short_attention_split"](L.ptr(qkv), B, S, heads, 64, float(scale), p.scale, L.ptr(p.data),
+                                                 _stream(qkv.device.index)), "cm_short_attention_split")
+        return p
+    if tuple(key_mask.shape) != (B, S) or key_mask.dtype != torch.int32 or key_mask.device != qkv.device or S > 32:
+        raise ValueError("key_mask must be int32 (B, S) on the qkv device, S <= 32")
+    key_mask = key_mask.contiguous()
+    L.check(L.fn["cm_short_attention_split_masked"](L.ptr(qkv), B, S, heads, 64, float(scale), p.scale,
+                                                    L.ptr(key_mask), L.ptr(p.data), _stream(qkv.device.index)),
+            "cm_short_attention_split_masked")
     return p
 
 # ---------------------------------------------------------------------------

@@ -427,8 +427,11 @@ __device__ inline f32x4_t mfma3(const h16x8_t &ah, const h16x8_t &al, const h16x
   return __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh, c, 0, 0, 0);
 }
 
+// key_mask (optional, B x S, nonzero = attend): padded keys leave the softmax (probability 0), as
+// the XLM-R extended attention mask does; padded query rows are computed like any other row.
 __global__ void __launch_bounds__(64) short_attention_f16x3_kernel(const float *__restrict__ qkv, int S, int H,
                                                                    float scale, float a_scale,
+                                                                   const int32_t *__restrict__ key_mask,
                                                                    _Float16 *__restrict__ planes) {
   constexpr int VT = 40;  // V^T row stride (keys, halves): 80 B keeps the 8-byte reads aligned
   constexpr float kPScale = 16384.f;  // P in [0, 1] -> [0, 2^14]
@@ -505,6 +508,13 @@ __global__ void __launch_bounds__(64) short_attention_f16x3_kernel(const float *
       sc[kt][it] = a;
     }
   const float lscale = scale / (sq * sk);  // exact: sq sk is a power of two
+  // this lane's 8 keys (kk = 16 kt + 4 g + r): attended or not
+  uint32_t kmask = 0;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int kk = 16 * (j >> 2) + 4 * g + (j & 3);
+    if (kk < S && (!key_mask || key_mask[b * S + kk] != 0)) kmask |= 1u << j;
+  }
   h16x8_t ph[2], pl[2];
 #pragma unroll
   for (int it = 0; it < 2; ++it) {
@@ -514,7 +524,8 @@ __global__ void __launch_bounds__(64) short_attention_f16x3_kernel(const float *
     for (int j = 0; j < 8; ++j) {
       const int kt = j >> 2, r = j & 3;
       const int kk = 16 * kt + 4 * g + r;
-      v[j] = kk < S ? sc[kt][it][r] * lscale : -INFINITY;
+      v[j] = ((kmask >> j) & 1u) ? sc[kt][it][r] * lscale : -INFINITY;
+      (void)kk;
       m = fmaxf(m, v[j]);
     }
     m = fmaxf(m, __shfl_xor(m, 16));
@@ -643,6 +654,19 @@ extern "C" int cm_add_layernorm_split(const float *x_dev, const float *r_dev, in
   }
 }
 
+extern "C" int cm_short_attention_split_masked(const float *qkv_dev, int32_t B, int32_t S, int32_t H,
+                                               int32_t head_dim, float scale, float a_scale,
+                                               const int32_t *key_mask_dev, void *planes_dev, void *stream) {
+  if (B <= 0) return CM_OK;
+  if (!qkv_dev || !planes_dev || !key_mask_dev) CM_FAIL(CM_EINVAL, "NULL argument");
+  if (head_dim != kAttnDh) CM_FAIL(CM_EINVAL, "head_dim must be 64");
+  if (S <= 0 || S > 32 || H <= 0) CM_FAIL(CM_EUNSUPPORTED, "masked attention: need 0 < S <= 32 and H > 0");
+  hipLaunchKernelGGL(short_attention_f16x3_kernel, dim3((unsigned)((int64_t)B * H)), dim3(64), 0, (hipStream_t)stream,
+                     qkv_dev, S, H, scale, a_scale, key_mask_dev, (_Float16 *)planes_dev);
+  CM_HIP(hipGetLastError());
+  return CM_OK;
+}
+
 extern "C" int cm_short_attention_split(const float *qkv_dev, int32_t B, int32_t S, int32_t H, int32_t head_dim,
                                         float scale, float a_scale, void *planes_dev, void *stream) {
   if (B <= 0) return CM_OK;
@@ -651,7 +675,8 @@ extern "C" int cm_short_attention_split(const float *qkv_dev, int32_t B, int32_t
   if (S <= 0 || S > kAttnMaxS || H <= 0) CM_FAIL(CM_EINVAL, "need 0 < S <= 64 and H > 0");
   if (S <= 32)   // matrix cores, split precision
     hipLaunchKernelGGL(short_attention_f16x3_kernel, dim3((unsigned)((int64_t)B * H)), dim3(64), 0,
-                       (hipStream_t)stream, qkv_dev, S, H, scale, a_scale, (_Float16 *)planes_dev);
+                       (hipStream_t)stream, qkv_dev, S, H, scale, a_scale, (const int32_t *)nullptr,
+                       (_Float16 *)planes_dev);
   else
     hipLaunchKernelGGL((short_attention_kernel<float, true>), dim3((unsigned)((int64_t)B * H)), dim3(64), 0,
                        (hipStream_t)stream, qkv_dev, S, H, scale, nullptr, a_scale, (_Float16 *)planes_dev);

@@ -368,7 +368,11 @@ int cm_short_attention(const void *qkv_dev, int32_t B, int32_t S, int32_t H, int
  * cm_add_layernorm_split: cm_add_layernorm (fp32) that also writes its output
  *   rows * a_scale as planes.  D % 32 == 0.
  * cm_short_attention_split: cm_short_attention (fp32) writing the context
- *   * a_scale as planes (B*S x H*64) instead of fp32 rows.                 */
+ *   * a_scale as planes (B*S x H*64) instead of fp32 rows.
+ * cm_short_attention_split_masked: the same for padded batches (S <= 32):
+ *   key_mask_dev (B x S int32, nonzero = attend) removes padded keys from
+ *   the softmax, as XLM-R's extended attention mask (the reference's HF
+ *   forward for a padded query batch, rag/embeddings/__init__.py:85-105).  */
 #define CM_EPI_BIAS 0
 #define CM_EPI_BIAS_GELU 1
 #define CM_EPI_PLANES_GELU 2
@@ -383,6 +387,9 @@ int cm_add_layernorm_split(const float *x_dev, const float *r_dev, int64_t r_row
                            void *planes_dev, void *stream);
 int cm_short_attention_split(const float *qkv_dev, int32_t B, int32_t S, int32_t H, int32_t head_dim, float scale,
                              float a_scale, void *planes_dev, void *stream);
+int cm_short_attention_split_masked(const float *qkv_dev, int32_t B, int32_t S, int32_t H, int32_t head_dim,
+                                    float scale, float a_scale, const int32_t *key_mask_dev, void *planes_dev,
+                                    void *stream);
 
 #ifdef __cplusplus
 }

@@ -143,3 +143,35 @@ def test_short_attention_split_f16x3_matches_fp64(S):
     e, e32 = float((got - ref).abs().max()), float((t32.double() - ref).abs().max())
     print(f"\nattention S={S}: max err {e:.2e} (torch fp32 {e32:.2e})")
     assert e <= 2 * e32 + 2e-6
+
+
+@pytest.mark.parametrize("S", [2, 13, 24, 32])
+def test_short_attention_split_masked_matches_fp64(S):
+    """Padded batches: cm_short_attention_split_masked (key mask, B x S int32) against an fp64
+    softmax with the padded keys removed -- XLM-R's extended attention mask -- on every query row,
+    padded rows included (they attend to the valid keys, as in the reference's HF forward)."""
+    import torch
+    from classmate_hip import engine
+    torch.manual_seed(100 + S)
+    B, H = 29, 12
+    qkv = 2 * torch.randn(B, S, 3 * H * 64, device="cuda")
+    lens = torch.randint(1, S + 1, (B,), device="cuda")
+    lens[0] = S
+    mask = (torch.arange(S, device="cuda")[None, :] < lens[:, None]).to(torch.int32)
+    keep = mask.bool()[:, None, None, :]
+    q, k, v = qkv.double().view(B, S, 3, H, 64).permute(2, 0, 3, 1, 4)
+    sc = (q @ k.transpose(-1, -2) / 8.0).masked_fill(~keep, float("-inf"))
+    ref = (torch.softmax(sc, dim=-1) @ v).transpose(1, 2).reshape(B * S, H * 64)
+    q32, k32, v32 = qkv.view(B, S, 3, H, 64).permute(2, 0, 3, 1, 4)
+    s32 = (q32 @ k32.transpose(-1, -2) / 8.0).masked_fill(~keep, float("-inf"))
+    t32 = (torch.softmax(s32, dim=-1) @ v32).transpose(1, 2).reshape(B * S, H * 64)
+    p = engine.short_attention_split(qkv, H, 0.125, 2.0 ** 8, key_mask=mask)
+    hi, lo = p.halves()
+    got = (hi.double() + lo.double()) / 2.0 ** 8
+    e, e32 = float((got - ref).abs().max()), float((t32.double() - ref).abs().max())
+    print(f"\nmasked attention S={S}: max err {e:.2e} (torch fp32 {e32:.2e})")
+    assert e <= 2 * e32 + 2e-6
+    # an all-ones mask is the unmasked kernel
+    p1 = engine.short_attention_split(qkv, H, 0.125, 2.0 ** 8, key_mask=torch.ones_like(mask))
+    p0 = engine.short_attention_split(qkv, H, 0.125, 2.0 ** 8)
+    assert all(torch.equal(a, b) for a, b in zip(p1.halves(), p0.halves()))
