@@ -169,3 +169,24 @@ def test_vector_store_argument_errors(tmp_path):
     assert vs.count() == 0 and vs.query(query_embeddings=np.zeros(4, np.float32)) == []
     with pytest.raises(ValueError):
         GpuVectorStore(persist_dir=None, distance="l2")
+
+
+def test_hash_tokenizer_memo_is_transparent():
+    """The word -> id memo of the offline E5 tokenizer returns what the hash returns, across a
+    memo reset (bounded memo), for repeated and new words."""
+    import hashlib
+    from classmate_hip.embeddings import HashTokenizer
+    tok = HashTokenizer()
+    tok._MEMO_MAX = 8                                  # force resets inside one batch
+
+    def fresh(w):
+        h = int.from_bytes(hashlib.blake2b(w.encode("utf-8"), digest_size=8).digest(), "little")
+        return 5 + h % (tok.vocab_size - 5)
+
+    texts = ["query: the cat sat on the mat, the cat!", "query: élan vital über alles", "", "a a a b b c"] * 3
+    ids, mask = tok(texts)
+    for i, t in enumerate(texts):
+        want = [0] + [fresh(w) for w in tok._re.findall(t)] + [2]
+        assert list(ids[i, :len(want)]) == want
+        assert int(mask[i].sum()) == len(want)
+    assert len(tok._memo) <= 8
