@@ -26,7 +26,6 @@ import contextlib
 import hashlib
 import math
 import os
-import warnings
 import re
 from typing import Iterable, List, Optional
 
@@ -230,7 +229,6 @@ class E5MultilingualEmbedder:
         import torch
         B, S = ids.shape
         if (not getattr(self, "f16x3", False) or B > self._SMALL_B or S > self._SMALL_S
-                or getattr(self, "_small_graph_failed", False)
                 or os.environ.get("CM_E5_SMALL_GRAPH", "1") == "0" or torch.cuda.is_current_stream_capturing()):
             return None
         Sb = 16 if S <= 16 else 32
@@ -256,13 +254,8 @@ class E5MultilingualEmbedder:
                 run()
             torch.cuda.current_stream(ids.device).wait_stream(side)
             graph = torch.cuda.CUDAGraph()
-            try:
-                with torch.cuda.graph(graph):
-                    run()
-            except RuntimeError as e:   # capture refused: the eager forward from now on, said once
-                self._small_graph_failed = True
-                warnings.warn(f"E5 small-batch graph capture failed ({e}); using the eager forward")
-                return None
+            with torch.cuda.graph(graph):
+                run()
             ent = cache[key] = (g_ids, g_mask, g_out, graph, pad)
         g_ids, g_mask, g_out, graph, pad = ent
         g_ids.fill_(pad)
