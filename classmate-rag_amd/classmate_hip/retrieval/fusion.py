@@ -163,9 +163,6 @@ class HybridRetriever:
     def retrieve(self, *, question: str, filters: Optional[Mapping[str, object]] = None, top_k: int = 8,
                  hybrid: bool = True) -> List[Dict[str, object]]:
         raw_filters = filters or {}
-        if os.environ.get("CM_RETRIEVE_DEVICE", "1") != "0" and device_batch.applicable(self, raw_filters, hybrid):
-            # the same chain as retrieve_batch for a batch of one (equal dicts: tests/test_gpu_dropin.py)
-            return device_batch.retrieve_batch(self, [question], top_k)[0]
         chroma_where = build_where_filter(raw_filters) if raw_filters else None
         bm_where = raw_filters or None
         bm25_res: List[Mapping[str, object]] = []

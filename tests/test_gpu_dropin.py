@@ -351,8 +351,3 @@ def test_retrieve_batch_device_path_equals_host_path(corpus, monkeypatch, top_k)
     got = retr.retrieve_batch(questions=qtexts, top_k=top_k)
     monkeypatch.setenv("CM_RETRIEVE_DEVICE", "0")
     assert got == retr.retrieve_batch(questions=qtexts, top_k=top_k)
-    # single queries: retrieve() takes the same device chain for a batch of one
-    monkeypatch.delenv("CM_RETRIEVE_DEVICE")
-    got1 = [retr.retrieve(question=q, top_k=top_k) for q in qtexts]
-    monkeypatch.setenv("CM_RETRIEVE_DEVICE", "0")
-    assert got1 == [retr.retrieve(question=q, top_k=top_k) for q in qtexts]
