@@ -58,6 +58,7 @@ SIGNATURES = {
     "cm_dense_destroy": (None, c_vp),
     "cm_dense_reserve": (c_int, c_vp, c_i64),
     "cm_dense_mem_stats": (c_int, c_vp, c_vp, c_vp, c_vp),
+    "cm_dense_set_growth": (c_int, c_vp, c_i32),
     "cm_dense_upsert": (c_int, c_vp, c_vp, c_vp, c_i64),
     "cm_dense_upsert_dev": (c_int, c_vp, c_vp, c_i64, c_i64, c_vp),
     "cm_dense_delete": (c_int, c_vp, c_vp, c_i64),

@@ -410,41 +410,63 @@ class E5MultilingualEmbedder:
                 fwd()
         return ids, mask, out, graph
 
-    def _encode_dev(self, texts: List[str], batch_size: int = 32):
+    def _rows_independent(self, seq_len: int) -> bool:
+        """True when every kernel of the forward computes a row independently of the other rows of
+        its batch and of the batch's pad length: the fp32 K10 path (fixed k order per output row,
+        per-row LayerNorm) with the HIP attention of S <= 32 (per-sequence, padded keys leave the
+        softmax exactly).  Torch SDPA (S > 32) and hipBLASLt (bf16, the HF module) may pick kernels
+        by batch shape, so their rows are only reproduced in sentence-transformers' own batches."""
+        if os.environ.get("CM_E5_LEAN", "1") == "0" or seq_len > 32:
+            return False
+        self._lean_forward()
+        return bool(getattr(self, "f16x3", False)) and os.environ.get("CM_E5_MASKED_ATTN", "1") != "0" \
+            and os.environ.get("CM_E5_FUSED_ATTN", "1") != "0"
+
+    def _encode_dev(self, texts: List[str], batch_size: int = 32, group: Optional[int] = None):
         """(len(texts), 768) fp32 device tensor: sentence-transformers' length-sorted batches of
-        ``batch_size`` (its encode() default), each through encode_token_ids, order restored."""
+        ``batch_size`` (its encode() default, rag/embeddings/__init__.py:84-103), each through
+        encode_token_ids, order restored.  ``group`` > batch_size tokenizes that many texts at once
+        and runs them as ONE forward when the rows are provably batch-independent
+        (``_rows_independent``); otherwise the group is cut back into the reference's batches
+        (each trimmed to its own longest row, exactly what tokenizing that batch alone gives)."""
         import torch
         out = torch.empty((len(texts), self.model.config.hidden_size), dtype=torch.float32, device=self.device)
         if not texts:
             return out
+        group = max(group or batch_size, batch_size)
         order = np.argsort([-len(t) for t in texts], kind="stable")
-        for s in range(0, len(texts), batch_size):
-            idx = order[s: s + batch_size]
+        for s in range(0, len(texts), group):
+            idx = order[s: s + group]
             ids, mask = self._tokenize([texts[i] for i in idx])
             # the order's device copy before the launches (a pageable copy waits for the stream)
             idx_dev = torch.from_numpy(np.ascontiguousarray(idx)).to(self.device)
-            out[idx_dev] = self.encode_token_ids(ids, mask).float()
+            if len(idx) <= batch_size or self._rows_independent(ids.shape[1]):
+                out[idx_dev] = self.encode_token_ids(ids, mask).float()
+                continue
+            lens = mask.sum(1).tolist()
+            for t in range(0, len(idx), batch_size):
+                w = max(lens[t:t + batch_size])
+                out[idx_dev[t:t + batch_size]] = self.encode_token_ids(
+                    ids[t:t + batch_size, :w].contiguous(), mask[t:t + batch_size, :w].contiguous()).float()
         return out
 
-    def _encode(self, texts: List[str], batch_size: int = 32) -> np.ndarray:
+    def _encode(self, texts: List[str], batch_size: int = 32, group: Optional[int] = None) -> np.ndarray:
         if not texts:
             return np.zeros((0, self.model.config.hidden_size), np.float32)
-        return self._encode_dev(texts, batch_size).cpu().numpy()
+        return self._encode_dev(texts, batch_size, group).cpu().numpy()
 
-    # Query batches: sentence-transformers encodes 32 texts per forward.  On the unpadded path every
-    # kernel here computes a row independently of the others in its batch (fixed k order in the
-    # GEMMs, per-sequence attention, per-row LayerNorm), so a larger batch returns the same
-    # embeddings with 8x fewer launches -- what a 256-query retrieve_batch call needs.  (Padded
-    # batches attend through torch SDPA, whose last bits can depend on the batch shape, as
-    # sentence-transformers' own length-sorted batches do.)
+    # Query batches: sentence-transformers encodes 32 texts per forward.  Up to 256 queries are
+    # tokenized together and run as one forward when the rows are batch-independent (the fp32 K10
+    # path at <= 32 tokens, _rows_independent): the same embeddings with 8x fewer launches, what a
+    # 256-query retrieve_batch call needs.  Otherwise they run in the reference's 32-text batches.
     query_batch_size = 256
 
     def encode_queries(self, queries: Iterable[str]) -> np.ndarray:
-        return self._encode(self._fmt_queries(queries), self.query_batch_size).astype("float32", copy=False)
+        return self._encode(self._fmt_queries(queries), group=self.query_batch_size).astype("float32", copy=False)
 
     def encode_queries_dev(self, queries: Iterable[str]):
         """encode_queries, left on the device (the batched retrieval path consumes it there)."""
-        return self._encode_dev(self._fmt_queries(queries), self.query_batch_size)
+        return self._encode_dev(self._fmt_queries(queries), group=self.query_batch_size)
 
     def encode_passages(self, texts: Iterable[str]) -> np.ndarray:
         return self._encode(self._fmt_passages(texts)).astype("float32", copy=False)

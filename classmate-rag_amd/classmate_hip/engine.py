@@ -100,6 +100,11 @@ class DenseIndex:
     def reserve(self, capacity: int):
         L.check(L.fn["cm_dense_reserve"](self._h, int(capacity)), "cm_dense_reserve")
 
+    def set_growth(self, mode: int):
+        """0 auto (device-to-device copy when old + new fit in free HBM, else host-staged), 1 always
+        host-staged above 1 GiB (peak = the final allocation) -- cm_dense_set_growth."""
+        L.check(L.fn["cm_dense_set_growth"](self._h, int(mode)), "cm_dense_set_growth")
+
     def mem_stats(self) -> dict:
         """Device bytes of the row arrays now / at most at once, and the growths staged through
         host memory (cm_dense_mem_stats)."""

@@ -93,7 +93,7 @@ def retrieve_batch(retr, questions: Sequence[str], top_k: int) -> List[List[Dict
     kv, kb = retr.k_vector, retr.k_bm25
     pool = max(kv, retr.mmr_max_pool)
     bm._ensure_index()
-    key = (vs._version, bm._version)
+    key = (id(vs), vs._version, id(bm), bm._version)   # the stores themselves, not only their counters
     km = getattr(retr, "_device_keymap", None)
     if km is None or km[0] != key:
         km = (key, _KeyMap(vs, bm, index.device))
@@ -137,7 +137,7 @@ def retrieve_batch(retr, questions: Sequence[str], top_k: int) -> List[List[Dict
         oki, fli, ofi, ovi, obi = ok[i], ofl[i], of[i], ov[i], ob[i]
         for j in range(m):
             kk, fl = oki[j], fli[j]
-            if kk < nvr:
+            if fl & 1:                                   # a vector item (the vector store's fields first)
                 _id = vids[kk]
                 doc, meta = vdocs[kk], vmetas[kk] or {}
                 if fl & 2 and (not doc or not meta):
@@ -146,8 +146,8 @@ def retrieve_batch(retr, questions: Sequence[str], top_k: int) -> List[List[Dict
                         doc = e.text
                     if not meta and e.metadata:
                         meta = e.metadata
-            else:
-                e = entries[bids[kk - nvr]]
+            else:                                        # BM25-only: the BM25 entry's fields (fusion.py:146-151)
+                e = entries[bids[int(vs2bm[kk])] if kk < nvr else bids[kk - nvr]]
                 _id, doc, meta = e.id, e.text or None, e.metadata or {}
             res.append({"id": _id, "document": doc, "metadata": meta,
                         "scores": {"vector_distance": ovi[j] if fl & 1 else None,

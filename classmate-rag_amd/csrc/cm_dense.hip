@@ -22,6 +22,9 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <cstdlib>
+#include <cstring>
+#include <memory>
 #include <mutex>
 #include <vector>
 
@@ -1342,6 +1345,7 @@ struct cm_dense {
   hipStream_t stream = nullptr;
   int64_t mem_cur = 0, mem_peak = 0;       // device bytes of the four row arrays (cm_dense_mem_stats)
   int64_t staged_growths = 0;              // growths that went through host memory
+  int32_t grow_mode = 0;                   // cm_dense_set_growth: 0 auto, 1 always staged (> 1 GiB)
   DevBuf staging, rows_buf, allow_buf, ws, out_buf;
   std::vector<float> host_tmp;
 };
@@ -1452,14 +1456,35 @@ DenseWs dense_ws_layout(const cm_dense *h, const DenseCfg &c, int nq, int k, voi
 // Bytes of the four row arrays at `rows` rows (C fp32, invc, live bits, Xh plane).
 int64_t dense_row_bytes(const cm_dense *h, int64_t rows) { return rows * h->ld * 6 + rows * 4 + rows / 8; }
 
-// Growth (dense_grow).  The arrays are reallocated at max(need, 1.5 x rows_alloc) rows.  A store
-// holding more than kStageBytes moves through host memory: its written rows' fp32 data, norms and
-// live bits are copied to the host, the old arrays freed, the new ones allocated and the rows copied
-// back; the f16 plane is recomputed on the device from them (dense_replane_kernel, bit-identical
-// to the upsert's).  The device then never holds the old and the new arrays at once -- a store
-// growing by upserts to hundreds of GB of HBM peaks at its final size, not 2.5 x it.  Smaller
-// stores copy device to device (faster; their double residency is at most 2 x kStageBytes).
+// Growth (dense_grow).  The arrays are reallocated at max(need, 1.5 x rows_alloc) rows.  When the
+// new arrays fit in the device's free memory next to the old ones (hipMemGetInfo, with kGrowSlack to
+// spare), the rows are copied device to device.  Otherwise -- or always above kStageBytes under
+// grow_mode 1 (cm_dense_set_growth) -- the store moves through host memory: its written rows' fp32
+// data, norms and live bits go to an uninitialised host buffer (through a pinned bounce buffer of
+// kBounceBytes, so no pageable copies), the old arrays are freed, the new ones allocated and the
+// rows copied back; the f16 plane is recomputed on the device from them (dense_replane_kernel,
+// bit-identical to the upsert's).  The device then never holds the old and the new arrays at once:
+// a store growing to hundreds of GB of HBM peaks at its final size, not 2.5 x it.
 constexpr int64_t kStageBytes = 1ll << 30;
+constexpr int64_t kGrowSlack = 1ll << 30;
+constexpr size_t kBounceBytes = 64ull << 20;
+
+// Host <-> device through one pinned bounce buffer (chunks of kBounceBytes, stream-synchronous).
+int staged_copy(cm_dense *h, char *host, char *dev, size_t bytes, bool to_host, char *bounce) {
+  for (size_t o = 0; o < bytes; o += kBounceBytes) {
+    const size_t n = std::min(kBounceBytes, bytes - o);
+    if (to_host) {
+      CM_HIP(hipMemcpyAsync(bounce, dev + o, n, hipMemcpyDeviceToHost, h->stream));
+      CM_HIP(hipStreamSynchronize(h->stream));
+      memcpy(host + o, bounce, n);
+    } else {
+      memcpy(bounce, host + o, n);
+      CM_HIP(hipMemcpyAsync(dev + o, bounce, n, hipMemcpyHostToDevice, h->stream));
+      CM_HIP(hipStreamSynchronize(h->stream));
+    }
+  }
+  return CM_OK;
+}
 
 __global__ void __launch_bounds__(256) dense_replane_kernel(const float *__restrict__ C, const float *__restrict__ invc,
                                                             int64_t n, int dim, int ld, _Float16 *__restrict__ Xh) {
@@ -1504,19 +1529,27 @@ int dense_grow(cm_dense *h, int64_t need_rows) {
   uint32_t *lv2;
   _Float16 *xh2;
   int rc;
-  if (keep > 0 && h->mem_cur > kStageBytes) {
+  bool staged = keep > 0 && h->mem_cur > kStageBytes;
+  if (staged && h->grow_mode == 0) {   // auto: copy on the device when old + new fit with slack
+    size_t free_b = 0, total_b = 0;
+    if (hipMemGetInfo(&free_b, &total_b) == hipSuccess &&
+        (int64_t)free_b >= dense_row_bytes(h, cap) + kGrowSlack)
+      staged = false;
+  }
+  if (staged) {
     // host-staged: fp32 rows + norms + live bits out, old arrays freed, new ones in
     const size_t cb = (size_t)keep * h->ld * 4, ib = (size_t)keep * 4, lb = (size_t)keep / 8;
-    std::vector<char> host;
-    try {
-      host.resize(cb + ib + lb);
-    } catch (const std::bad_alloc &) {
-      CM_FAIL(CM_ENOMEM, "dense: no host memory to stage the growth");
-    }
+    std::unique_ptr<char, void (*)(void *)> host_p(static_cast<char *>(malloc(cb + ib + lb)), free);
+    char *bounce = nullptr;
+    if (!host_p) CM_FAIL(CM_ENOMEM, "dense: no host memory to stage the growth");
+    if (hipHostMalloc(reinterpret_cast<void **>(&bounce), kBounceBytes, hipHostMallocDefault) != hipSuccess)
+      CM_FAIL(CM_ENOMEM, "dense: no pinned host memory to stage the growth");
+    std::unique_ptr<char, hipError_t (*)(void *)> bounce_p(bounce, hipHostFree);
+    char *host = host_p.get();
     CM_HIP(hipStreamSynchronize(h->stream));
-    CM_HIP(hipMemcpy(host.data(), h->C, cb, hipMemcpyDeviceToHost));
-    CM_HIP(hipMemcpy(host.data() + cb, h->invc, ib, hipMemcpyDeviceToHost));
-    CM_HIP(hipMemcpy(host.data() + cb + ib, h->live, lb, hipMemcpyDeviceToHost));
+    if ((rc = staged_copy(h, host, reinterpret_cast<char *>(h->C), cb, true, bounce))) return rc;
+    if ((rc = staged_copy(h, host + cb, reinterpret_cast<char *>(h->invc), ib, true, bounce))) return rc;
+    if ((rc = staged_copy(h, host + cb + ib, reinterpret_cast<char *>(h->live), lb, true, bounce))) return rc;
     dense_free_rows(h);
     h->rows_alloc = 0;
     h->mem_cur = 0;
@@ -1536,9 +1569,16 @@ int dense_grow(cm_dense *h, int64_t need_rows) {
       }
       rc = CM_ENOMEM;
     }
-    CM_HIP(hipMemcpyAsync(C2, host.data(), cb, hipMemcpyHostToDevice, h->stream));
-    CM_HIP(hipMemcpyAsync(ic2, host.data() + cb, ib, hipMemcpyHostToDevice, h->stream));
-    CM_HIP(hipMemcpyAsync(lv2, host.data() + cb + ib, lb, hipMemcpyHostToDevice, h->stream));
+    // (cap may now be keep: the old rows go back into an array of their old size)
+    int rc2;
+    if ((rc2 = staged_copy(h, host, reinterpret_cast<char *>(C2), cb, false, bounce)) ||
+        (rc2 = staged_copy(h, host + cb, reinterpret_cast<char *>(ic2), ib, false, bounce)) ||
+        (rc2 = staged_copy(h, host + cb + ib, reinterpret_cast<char *>(lv2), lb, false, bounce))) {
+      h->C = C2, h->invc = ic2, h->live = lv2, h->Xh = xh2;
+      h->rows_alloc = cap;
+      h->mem_cur = dense_row_bytes(h, cap);
+      return rc2;
+    }
     hipLaunchKernelGGL(dense_replane_kernel, dim3((unsigned)keep), dim3(256), 0, h->stream, C2, ic2, keep, h->dim,
                        h->ld, xh2);
     CM_HIP(hipGetLastError());
@@ -1992,6 +2032,13 @@ int cm_dense_reset(cm_dense *h) {
   CM_HIP(hipMemsetAsync(h->rnorm, 0, 8, h->stream));
   CM_HIP(hipStreamSynchronize(h->stream));
   h->size = 0;
+  return CM_OK;
+}
+
+int cm_dense_set_growth(cm_dense *h, int32_t mode) {
+  if (!h) CM_FAIL(CM_EINVAL, "cm_dense_set_growth: null handle");
+  if (mode != 0 && mode != 1) CM_FAIL(CM_EINVAL, "cm_dense_set_growth: mode must be 0 (auto) or 1 (staged)");
+  h->grow_mode = mode;
   return CM_OK;
 }
 

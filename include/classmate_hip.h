@@ -71,10 +71,14 @@ int cm_dense_create(int device, int32_t dim, int64_t capacity, cm_dense **out);
 void cm_dense_destroy(cm_dense *h);
 int cm_dense_reserve(cm_dense *h, int64_t capacity);
 /* Device bytes of the row arrays (fp32 rows, norms, live bits, f16 plane): now and the most ever
- * held at once, and how many growths went through host memory.  A store above 1 GiB grows by
- * staging its rows through the host (the device never holds the old and the new arrays together);
- * smaller ones copy device to device.  Not a reference interface (capacity planning for 288 GB). */
+ * held at once, and how many growths went through host memory (cm_dense_set_growth decides when).
+ * Not a reference interface (capacity planning for 288 GB). */
 int cm_dense_mem_stats(cm_dense *h, int64_t *cur_bytes, int64_t *peak_bytes, int64_t *staged_growths);
+/* Growth policy (no reference counterpart: Chroma grows its own collection).  0 = automatic: a
+ * growth copies device to device when the new arrays fit in the free device memory next to the old
+ * ones, else it stages the rows through host memory; 1 = a store above 1 GiB always stages (peak
+ * device footprint = the final allocation, never old + new).  CM_EINVAL for other modes. */
+int cm_dense_set_growth(cm_dense *h, int32_t mode);
 /* ChromaVectorStore.upsert (vector_chroma.py:168-200): write n fp32 rows
  * (host, n x dim row-major) at the given row indices, marking them live.
  * Rows beyond the current size grow the store. */

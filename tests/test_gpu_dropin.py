@@ -351,3 +351,28 @@ def test_retrieve_batch_device_path_equals_host_path(corpus, monkeypatch, top_k)
     got = retr.retrieve_batch(questions=qtexts, top_k=top_k)
     monkeypatch.setenv("CM_RETRIEVE_DEVICE", "0")
     assert got == retr.retrieve_batch(questions=qtexts, top_k=top_k)
+
+
+@pytest.mark.gpu
+def test_retrieve_batch_device_bm25_only_items_take_bm25_fields(corpus, monkeypatch):
+    """A BM25-only hit whose id the vector store also holds is built from the BM25 entry (document
+    and metadata), as the reference's merge does (rag/retrieval/fusion.py:146-151): here the two
+    stores hold different non-empty documents and metadata (the BM25 side without 'language', which
+    BM25Store.upsert_many then detects), so the device path must not take the vector store's."""
+    from classmate_hip.retrieval import BM25Store, GpuVectorStore, HybridRetriever, device_batch
+    ids, texts, metas, emb = corpus["ids"], corpus["texts"], corpus["metas"], corpus["emb"]
+    vs = GpuVectorStore(persist_dir=None)
+    vs.upsert(ids=ids, documents=texts, metadatas=metas, embeddings=emb)
+    bm = BM25Store(index_dir=None)
+    bm.upsert_many(ids=ids, texts=[t + " bmside" for t in texts],
+                   metadatas=[{"course": "bm25-" + str(m.get("course"))} for m in metas])
+    retr = HybridRetriever(vector_store=vs, bm25_store=bm, embedder=PresetEmbedder(corpus["qtexts"], corpus["qvecs"]),
+                           k_vector=8, k_bm25=8)
+    assert device_batch.applicable(retr, {}, True)
+    got = retr.retrieve_batch(questions=corpus["qtexts"], top_k=16)
+    monkeypatch.setenv("CM_RETRIEVE_DEVICE", "0")
+    want = retr.retrieve_batch(questions=corpus["qtexts"], top_k=16)
+    assert got == want
+    bm_only = [r for res in got for r in res if r["scores"]["vector_distance"] is None]
+    assert bm_only and all(r["document"].endswith(" bmside") and r["metadata"]["course"].startswith("bm25-")
+                           for r in bm_only)

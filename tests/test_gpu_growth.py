@@ -1,10 +1,12 @@
-"""Ingest growth without double residency (VERDICT r2 "next" 8).
+"""Ingest growth (VERDICT r2 "next" 8).
 
 ChromaVectorStore.upsert (rag/retrieval/vector_chroma.py:168-200) grows the collection one batch at
-a time.  Above 1 GiB the HBM store grows through host memory (cm_dense.hip dense_grow): its rows go
-to the host, the old arrays are freed, the new ones allocated and the rows copied back with the f16
-plane recomputed on the device -- so the device never holds the old and the new arrays together
-and the peak footprint is the final allocation.  Smaller stores copy device to device.
+a time.  cm_dense.hip dense_grow copies device to device when the new arrays fit next to the old
+ones in free HBM (the automatic policy); under cm_dense_set_growth(1), or when they do not fit, a
+store above 1 GiB grows through host memory: its rows go to the host (pinned bounce buffer), the
+old arrays are freed, the new ones allocated and the rows copied back with the f16 plane recomputed
+on the device -- so the device never holds the old and the new arrays together and the peak
+footprint is the final allocation.
 (An in-place growth through reserved address ranges, hipMemAddressReserve + hipMemMap, was tried
 first and dropped: hipMemSetAccess rejects some chunk ranges on this ROCm, tools/vmm_probe.hip.)
 """
@@ -51,6 +53,7 @@ def test_dense_growth_peak_is_final_size():
     from classmate_hip import engine
     nb, per = 16, 125_000                                 # 0 -> 2M rows (9.2 GB) in 16 upserts
     idx = engine.DenseIndex(D, capacity=0)
+    idx.set_growth(1)                                     # the peak-bounded policy
     stats, probes = _grow(idx, nb, per, seed=3)
     final = stats[-1]
     n = nb * per
@@ -88,5 +91,22 @@ def test_dense_small_store_copies_on_device():
     final = stats[-1]
     assert final["staged_growths"] == 0
     assert final["peak_bytes"] >= 1.5 * final["bytes"]              # old + new coexisted
+    _check_search(idx, probes)
+    idx.close()
+
+
+def test_dense_large_store_auto_growth_stays_on_device():
+    """with free HBM for old + new, the automatic policy copies a > 1 GiB store device to
+    device (no host round trip); rows and searches are unchanged."""
+    from classmate_hip import engine
+    idx = engine.DenseIndex(D, capacity=0)
+    with pytest.raises(ValueError):
+        idx.set_growth(2)
+    stats, probes = _grow(idx, 6, 125_000, seed=5)        # 0 -> 750k rows (3.5 GB): growths above 1 GiB
+    final = stats[-1]
+    assert final["bytes"] > 1 << 30
+    assert final["staged_growths"] == 0
+    assert final["peak_bytes"] > final["bytes"]           # old + new coexisted
+    assert idx.size == 750_000 and idx.live_count() == 750_000
     _check_search(idx, probes)
     idx.close()

@@ -1,7 +1,8 @@
-"""World-size-2 (gloo, CPU) tests of the multi-GPU exchange steps in
-classmate_hip.parallel: sharded BM25 statistics must give the
-single-shard idf table / avgdl bit-for-bit, and the all-gather top-k merges must
-give the unsharded oracle top-k (ties by global row, zero-score padding).
+"""World-size-2 and world-size-8 (gloo, CPU) tests of the multi-GPU exchange steps
+in classmate_hip.parallel (8 = BASELINE configs[4]'s 8-way split):
+sharded BM25 statistics must give the single-shard idf table / avgdl
+bit-for-bit, and the all-gather top-k merges must give the unsharded oracle
+top-k (ties by global row, zero-score padding).
 
 Per-shard top-k here comes from the C oracle (no GPU); on the GPU the same merge
 consumes the HIP shards' outputs (bench.py).
@@ -17,7 +18,7 @@ import torch.multiprocessing as mp
 
 from oracle import corc
 
-WS = 2
+NQ = 8          # dense / packed-exchange queries: B = NQ splits into equal blocks at WS = 2 and 8
 
 
 def _free_port():
@@ -79,7 +80,7 @@ def _filtered_shard_search(P, toks, off, vocab, queries, row0, n, k):
     return S.numpy(), R.numpy()
 
 
-def _worker(rank, port, out_q):
+def _worker(rank, WS, port, out_q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(WS))
     dist.init_process_group("gloo", rank=rank, world_size=WS)
     try:
@@ -105,7 +106,7 @@ def _worker(rank, port, out_q):
         emb = rng.standard_normal((nd, 32)).astype(np.float32)
         emb[5] = emb[4]                               # exact duplicate rows across the shard boundary region
         emb[nd // 2 + 1] = emb[4]
-        q = rng.standard_normal((6, 32)).astype(np.float32)
+        q = rng.standard_normal((NQ, 32)).astype(np.float32)
         q[0] = emb[4]
         d, r = corc.dense_topk_f64(emb[row0:row0 + n], q, 16)
         D, R = P.merge_dense_topk(torch.from_numpy(d.astype(np.float32)), torch.from_numpy(r + row0), 16)
@@ -118,15 +119,26 @@ def _worker(rank, port, out_q):
         res["max"] = P.max_over_ranks(float(rank) + 0.5)
         # the batched path's exchanges: ONE packed all-gather of both shard lists, then the pool
         # rows of this rank's query block fetched from their owners with one all-to-all
-        sc, rw = corc.bm25_topk(csr, idf, avgdl, queries[:6], 10)
+        sc, rw = corc.bm25_topk(csr, idf, avgdl, queries[:NQ], 10)
         d_m, r_m, s_m, b_m = P.exchange_topk(torch.from_numpy(d.astype(np.float32)), torch.from_numpy(r + row0),
                                              torch.from_numpy(sc), torch.from_numpy(np.where(rw >= 0, rw + row0, rw)))
         res["xchg"] = (d_m.numpy(), r_m.numpy(), s_m.numpy(), b_m.numpy())
-        bq = 6 // WS
+        bq = NQ // WS
         shard_emb = torch.from_numpy(emb[row0:row0 + n])
-        pool = P.fetch_pool_vectors(r_m, rank * bq, bq, lambda lr: shard_emb[lr],
-                                    [P.shard_range(nd, i, WS)[0] for i in range(WS)] + [nd], 32)
+        starts = [P.shard_range(nd, i, WS)[0] for i in range(WS)] + [nd]
+
+        def gather_local(lr):          # cm_dense_gather_dev's contract: row < 0 -> a zero row
+            return torch.where((lr >= 0)[:, None], shard_emb[lr.clamp(min=0)], torch.zeros(()))
+        pool = P.fetch_pool_vectors(r_m, rank * bq, bq, gather_local, starts, 32)
         res["pool_block"] = pool.numpy()
+        r_pad = r_m.clone()
+        r_pad[:, -3:] = -1                                  # padded pools: zero rows
+        res["pool_block_pad"] = P.fetch_pool_vectors(r_pad, rank * bq, bq, gather_local, starts, 32).numpy()
+        try:                                                # uneven blocks are refused on every rank
+            P.fetch_pool_vectors(r_m[:NQ - 1], rank * bq, bq, gather_local, starts, 32)
+            res["uneven"] = None
+        except ValueError:
+            res["uneven"] = "ValueError"
         # filtered BM25 (quirk Q2): candidate statistics all-reduced, epsilon floor from the
         # global first-occurrence order -- the exchange bm25_search_filtered_sharded runs
         for k in (1, 10, 64):
@@ -148,12 +160,13 @@ def _worker(rank, port, out_q):
         dist.destroy_process_group()
 
 
-@pytest.fixture(scope="module")
-def results():
+@pytest.fixture(scope="module", params=[2, 8], ids=["ws2", "ws8"])
+def results(request):
+    WS = request.param
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, port, q)) for r in range(WS)]
+    procs = [ctx.Process(target=_worker, args=(r, WS, port, q)) for r in range(WS)]
     for p in procs:
         p.start()
     out = [q.get(timeout=240) for _ in range(WS)]
@@ -193,7 +206,7 @@ def test_dense_merge_equals_unsharded(results):
     emb = rng.standard_normal((nd, 32)).astype(np.float32)
     emb[5] = emb[4]
     emb[nd // 2 + 1] = emb[4]
-    q = rng.standard_normal((6, 32)).astype(np.float32)
+    q = rng.standard_normal((NQ, 32)).astype(np.float32)
     q[0] = emb[4]
     d, r = corc.dense_topk_f64(emb, q, 16)
     for res in results:
@@ -209,7 +222,7 @@ def test_pool_assembly_and_max(results):
     want = emb[[0, nd - 1, nd // 2, 7]]
     for r in results:
         np.testing.assert_array_equal(r["pool"][0], want)
-        assert r["max"] == 1.5
+        assert r["max"] == len(results) - 0.5
 
 
 @pytest.mark.parametrize("k", [1, 10, 64])
@@ -242,25 +255,30 @@ def test_packed_exchange_and_pool_fetch(results):
     emb = rng.standard_normal((nd, 32)).astype(np.float32)
     emb[5] = emb[4]
     emb[nd // 2 + 1] = emb[4]
-    q = rng.standard_normal((6, 32)).astype(np.float32)
+    q = rng.standard_normal((NQ, 32)).astype(np.float32)
     q[0] = emb[4]
     d, r = corc.dense_topk_f64(emb, q, 16)
     csr = corc.build_csr(toks, off, vocab)
     idf, _ = corc.bm25_idf(csr["df"], csr["first_key"], nd)
-    sc, rw = corc.bm25_topk(csr, idf, float(off[-1]) / nd, queries[:6], 10)
-    bq = 6 // WS
+    sc, rw = corc.bm25_topk(csr, idf, float(off[-1]) / nd, queries[:NQ], 10)
+    bq = NQ // len(results)
     for res in results:
         D, R, S, BR = res["xchg"]
         assert np.array_equal(R, r) and np.array_equal(D, d.astype(np.float32))
         assert np.array_equal(BR, rw) and np.array_equal(S, sc)
         blk = r[res["rank"] * bq:(res["rank"] + 1) * bq]
         np.testing.assert_array_equal(res["pool_block"], emb[blk])
+        want = emb[blk].copy()
+        want[:, -3:] = 0.0
+        np.testing.assert_array_equal(res["pool_block_pad"], want)
+        assert res["uneven"] == "ValueError"
 
 
 def test_errors_raise_on_every_rank_and_empty_shard_eps(results):
     """ADVICE r2: a local failure must not leave the other ranks blocked in the next collective;
     an empty shard (no vocabulary) joins the epsilon exchange with padded arrays."""
-    assert [r["raise"] for r in results] == ["RuntimeError", "ValueError"]
+    WS = len(results)
+    assert [r["raise"] for r in results] == ["RuntimeError", "ValueError"] + ["RuntimeError"] * (WS - 2)
     toks, off, vocab, _ = _corpus()
     nd = off.shape[0] - 1
     _, n0 = shard_range_cpu(nd, 0, WS)
