@@ -27,6 +27,7 @@ import hashlib
 import math
 import os
 import re
+import warnings
 from typing import Iterable, List, Optional
 
 import numpy as np
@@ -210,8 +211,66 @@ class E5MultilingualEmbedder:
         if os.environ.get("CM_E5_LEAN", "1") == "0":
             return self._encode_hf(input_ids, attention_mask, out=out)
         with torch.inference_mode():
-            hidden = self._lean_forward()(input_ids, attention_mask)
+            fwd = self._lean_forward()
+            g = self._small_batch_graph(input_ids, attention_mask)
+            if g is not None:
+                return g if out is None else out.copy_(g)
+            hidden = fwd(input_ids, attention_mask)
             return engine.meanpool_l2norm(hidden, attention_mask, self.normalize, out=out)
+
+    _SMALL_B, _SMALL_S = (8, 32)
+
+    def _small_batch_graph(self, ids, mask):
+        """Small fp32 batches (B <= 8, S <= 32: single queries) are launch-bound (~100 kernels of a
+        few us each): they replay a hipGraph of the K10 lean forward captured per (B, S bucket of
+        16 / 32), the tokens right-padded into the bucket and masked (key-masked HIP attention,
+        positions from the non-pad tokens, masked mean pool -- the padded batch semantics of the
+        reference's HF forward).  Returns a fresh (B, 768) tensor, or None where it does not apply
+        (CM_E5_SMALL_GRAPH=0 disables it)."""
+        import torch
+        B, S = ids.shape
+        if (not getattr(self, "f16x3", False) or B > self._SMALL_B or S > self._SMALL_S
+                or getattr(self, "_small_graph_failed", False)
+                or os.environ.get("CM_E5_SMALL_GRAPH", "1") == "0" or torch.cuda.is_current_stream_capturing()):
+            return None
+        Sb = 16 if S <= 16 else 32
+        cache = self.__dict__.setdefault("_small_graphs", {})
+        key = (B, Sb, ids.device)
+        ent = cache.get(key)
+        if ent is None:
+            pad = self.model.config.pad_token_id
+            g_ids = torch.full((B, Sb), pad, dtype=torch.long, device=ids.device)
+            g_mask = torch.zeros((B, Sb), dtype=torch.long, device=ids.device)
+            g_ids[:, 0] = 0
+            g_mask[:, 0] = 1
+            g_out = torch.empty((B, self.model.config.hidden_size), dtype=torch.float32, device=ids.device)
+            fwd = self._lean_forward()
+
+            def run():
+                hidden = fwd(g_ids, g_mask, padded=True)
+                engine.meanpool_l2norm(hidden, g_mask, self.normalize, out=g_out)
+
+            side = torch.cuda.Stream(device=ids.device)
+            side.wait_stream(torch.cuda.current_stream(ids.device))
+            with torch.cuda.stream(side):
+                run()
+            torch.cuda.current_stream(ids.device).wait_stream(side)
+            graph = torch.cuda.CUDAGraph()
+            try:
+                with torch.cuda.graph(graph):
+                    run()
+            except RuntimeError as e:   # capture refused: the eager forward from now on, said once
+                self._small_graph_failed = True
+                warnings.warn(f"E5 small-batch graph capture failed ({e}); using the eager forward")
+                return None
+            ent = cache[key] = (g_ids, g_mask, g_out, graph, pad)
+        g_ids, g_mask, g_out, graph, pad = ent
+        g_ids.fill_(pad)
+        g_mask.zero_()
+        g_ids[:, :S].copy_(ids)
+        g_mask[:, :S].copy_(mask)
+        graph.replay()
+        return g_out.clone()
 
     def _encode_hf(self, input_ids, attention_mask, out=None):
         """The Hugging Face XLM-R module forward + K6 pooling."""
@@ -269,11 +328,12 @@ class E5MultilingualEmbedder:
             def add_ln(x, r, g, b):
                 return F.layer_norm(x + r, (D,), g, b, eps)
 
-        def embed(ids, mask):
-            """word + position/type embeddings -> (x0 input of the embedding LayerNorm, residual, keep)."""
+        def embed(ids, mask, padded=False):
+            """word + position/type embeddings -> (x0 input of the embedding LayerNorm, residual, keep).
+            padded=True takes the padded-batch path without the host-side all-ones check (graphs)."""
             B, S = ids.shape
             keep = None
-            if mask is not None and not bool(mask.all()):
+            if mask is not None and (padded or not bool(mask.all())):
                 # padded rows (HF semantics): positions from the non-pad tokens
                 # (create_position_ids_from_input_ids), padded keys masked out of attention
                 npad = ids.ne(pad).int()
@@ -293,11 +353,11 @@ class E5MultilingualEmbedder:
             o = F.scaled_dot_product_attention(qkv[0], qkv[1], qkv[2], attn_mask=keep)
             return o.transpose(1, 2).reshape(B, S, D)
 
-        def fwd_f16x3(ids, mask=None):
+        def fwd_f16x3(ids, mask=None, padded=False):
             # K10 path: every GEMM operand is produced directly as split planes (K8 / attention /
             # the FFN-up epilogue write them), so the projections are pure LDS-DMA + MFMA kernels
             B, S = ids.shape
-            w0, pt, keep = embed(ids, mask)
+            w0, pt, keep = embed(ids, mask, padded)
             x, xp = engine.add_layernorm_split(w0, pt, emb.LayerNorm.weight, emb.LayerNorm.bias, eps, layers[0][1])
             short = fused_attn and S <= 64 and keep is None
             # padded batches (S <= 32): the same HIP attention with the key mask (CM_E5_MASKED_ATTN=0:
@@ -320,9 +380,9 @@ class E5MultilingualEmbedder:
                     x = add_ln(x, y, g2, bb2)
             return x.view(B, S, D)
 
-        def fwd(ids, mask=None):
+        def fwd(ids, mask=None, padded=False):
             B, S = ids.shape
-            w0, pt, keep = embed(ids, mask)
+            w0, pt, keep = embed(ids, mask, padded)
             x = add_ln(w0, pt, emb.LayerNorm.weight, emb.LayerNorm.bias)
             short = fused_attn and S <= 64 and keep is None
             for (wqkv, bqkv, wo, bo, g1, b1, wi, bi, w2, b2, g2, bb2) in layers:

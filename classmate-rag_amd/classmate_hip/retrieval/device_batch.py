@@ -1,13 +1,16 @@
-"""``HybridRetriever.retrieve_batch`` with the whole batch resident on the device.
+"""``HybridRetriever.retrieve`` / ``retrieve_batch`` with the whole batch resident on the device.
 
 The drop-in path (fusion.py) follows the reference's control flow per stage: the vector store
 returns result dicts with their embeddings, MMR runs over host copies of the pools, the BM25 store
 returns result dicts, and the merge matches items by id on the host (rag/retrieval/fusion.py:
-108-167).  For an unfiltered hybrid batch with MMR -- the configuration the reference's callers
-use (rag/pipeline/rag.py:549, tools/bench_ask.py:19-38) -- every one of those steps has a device
-form: cosine pool search (K1c/K1s), pool gather + MMR (K4), BM25 top-k (K2a/K2b/K2 + K3), pool
-preparation + RRF merge (K5).  This module chains them without a host round trip and builds result
-dicts only for the final top_k items of each query.
+108-167).  For a hybrid query with MMR -- the configuration the reference's callers use
+(rag/pipeline/rag.py:531-554: ``ask_question`` sends ONE question with ``filters.to_dict()``) --
+every one of those steps has a device form: where-filters as allow bitmaps (cm_filter_eval: Chroma
+semantics for the dense side, ``_matches_filter`` semantics with quirk Q4 for BM25), cosine pool
+search (K1c/K1s), pool gather + MMR (K4), BM25 top-k (K2a/K2b/K2 + K3; with a filter, K2f's
+statistics over the allowed candidates, quirk Q2), pool preparation + RRF merge (K5).  This module
+chains them without a host round trip and builds result dicts only for the final top_k items of
+each query.  Single questions are a batch of one (their E5 encode replays a small-batch graph).
 
 Id matching: the merge compares integer keys.  A document's key is its vector-store row; a BM25
 document that the vector store does not hold gets ``n_vector_rows + bm25_row``.  The BM25-row ->
@@ -51,12 +54,13 @@ class _KeyMap:
 
 
 def applicable(retr, filters, hybrid: bool) -> bool:
-    """The device batch path covers unfiltered hybrid retrieval with MMR over this package's stores
-    (anything else takes the host path)."""
+    """The device path covers hybrid retrieval with MMR over this package's stores, filtered or not
+    (anything else takes the host path).  With a filter, ``retrieve_batch`` may still decline
+    (None) when fewer vectors than the MMR pool pass it: the host path's k clamp covers that."""
     from .bm25 import BM25Store
     from .vector_store import GpuVectorStore
     vs, bm = retr.vector_store, retr.bm25_store
-    if filters or not hybrid or not retr.use_mmr:
+    if not hybrid or not retr.use_mmr:
         return False
     if not isinstance(vs, GpuVectorStore) or not isinstance(bm, BM25Store):
         return False
@@ -82,10 +86,43 @@ def _query_vectors(embedder, questions: Sequence[str], dev):
     return torch.from_numpy(q).to(dev)
 
 
-def retrieve_batch(retr, questions: Sequence[str], top_k: int) -> List[List[Dict[str, Any]]]:
-    """retr.retrieve_batch(questions, filters=None, top_k, hybrid=True) on the device (see module
-    docstring); the caller checked ``applicable``."""
+_ALLOW_CACHE_MAX = 64
+
+
+def _allow(meta, where, semantics: str, device: int, n_words: int, cache: dict):
+    """Device allow words + candidate count of ``where`` (engine.where_bits), cached per (metadata
+    version, filter): a caller repeating one filter -- ask_question's to_dict() -- pays the filter
+    program once per store change."""
+    import json
     import torch
+    try:
+        fkey = json.dumps(where, sort_keys=True, default=str)
+    except (TypeError, ValueError):
+        fkey = None
+    key = (id(meta), meta.version, semantics, fkey)
+    hit = cache.get(key) if fkey is not None else None
+    if hit is not None:
+        return hit
+    from .. import engine as E
+    words, n = E.where_bits(meta, where, semantics, device)
+    if not hasattr(words, "data_ptr"):
+        words = torch.from_numpy(np.ascontiguousarray(words).view(np.int32)).to(torch.device("cuda", device))
+    if words.numel() < n_words:             # rows past the metadata (never written): not allowed
+        words = torch.cat([words, torch.zeros(n_words - words.numel(), dtype=words.dtype, device=words.device)])
+    if fkey is not None:
+        if len(cache) >= _ALLOW_CACHE_MAX:
+            cache.clear()
+        cache[key] = (words, n)
+    return words, n
+
+
+def retrieve_batch(retr, questions: Sequence[str], top_k: int,
+                   filters: Optional[Dict[str, Any]] = None) -> Optional[List[List[Dict[str, Any]]]]:
+    """retr.retrieve_batch(questions, filters, top_k, hybrid=True) on the device (see module
+    docstring); the caller checked ``applicable``.  Returns None when a filter leaves fewer vectors
+    than the MMR pool (the host path then clamps k as the reference does)."""
+    import torch
+    from .filters import build_where_filter
     vs, bm = retr.vector_store, retr.bm25_store
     index = vs._index
     dev = torch.device("cuda", index.device)
@@ -93,6 +130,17 @@ def retrieve_batch(retr, questions: Sequence[str], top_k: int) -> List[List[Dict
     kv, kb = retr.k_vector, retr.k_bm25
     pool = max(kv, retr.mmr_max_pool)
     bm._ensure_index()
+    allow_v = allow_b = None
+    if filters:
+        cache = retr.__dict__.setdefault("_device_allow_cache", {})
+        chroma_where = build_where_filter(filters)
+        if chroma_where:
+            allow_v, n_ok = _allow(vs._meta, chroma_where, "chroma", index.device, (index.size + 31) // 32, cache)
+            if n_ok < pool:
+                return None
+        bm._ensure_meta()
+        allow_b, n_cand = _allow(bm._meta, filters, "bm25", index.device, (len(bm._id_list) + 31) // 32, cache)
+        kb = min(kb, n_cand)
     key = (id(vs), vs._version, id(bm), bm._version)   # the stores themselves, not only their counters
     km = getattr(retr, "_device_keymap", None)
     if km is None or km[0] != key:
@@ -102,7 +150,7 @@ def retrieve_batch(retr, questions: Sequence[str], top_k: int) -> List[List[Dict
     # E5 encode first (its launches return at once), so the host tokenizes the BM25 queries while
     # the device encodes; then dense pool + MMR
     q = _query_vectors(retr.embedder, questions, dev)
-    d, r = index.search_dev(q, pool)
+    d, r = index.search_dev(q, pool, allow=allow_v)
     vecs = index.gather_dev(r.reshape(-1)).view(nq, pool, index.dim)
     order = engine.mmr_dev(q, vecs, kv, float(retr.mmr_lambda))
     blank = np.array([not q_.strip() for q_ in questions], bool)
@@ -113,8 +161,16 @@ def retrieve_batch(retr, questions: Sequence[str], top_k: int) -> List[List[Dict
     # pinned, stream-ordered copies: a pageable copy would wait here for the encode and search
     q_terms = torch.from_numpy(flat).pin_memory().to(dev, non_blocking=True)
     q_off = torch.from_numpy(off).pin_memory().to(dev, non_blocking=True)
-    # BM25 top-k (whitespace-only queries: no BM25 list, bm25.py:178)
-    bs, br = bm._index.search_dev(q_terms, q_off, kb)
+    # BM25 top-k (whitespace-only queries: no BM25 list, bm25.py:178); with a filter, rank_bm25's
+    # statistics over the allowed candidates (K2f; no candidate: empty lists, bm25.py:187)
+    if allow_b is None:
+        bs, br = bm._index.search_dev(q_terms, q_off, kb)
+    elif kb > 0:
+        bm._index.prepare_filtered()            # the device log table (once per index)
+        bs, br = bm._index.search_filtered(q_terms, q_off, kb, allow_b)
+    else:
+        bs = torch.zeros((nq, 1), dtype=torch.float64, device=dev)
+        br = torch.full((nq, 1), -1, dtype=torch.int64, device=dev)
     bkeys = torch.where(br >= 0, km.bm2key_dev[br.clamp(min=0)], torch.full_like(br, -1))
     if blank.any():
         blank_dev = torch.from_numpy(blank).pin_memory().to(dev, non_blocking=True)

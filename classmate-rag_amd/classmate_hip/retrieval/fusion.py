@@ -5,9 +5,9 @@
 values; the arithmetic runs in HIP kernels (K4 MMR, K5 RRF merge) instead of
 Python/numpy.  ``HybridRetriever.retrieve_batch`` is the batched form: one
 embedder call, one dense search, one MMR launch, one BM25 launch and one RRF
-launch for the whole batch (per-query semantics unchanged); unfiltered hybrid
-batches stay on the device end to end (``device_batch``; CM_RETRIEVE_DEVICE=0
-takes the host path).
+launch for the whole batch (per-query semantics unchanged).  Hybrid MMR
+queries -- single or batched, filtered or not -- stay on the device end to end
+(``device_batch``; CM_RETRIEVE_DEVICE=0 takes the host path).
 """
 from __future__ import annotations
 
@@ -163,6 +163,11 @@ class HybridRetriever:
     def retrieve(self, *, question: str, filters: Optional[Mapping[str, object]] = None, top_k: int = 8,
                  hybrid: bool = True) -> List[Dict[str, object]]:
         raw_filters = filters or {}
+        if os.environ.get("CM_RETRIEVE_DEVICE", "1") != "0" and device_batch.applicable(self, raw_filters, hybrid):
+            # the device chain of retrieve_batch for a batch of one (equal dicts: tests/test_gpu_dropin.py)
+            out = device_batch.retrieve_batch(self, [question], top_k, raw_filters)
+            if out is not None:
+                return out[0]
         chroma_where = build_where_filter(raw_filters) if raw_filters else None
         bm_where = raw_filters or None
         bm25_res: List[Mapping[str, object]] = []
@@ -181,7 +186,9 @@ class HybridRetriever:
             return []
         raw_filters = filters or {}
         if os.environ.get("CM_RETRIEVE_DEVICE", "1") != "0" and device_batch.applicable(self, raw_filters, hybrid):
-            return device_batch.retrieve_batch(self, questions, top_k)   # whole batch on the device
+            out = device_batch.retrieve_batch(self, questions, top_k, raw_filters)   # whole batch on the device
+            if out is not None:
+                return out
         chroma_where = build_where_filter(raw_filters) if raw_filters else None
         bm_where = raw_filters or None
         k = self.k_vector if hybrid else max(top_k, self.k_vector)

@@ -162,29 +162,57 @@ def _check(got, want):
             assert abs(g[2] - w[2]) <= TOL
 
 
+def _path_spy(monkeypatch, path):
+    """path "device": count the device chain's answered calls; "host": CM_RETRIEVE_DEVICE=0."""
+    from classmate_hip.retrieval import device_batch
+    calls = []
+    if path == "host":
+        monkeypatch.setenv("CM_RETRIEVE_DEVICE", "0")
+        return calls
+    real = device_batch.retrieve_batch
+
+    def spy(*a, **kw):
+        out = real(*a, **kw)
+        calls.append(out is not None)
+        return out
+    monkeypatch.setattr(device_batch, "retrieve_batch", spy)
+    return calls
+
+
+@pytest.mark.parametrize("path", ["device", "host"])
 @pytest.mark.parametrize("fname", list(FILTERS) + ["none_vector_only"])
-def test_hybrid_retrieve(stores, corpus, golden, fname):
+def test_hybrid_retrieve(stores, corpus, golden, fname, path, monkeypatch):
+    """Single-query retrieve() against the reference-generated goldens, filtered cases included
+    (course_cs101 is ask_question's DocumentMetadata.to_dict() shape with None keys, quirk Q4), on
+    the device chain (retrieve_batch of one) and on the host per-stage path."""
     from classmate_hip.retrieval import HybridRetriever
     vs, bm, _ = stores
     retr = HybridRetriever(vector_store=vs, bm25_store=bm, embedder=PresetEmbedder(corpus["qtexts"], corpus["qvecs"]),
                            k_vector=10, k_bm25=10)
+    calls = _path_spy(monkeypatch, path)
     for q, want in zip(corpus["qtexts"], golden["retrieve"][fname]):
         if fname == "none_vector_only":
             got = retr.retrieve(question=q, filters=None, top_k=12, hybrid=False)
         else:
             got = retr.retrieve(question=q, filters=FILTERS[fname], top_k=10)
         _check(_rows(got), want)
+    if path == "device" and fname != "none_vector_only":
+        assert calls and (all(calls) or fname not in ("none", "course_cs101"))   # the device chain answered
 
 
-@pytest.mark.parametrize("fname", ["none", "course_cs101", "tags_exam"])
-def test_retrieve_batch_equals_retrieve(stores, corpus, golden, fname):
+@pytest.mark.parametrize("path", ["device", "host"])
+@pytest.mark.parametrize("fname", list(FILTERS))
+def test_retrieve_batch_equals_retrieve(stores, corpus, golden, fname, path, monkeypatch):
     from classmate_hip.retrieval import HybridRetriever
     vs, bm, _ = stores
     retr = HybridRetriever(vector_store=vs, bm25_store=bm, embedder=PresetEmbedder(corpus["qtexts"], corpus["qvecs"]),
                            k_vector=10, k_bm25=10)
+    calls = _path_spy(monkeypatch, path)
     batch = retr.retrieve_batch(questions=corpus["qtexts"], filters=FILTERS[fname], top_k=10)
     for got, want in zip(batch, golden["retrieve"][fname]):
         _check(_rows(got), want)
+    if path == "device":
+        assert calls == [True] or (len(calls) == 1 and fname not in ("none", "course_cs101"))
 
 
 def test_mmr_and_rrf_public_functions(corpus, golden):
@@ -351,6 +379,14 @@ def test_retrieve_batch_device_path_equals_host_path(corpus, monkeypatch, top_k)
     got = retr.retrieve_batch(questions=qtexts, top_k=top_k)
     monkeypatch.setenv("CM_RETRIEVE_DEVICE", "0")
     assert got == retr.retrieve_batch(questions=qtexts, top_k=top_k)
+    # single queries and filtered batches: the same device chain, equal dicts
+    for f in (None, FILTERS["course_cs101"], FILTERS["course_only"], {"course": "no-such-course"}):
+        monkeypatch.delenv("CM_RETRIEVE_DEVICE")
+        got1 = [retr.retrieve(question=q, filters=f, top_k=top_k) for q in qtexts]
+        gotb = retr.retrieve_batch(questions=qtexts, filters=f, top_k=top_k)
+        monkeypatch.setenv("CM_RETRIEVE_DEVICE", "0")
+        assert got1 == [retr.retrieve(question=q, filters=f, top_k=top_k) for q in qtexts], f
+        assert gotb == retr.retrieve_batch(questions=qtexts, filters=f, top_k=top_k), f
 
 
 @pytest.mark.gpu

@@ -618,6 +618,31 @@ def test_e5_lean_forward_fp32_matches_hf():
     torch.testing.assert_close(emb.encode_token_ids(ids, mask), emb._encode_hf(ids, mask), atol=2e-5, rtol=0)
 
 
+def test_e5_small_batch_graph_matches_hf(monkeypatch):
+    """Single queries / small batches (B <= 8, S <= 32) replay a hipGraph of the K10 lean forward
+    with the tokens padded into a 16 / 32 bucket and masked: equal to the Hugging Face fp32 module
+    and to the eager lean forward within 2e-5, ragged rows included; one graph per (B, bucket)."""
+    import torch
+    from classmate_hip.embeddings import E5MultilingualEmbedder
+    emb = E5MultilingualEmbedder.random_init(seed=4, device="cuda", num_layers=2, dtype="float32")
+    g = torch.Generator(device="cuda").manual_seed(11)
+    for B, S, cut in ((1, 7, None), (1, 16, None), (3, 20, 9), (8, 32, 5), (2, 17, 1)):
+        ids = torch.randint(5, 250002, (B, S), device="cuda", generator=g)
+        ids[:, 0] = 0
+        mask = torch.ones_like(ids)
+        if cut is not None:
+            mask[B - 1, cut:] = 0
+            ids[B - 1, cut:] = 1
+        got = emb.encode_token_ids(ids, mask)
+        got2 = emb.encode_token_ids(ids, mask)           # replay of the cached graph
+        torch.testing.assert_close(got, emb._encode_hf(ids, mask), atol=2e-5, rtol=0)
+        assert torch.equal(got, got2)
+        monkeypatch.setenv("CM_E5_SMALL_GRAPH", "0")
+        torch.testing.assert_close(got, emb.encode_token_ids(ids, mask), atol=2e-5, rtol=0)
+        monkeypatch.delenv("CM_E5_SMALL_GRAPH")
+    assert sorted((b, s) for b, s, _ in emb._small_graphs) == [(1, 16), (2, 32), (3, 32), (8, 32)]
+
+
 @pytest.mark.parametrize("S", [1, 7, 16, 24, 32, 33, 64])
 def test_short_attention_matches_torch(eng, S):
     """cm_short_attention == per-head softmax(q k^T / 8) v on the (B, S, 3, H, 64) QKV layout

@@ -320,18 +320,26 @@ def _free_port():
 
 
 def _bm25_docs(lo, hi, block=1 << 16):
-    """Zipf(1.07) tokens of documents [lo, hi), generated per 64k-doc block (shard-independent)."""
-    toks, lens = [], []
-    for b0 in range(lo - lo % block, hi, block):
+    """Zipf(1.07) tokens of documents [lo, hi), generated per 64k-doc block (shard-independent;
+    the draw is numpy Generator.choice(VOCAB, p=...)'s own: cdf + uniform + searchsorted, with the
+    cdf computed once and the blocks on a thread pool)."""
+    from concurrent.futures import ThreadPoolExecutor
+    p = 1.0 / np.arange(1, VOCAB + 1) ** 1.07
+    cdf = np.cumsum(p / p.sum())
+    cdf /= cdf[-1]
+
+    def one(b0):
         rng = np.random.default_rng([77, b0 // block])
         ln = np.maximum(rng.poisson(60, block), 1)
-        p = 1.0 / np.arange(1, VOCAB + 1) ** 1.07
-        t = rng.choice(VOCAB, size=int(ln.sum()), p=p / p.sum()).astype(np.int32)
+        t = cdf.searchsorted(rng.random(int(ln.sum())), side="right").astype(np.int32)
         off = np.concatenate([[0], np.cumsum(ln)])
         a, b = max(lo, b0) - b0, min(hi, b0 + block) - b0
-        toks.append(t[off[a]:off[b]])
-        lens.append(ln[a:b])
-    lens = np.concatenate(lens)
+        return t[off[a]:off[b]], ln[a:b]
+
+    with ThreadPoolExecutor(max_workers=min(8, os.cpu_count() or 1)) as ex:
+        parts = list(ex.map(one, range(lo - lo % block, hi, block)))
+    toks = [t for t, _ in parts]
+    lens = np.concatenate([ln for _, ln in parts])
     off = np.zeros(lens.shape[0] + 1, np.int64)
     off[1:] = np.cumsum(lens)
     return np.concatenate(toks), off
