@@ -70,6 +70,9 @@ def parse_args():
     ap.add_argument("--dense-legs", type=int, default=1,
                     help="hybrid mode: also time the north_star dense configs -- C2' (this 10M shard, B=16, "
                          "k=10, the >=80%% HBM target) and C2 (a 1M-chunk shard, B=256, k=10)")
+    ap.add_argument("--ingest-leg", type=int, default=1,
+                    help="hybrid mode: also time BASELINE configs[2]'s passage encode at the reference's fp32 "
+                         "(256 chunks x --seq-len tokens per step; reported as ingest_fp32 + rooflines.e5_ingest)")
     ap.add_argument("--no-e5", action="store_true", help="use perturbed corpus rows as query embeddings")
     ap.add_argument("--no-graph", action="store_true", help="run the E5 query encode eagerly (no hipGraph)")
     ap.add_argument("--serial", action="store_true", help="run BM25 on the main stream (no overlap with E5 + dense)")
@@ -400,6 +403,9 @@ def main():
         e5 = main_e5
     if args.mode == "hybrid" and args.dense_legs:
         legs.update(dense_legs(args, dense, N, D, dev, ws))
+    if use_e5 and args.ingest_leg:
+        legs["ingest_fp32"], roofs["e5_ingest"] = ingest_leg(args, e5["emb"] if e5["dtype"] == "float32" else None,
+                                                           dev, ws, rank)
 
     out = {
         "metric": METRIC if args.mode == "hybrid" else f"dense cosine top-{K} queries/sec, {N}x{D} fp32",
@@ -570,6 +576,55 @@ def dense_legs(args, dense, N, D, dev, ws):
     del d1
     torch.cuda.empty_cache()
     return legs
+
+
+def ingest_leg(args, emb, dev, ws, rank):
+    """BASELINE configs[2] beside the headline: the passage encode of 256 chunks x --seq-len tokens
+    per step at the reference's fp32 (K10 GEMMs + attention + K8 + K6 pooling), chunks/s over all
+    ranks (data-parallel replicas) and the encode against the f16 MFMA peak with the
+    issued flops (3 x the fp32-equivalent 12 (24 S d^2 + 4 S^2 d) per chunk)."""
+    import torch
+    from classmate_hip import parallel
+    from classmate_hip.embeddings import E5MultilingualEmbedder
+    if emb is None:
+        emb = E5MultilingualEmbedder.random_init(seed=0, device=str(dev), num_layers=args.e5_layers, dtype="float32")
+    B, S = 256, args.seq_len
+    g = torch.Generator(device="cuda").manual_seed(args.seed + 101 + rank)
+    ids = torch.randint(5, 250002, (B, S), device=dev, generator=g)
+    ids[:, 0] = 0
+    ids[:, -1] = 2
+    mask = torch.ones_like(ids)
+    out = torch.empty((B, 768), dtype=torch.float32, device=dev)
+    for _ in range(max(1, min(args.warmup, 2))):
+        emb.encode_token_ids(ids, mask, out=out)
+    steps = max(3, min(args.steps, 10))
+    torch.cuda.synchronize()
+    if ws > 1:
+        torch.distributed.barrier()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record()
+    for _ in range(steps):
+        emb.encode_token_ids(ids, mask, out=out)
+    e1.record()
+    torch.cuda.synchronize()
+    if ws > 1:
+        torch.distributed.barrier()
+    el = parallel.max_over_ranks(time.perf_counter() - t0, device=dev)
+    ms = e0.elapsed_time(e1) / steps
+    alg = float(B) * args.e5_layers * (24.0 * S * 768 ** 2 + 4.0 * S * S * 768)
+    issued = 3.0 * alg
+    leg = {"value": B * steps * ws / el, "unit": "chunks/s", "ms_per_step": el / steps * 1e3, "steps": steps,
+           "config": {"workload": "E5-base passage encode (BASELINE configs[2] shape)", "chunks_per_step": B * ws,
+                      "seq_len": S, "e5_forward": "fp32 (K10 f16x3)", "parallelism": f"replicas x{ws}"},
+           "fp32_equiv_tflops": alg / (ms * 1e-3) / 1e12}
+    roof = {"bound": "mfma", "achieved": issued / (ms * 1e-3) / 1e12, "peak": PEAK_F16_MFMA_TFLOPS,
+            "unit": "TFLOP/s", "frac": issued / (ms * 1e-3) / 1e12 / PEAK_F16_MFMA_TFLOPS, "traffic": None,
+            "avg_launch_ms": ms, "kernel": "E5 passage encode (K10 f16x3 GEMMs + attention + K8 + K6), whole forward",
+            "algorithmic_per_launch": {"flops_fp32_equiv": alg, "flops_issued": issued, "chunks": B, "tokens": S,
+                                       "layers": args.e5_layers}}
+    log(f"ingest_fp32: {leg['value']:.0f} chunks/s ({ms:.2f} ms per {B} x {S} tokens, {roof['frac']:.3f} of f16 peak)")
+    return leg, roof
 
 
 def _pmc_traffic(args, which):
@@ -759,7 +814,9 @@ def run_e2e(args, rank, ws, dev):
         texts.extend(blob[i * L:(i + 1) * L - 1].decode("ascii") for i in range(c1 - c0))
         del words, blob
     ids = [f"c{i}" for i in range(N)]
-    metas = [{"course": f"C{i % 16}", "week": int(i % 12), "language": "en"} for i in range(N)]
+    # a quarter of the chunks carry no course: ask_question's filters.to_dict() keeps course=None, and
+    # BM25's _matches_filter then admits exactly those (quirk Q4, rag/retrieval/bm25.py:103-106)
+    metas = [({"course": f"C{i % 16}"} if i % 4 else {}) | {"week": int(i % 12), "language": "en"} for i in range(N)]
     log(f"e2e corpus: {N} chunks x {args.e2e_words} words ({time.perf_counter() - t_setup:.1f}s)")
     g = torch.Generator(device="cuda").manual_seed(args.seed * 1000)
     emb = torch.randn(N, D, device=dev, generator=g)
@@ -806,17 +863,39 @@ def run_e2e(args, rank, ws, dev):
         import pstats
         prof.disable()
         pstats.Stats(prof, stream=sys.stderr).sort_stats("cumulative").print_stats(40)
-    for i in range(3):                                 # batch-1 shapes: first-call setup
-        retr.retrieve(question=qs[-1 - i], top_k=K)
-    lat = []
-    for i in range(args.e2e_latency_queries):
-        t1 = time.perf_counter()
-        retr.retrieve(question=qs[i], top_k=K)
-        lat.append((time.perf_counter() - t1) * 1e3)
-    lat.sort()
+    # single-query retrieve() latency: unfiltered, and with ask_question's filters
+    # (rag/pipeline/rag.py:548-554: DocumentMetadata(...).to_dict(), None keys kept -- quirk Q4)
+    none_keys = {"course": None, "unit": None, "author": None, "semester": None, "source_path": None,
+                 "created_at": None}
+    shapes = {"unfiltered": None, "to_dict_default": none_keys, "to_dict_course": dict(none_keys, course="C3")}
+    lat_all, paths = {}, {}
+    for name, f in shapes.items():
+        calls = []
+        real = device_batch.retrieve_batch
+
+        def spy(*a, **kw):
+            out = real(*a, **kw)
+            calls.append(out is not None)
+            return out
+        device_batch.retrieve_batch = spy
+        try:
+            for i in range(3):                             # batch-1 shapes: first-call setup
+                retr.retrieve(question=qs[-1 - i], filters=f, top_k=K)
+            lat = []
+            for i in range(args.e2e_latency_queries):
+                t1 = time.perf_counter()
+                retr.retrieve(question=qs[i], filters=f, top_k=K)
+                lat.append((time.perf_counter() - t1) * 1e3)
+        finally:
+            device_batch.retrieve_batch = real
+        lat.sort()
+        lat_all[name] = {"p50": lat[len(lat) // 2], "p99": lat[min(len(lat) - 1, int(len(lat) * 0.99))],
+                         "n": len(lat), "filters": f}
+        paths[name] = "device chain" if calls and all(calls) else "host (per-stage dicts)"
+        log(f"retrieve() {name}: p50 {lat_all[name]['p50']:.2f} ms, p99 {lat_all[name]['p99']:.2f} ms ({paths[name]})")
+    lat = lat_all
     qps = B * args.steps / elapsed
-    log(f"{args.steps} retrieve_batch calls in {elapsed:.3f}s -> {qps:.1f} q/s; retrieve() p50 "
-        f"{lat[len(lat) // 2]:.2f} ms, p99 {lat[min(len(lat) - 1, int(len(lat) * 0.99))]:.2f} ms")
+    log(f"{args.steps} retrieve_batch calls in {elapsed:.3f}s -> {qps:.1f} q/s")
     out = {
         "metric": f"drop-in HybridRetriever.retrieve_batch queries/sec (strings -> result dicts), {N} chunks",
         "value": qps, "unit": "queries/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
@@ -825,8 +904,9 @@ def run_e2e(args, rank, ws, dev):
         "data": "synthetic (seeded): Zipf-word chunks, random unit embeddings, random-init E5-base weights",
         "config": {"workload": "drop-in retrieve_batch (E5 query encode + cosine pool 24 + MMR 8 + BM25 8 + RRF)",
                    "chunks": N, "words_per_chunk": args.e2e_words, "global_batch": B, "top_k": K, "dim": D},
-        "retrieve_latency_ms": {"p50": lat[len(lat) // 2], "p99": lat[min(len(lat) - 1, int(len(lat) * 0.99))],
-                                "n": len(lat)},
+        "retrieve_latency_ms": lat["unfiltered"],
+        "retrieve_latency_ms_by_filter": lat,
+        "retrieve_paths": paths,
         "results_returned": n_res, "setup_s": time.perf_counter() - t_setup,
         "retrieve_batch_path": ("device-resident (retrieval/device_batch.py)"
                                 if os.environ.get("CM_RETRIEVE_DEVICE", "1") != "0" and device_batch.applicable(retr, {}, True)

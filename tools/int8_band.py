@@ -119,40 +119,59 @@ def main():
     print("row stats", res["row_stats"], flush=True)
 
     for qname, Q in qsets.items():
-        for fmt, rf in (("f16", "f16"), ("i8", "i8"), ("i8split", "i8"), ("fp8", "fp8")):
+        for fmt, rf in (("f16", "f16"), ("i8", "i8"), ("i8split", "i8")):
             qt = coarse_q(fmt, Q)
             eq = (Q - qt).norm(dim=1)
             qn = qt.norm(dim=1)
             mx_c, mx_e, _ = row_stats[rf]
             E = (eq * mx_c + qn * mx_e + eq * mx_e) * 1.001 + 2e-6
+            # per-row bound: E_r = ||e_q|| ||c~_r|| + ||q~|| ||e_c,r|| + ||e_q|| ||e_c,r|| (a row
+            # test coarse - E_r; the k'-th threshold from coarse + E_r)
+            def e_row(xt, e):
+                cn, en = xt.norm(dim=1), e.norm(dim=1)
+                return ((eq[:, None] * cn[None] + qn[:, None] * en[None] + eq[:, None] * en[None]) * 1.001 + 2e-6)
             # pass 1: k'-th largest coarse sim (full and 1/64, 1/16 samples) and the exact k'-th sim
             topc = torch.full((B, 0), -2.0, device=dev)
-            tops = {64: torch.full((B, 0), -2.0, device=dev), 16: torch.full((B, 0), -2.0, device=dev)}
+            topr = torch.full((B, 0), -2.0, device=dev)            # k'-th largest (coarse - E_r)
+            tops = {64: torch.full((B, 0), -2.0, device=dev), 16: torch.full((B, 0), -2.0, device=dev),
+                    8: torch.full((B, 0), -2.0, device=dev)}
+            topsr = {s_: torch.full((B, 0), -2.0, device=dev) for s_ in tops}
             tope = torch.full((B, 0), -2.0, device=dev)
             for r0 in range(0, N, chunk):
                 x = X[r0:r0 + chunk]
-                xt, _ = coarse_rows(rf, x)
+                xt, ex = coarse_rows(rf, x)
                 cs = qt @ xt.T                                   # (B, m) coarse
+                lo = cs - e_row(xt, ex)
                 es = Q @ x.T
                 topc = torch.cat([topc, cs], 1).topk(P, dim=1).values
+                topr = torch.cat([topr, lo], 1).topk(P, dim=1).values
                 tope = torch.cat([tope, es], 1).topk(P, dim=1).values
                 for s in tops:
                     idx = torch.arange((-r0) % s, x.shape[0], s, device=dev)
                     tops[s] = torch.cat([tops[s], cs[:, idx]], 1).topk(P, dim=1).values
+                    topsr[s] = torch.cat([topsr[s], lo[:, idx]], 1).topk(P, dim=1).values
+                del lo
             kth = topc[:, -1]
             thr = {"band": kth - 2 * E, **{f"cand@{s}": tops[s][:, -1] - 2 * E for s in tops}}
-            cnt = {k: torch.zeros(B, device=dev, dtype=torch.int64) for k in thr}
+            # per-row E: a row is in the band when coarse + E_r >= the k'-th largest (coarse - E_r)
+            thr_r = {"band_rowE": topr[:, -1], **{f"cand_rowE@{s}": topsr[s][:, -1] for s in topsr}}
+            cnt = {k: torch.zeros(B, device=dev, dtype=torch.int64) for k in list(thr) + list(thr_r)}
             for r0 in range(0, N, chunk):
-                xt, _ = coarse_rows(rf, X[r0:r0 + chunk])
+                xt, ex = coarse_rows(rf, X[r0:r0 + chunk])
                 cs = qt @ xt.T
                 for k, t in thr.items():
                     cnt[k] += (cs >= t[:, None]).sum(1)
+                hi = cs + e_row(xt, ex)
+                for k, t in thr_r.items():
+                    cnt[k] += (hi >= t[:, None]).sum(1)
+                del hi
             out = {"E_mean": float(E.mean()), "E_max": float(E.max()),
                    "kth_exact_sim_mean": float(tope[:, -1].mean())}
             for k, c in cnt.items():
                 c = c.float()
                 out[k] = {"mean": float(c.mean()), "p50": float(c.median()), "max": float(c.max())}
             out["band_rerank_bytes_per_batch"] = float(cnt["band"].sum()) * D * 4
+            out["band_rowE_rerank_bytes_per_batch"] = float(cnt["band_rowE"].sum()) * D * 4
             res[f"{qname}/{fmt}"] = out
             print(qname, fmt, json.dumps(out), flush=True)
     Path(a.out).parent.mkdir(parents=True, exist_ok=True)
