@@ -126,6 +126,7 @@ SIGNATURES = {
     "cm_add_layernorm_split": (c_int, c_vp, c_vp, c_i64, c_vp, c_vp, c_i64, c_i32, c_f32, c_vp, c_f32, c_vp, c_vp),
     "cm_short_attention_split": (c_int, c_vp, c_i32, c_i32, c_i32, c_i32, c_f32, c_f32, c_vp, c_vp),
     "cm_short_attention_split_masked": (c_int, c_vp, c_i32, c_i32, c_i32, c_i32, c_f32, c_f32, c_vp, c_vp, c_vp),
+    "cm_long_attention_split": (c_int, c_vp, c_i32, c_i32, c_i32, c_i32, c_f32, c_f32, c_vp, c_vp, c_vp),
 }
 CM_EPI_BIAS, CM_EPI_BIAS_GELU, CM_EPI_PLANES_GELU = 0, 1, 2
 

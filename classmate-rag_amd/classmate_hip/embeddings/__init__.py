@@ -359,16 +359,21 @@ class E5MultilingualEmbedder:
             B, S = ids.shape
             w0, pt, keep = embed(ids, mask, padded)
             x, xp = engine.add_layernorm_split(w0, pt, emb.LayerNorm.weight, emb.LayerNorm.bias, eps, layers[0][1])
-            short = fused_attn and S <= 64 and keep is None
-            # padded batches (S <= 32): the same HIP attention with the key mask (CM_E5_MASKED_ATTN=0:
-            # key-masked SDPA)
-            masked = (fused_attn and keep is not None and S <= 32
-                      and os.environ.get("CM_E5_MASKED_ATTN", "1") != "0")
-            km = mask.to(torch.int32).contiguous() if masked else None
+            # S <= 32: K9s (one wave per (sequence, head)); longer sequences -- passages up to 512
+            # tokens -- K9L (64-key chunks, online softmax); both key-masked on padded batches and both
+            # write the O projection's planes.  CM_E5_LONG_ATTN=0 / CM_E5_MASKED_ATTN=0 restore torch
+            # SDPA + a split pass for those cases.
+            short = fused_attn and S <= 32 and (keep is None or os.environ.get("CM_E5_MASKED_ATTN", "1") != "0")
+            long_ = fused_attn and S > 32 and os.environ.get("CM_E5_LONG_ATTN", "1") != "0"
+            km = mask.to(torch.int32).contiguous() if (short or long_) and keep is not None else None
             for li, (wqkv, a_qkv, wo, a_o, g1, b1, wi, a_i, w2, a_2, g2, bb2) in enumerate(layers):
                 qkv = engine.linear_f16x3(xp, wqkv)
-                if short or masked:   # HIP attention reads the QKV output in place and writes the O operand planes
+                if short:   # HIP attention reads the QKV output in place and writes the O operand planes
                     op = engine.short_attention_split(qkv.view(B, S, 3 * D), H, scale, a_o, key_mask=km)
+                elif long_:
+                    op = engine.long_attention_split(qkv.view(B, S, 3 * D), H, scale, a_o, key_mask=km)
+                elif fused_attn and S <= 64 and keep is None:
+                    op = engine.short_attention_split(qkv.view(B, S, 3 * D), H, scale, a_o)
                 else:
                     op = engine.split_rows(sdpa(qkv, B, S, keep), a_o)
                 x, xp = engine.add_layernorm_split(x, engine.linear_f16x3(op, wo), g1, b1, eps, a_i)

@@ -790,6 +790,25 @@ def short_attention_split(qkv, heads: int, scale: float, a_scale: float, key_mas
             "cm_short_attention_split_masked")
     return p
 
+def long_attention_split(qkv, heads: int, scale: float, a_scale: float, key_mask=None) -> Planes:
+    """Attention of any sequence length at fp32 accuracy (K9L, cm_long_attention_split) writing the
+    context * a_scale as K10 Planes (B*S x heads*64).  qkv: fp32 (B, S, 3*heads*64); key_mask:
+    optional int32 (B, S) on the device, nonzero = attend (padded keys leave the softmax)."""
+    B, S, F3 = qkv.shape
+    if F3 != 3 * heads * 64 or not 0 < S <= 4096 or qkv.dtype != torch.float32:
+        raise ValueError("qkv must be fp32 (B, 0 < S <= 4096, 3*heads*64)")
+    qkv = qkv.contiguous()
+    if key_mask is not None:
+        if tuple(key_mask.shape) != (B, S) or key_mask.dtype != torch.int32 or key_mask.device != qkv.device:
+            raise ValueError("key_mask must be int32 (B, S) on the qkv device")
+        key_mask = key_mask.contiguous()
+    p = Planes(B * S, heads * 64, a_scale, qkv.device)
+    L.check(L.fn["cm_long_attention_split"](L.ptr(qkv), B, S, heads, 64, float(scale), p.scale,
+                                            L.ptr(key_mask) if key_mask is not None else None, L.ptr(p.data),
+                                            _stream(qkv.device.index)), "cm_long_attention_split")
+    return p
+
+
 # ---------------------------------------------------------------------------
 # Where-filters on the device (SURVEY §8f-2): retrieval.filters compiles, cm_filter_eval runs.
 def filter_bits(prog, device: Optional[int] = None):

@@ -589,6 +589,230 @@ __global__ void __launch_bounds__(64) short_attention_f16x3_kernel(const float *
   }
 }
 
+// K9L: fp32-accurate attention for sequences of any length (passages: S up to 512, padded or not)
+// on the K10 path, replacing torch SDPA + a split pass.  One workgroup of 4 waves per (sequence,
+// head, block of 64 queries), 16 queries per wave; the keys stream through LDS in chunks of 64 with
+// a flash-style online softmax (running max m and sum l per query, in fp32).  Per chunk the
+// workgroup loads K and V once, splits them after exact power-of-two scales of the chunk's max|K| /
+// max|V| (as K9s does per sequence: every lo half stays a normal f16) into MFMA fragment order in
+// LDS: K as the A operand of S^T = K Q^T, V in the permuted key order that lets the S^T accumulator
+// be the P operand of O = P V (short_attention_f16x3_kernel's trick).  Products are lo.hi + hi.lo +
+// hi.hi on v_mfma_f32_16x16x32_f16 (K10's split precision); P = exp(s - m) <= 1 is split after a
+// 2^14 scale; each chunk's P V lands in a fresh accumulator and joins the running output as
+// o = o alpha + (P V) / (2^14 sv) in fp32.  The context is written as K10 planes of o * a_scale.
+constexpr int kLaKeys = 64;  // keys per chunk
+
+__global__ void __launch_bounds__(256) long_attention_f16x3_kernel(const float *__restrict__ qkv, int S, int H,
+                                                                   float scale, float a_scale,
+                                                                   const int32_t *__restrict__ key_mask,
+                                                                   _Float16 *__restrict__ planes) {
+  constexpr float kPScale = 16384.f;
+  constexpr int OST = kAttnDh + 4;                      // output image row stride (floats)
+  // [kt 4][st 2][hi/lo][lane 64][8 halves] K fragments, then [u 2][dt 4][hi/lo][lane][8] V fragments;
+  // after the last chunk the same bytes hold the 4 waves' 16 x 64 fp32 output images
+  __shared__ __attribute__((aligned(16))) _Float16 lds[2 * 16 * 512];
+  __shared__ float red[2][4];
+  __shared__ uint32_t kbits[2];
+  _Float16 *kst = lds, *vst = lds + 16 * 512;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, c = lane & 15;
+  const int nqb = (S + 63) >> 6;
+  const int qb = (int)(blockIdx.x % nqb);
+  const int h = (int)((blockIdx.x / nqb) % H);
+  const int64_t b = blockIdx.x / ((int64_t)nqb * H);
+  const int64_t tok = 3LL * H * kAttnDh;
+  const float *base = qkv + b * S * tok + (int64_t)h * kAttnDh;
+  const float *kbp = base + (int64_t)H * kAttnDh;
+  const float *vbp = base + 2LL * H * kAttnDh;
+  const int q0 = qb * 64 + wave * 16;
+  // Q fragments (B operand): lane (g, c) = query q0 + c, dims 32 st + 8 g .. + 7
+  float qx[2][8];
+  float mq = 0.f;
+#pragma unroll
+  for (int st = 0; st < 2; ++st) {
+    load_frag8(base + (int64_t)(q0 + c) * tok + 32 * st + 8 * g, q0 + c < S, qx[st]);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) mq = fmaxf(mq, fabsf(qx[st][e]));
+  }
+  const float sq = pow2_scale_for(wave_max(mq));
+  h16x8_t qh[2], ql[2];
+#pragma unroll
+  for (int st = 0; st < 2; ++st) split_frag8(qx[st], sq, qh[st], ql[st]);
+
+  float m_run = -INFINITY, l_run = 0.f;               // per query column c (same in every g)
+  f32x4_t o_run[4];                                   // [dt]: O[query 4 g + r][dim 16 dt + c]
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) o_run[dt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  const int vk = 4 * (tid >> 4), vd = 4 * (tid & 15);  // V staging: keys vk .. + 3, dims vd .. + 3
+
+  for (int k0 = 0; k0 < S; k0 += kLaKeys) {
+    // ---- the chunk's K (two fragment combos per thread) and V rows, their maxima, the key mask
+    float kx[2][8];
+    float mk = 0.f, mv = 0.f;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int cb = tid + 256 * i, cc = cb & 15, gg = (cb >> 4) & 3, st = (cb >> 6) & 1, kt = cb >> 7;
+      const int key = k0 + 16 * kt + cc;
+      load_frag8(kbp + (int64_t)key * tok + 32 * st + 8 * gg, key < S, kx[i]);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) mk = fmaxf(mk, fabsf(kx[i][e]));
+    }
+    float4 vv[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int key = k0 + vk + j;
+      vv[j] = key < S ? *reinterpret_cast<const float4 *>(vbp + (int64_t)key * tok + vd) : make_float4(0.f, 0.f, 0.f, 0.f);
+      mv = fmaxf(mv, fmaxf(fmaxf(fabsf(vv[j].x), fabsf(vv[j].y)), fmaxf(fabsf(vv[j].z), fabsf(vv[j].w))));
+    }
+    mk = wave_max(mk);
+    mv = wave_max(mv);
+    if (lane == 0) {
+      red[0][wave] = mk;
+      red[1][wave] = mv;
+    }
+    if (wave == 0) {
+      const int key = k0 + lane;
+      const bool ok = key < S && (!key_mask || key_mask[b * S + key] != 0);
+      const uint64_t bits = __ballot(ok);
+      if (lane == 0) {
+        kbits[0] = (uint32_t)bits;
+        kbits[1] = (uint32_t)(bits >> 32);
+      }
+    }
+    __syncthreads();                                  // maxima + mask published; previous chunk's reads done
+    const float sk = pow2_scale_for(fmaxf(fmaxf(red[0][0], red[0][1]), fmaxf(red[0][2], red[0][3])));
+    const float sv = pow2_scale_for(fmaxf(fmaxf(red[1][0], red[1][1]), fmaxf(red[1][2], red[1][3])));
+    // the mask is read before the staging barrier: wave 0 rewrites it for the next chunk as soon as
+    // every wave has passed that barrier
+    const uint64_t kb = (uint64_t)kbits[0] | ((uint64_t)kbits[1] << 32);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int cb = tid + 256 * i, cc = cb & 15, gg = (cb >> 4) & 3, st = (cb >> 6) & 1, kt = cb >> 7;
+      h16x8_t hh, ll;
+      split_frag8(kx[i], sk, hh, ll);
+      const int o = ((kt * 2 + st) * 2) * 512 + (gg * 16 + cc) * 8;
+      *reinterpret_cast<h16x8_t *>(kst + o) = hh;
+      *reinterpret_cast<h16x8_t *>(kst + o + 512) = ll;
+    }
+    {
+      // V fragment (u, dt): lane (g', c') holds keys pi(8 g' + e) of 32-key step u, dim 16 dt + c';
+      // pi(8 g' + e) = 4 g' + e (e < 4), 16 + 4 g' + e - 4 (e >= 4): this thread's 4 keys are 4
+      // consecutive e of one lane per dim
+      const int kk = vk & 31, u = vk >> 5, gv = (kk & 15) >> 2, e0 = (kk >> 4) << 2, dt = vd >> 4;
+#pragma unroll
+      for (int e4 = 0; e4 < 4; ++e4) {
+        const float x4[4] = {(&vv[0].x)[e4], (&vv[1].x)[e4], (&vv[2].x)[e4], (&vv[3].x)[e4]};
+        _Float16 hh[4], ll[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) f16x3_split1(x4[j] * sv, hh[j], ll[j]);
+        const int o = ((u * 4 + dt) * 2) * 512 + (gv * 16 + (vd & 15) + e4) * 8 + e0;
+        *reinterpret_cast<uint2 *>(vst + o) = *reinterpret_cast<const uint2 *>(hh);
+        *reinterpret_cast<uint2 *>(vst + o + 512) = *reinterpret_cast<const uint2 *>(ll);
+      }
+    }
+    __syncthreads();                                  // fragments staged
+    // ---- S^T = K Q^T: sc[kt] lane (g, c) = keys 16 kt + 4 g + r, query c
+    f32x4_t sc[4];
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt) {
+      f32x4_t a = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int st = 0; st < 2; ++st) {
+        const h16x8_t kh = *reinterpret_cast<const h16x8_t *>(kst + ((kt * 2 + st) * 2) * 512 + lane * 8);
+        const h16x8_t kl = *reinterpret_cast<const h16x8_t *>(kst + ((kt * 2 + st) * 2 + 1) * 512 + lane * 8);
+        a = mfma3(kh, kl, qh[st], ql[st], a);
+      }
+      sc[kt] = a;
+    }
+    const float lscale = scale / (sq * sk);           // exact power-of-two ratio times scale
+    float mloc = -INFINITY;
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int j = 16 * kt + 4 * g + r;
+        const float v = ((kb >> j) & 1ull) ? sc[kt][r] * lscale : -INFINITY;
+        sc[kt][r] = v;
+        mloc = fmaxf(mloc, v);
+      }
+    mloc = fmaxf(mloc, __shfl_xor(mloc, 16));
+    mloc = fmaxf(mloc, __shfl_xor(mloc, 32));
+    const float m_new = fmaxf(m_run, mloc);
+    const float alpha = m_new == -INFINITY ? 0.f : __expf(m_run - m_new);
+    float psum = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float v = sc[kt][r];
+        const float p = v == -INFINITY ? 0.f : __expf(v - m_new);
+        sc[kt][r] = p;
+        psum += p;
+      }
+    psum += __shfl_xor(psum, 16);
+    psum += __shfl_xor(psum, 32);
+    l_run = l_run * alpha + psum;
+    m_run = m_new;
+    // P fragments of the two 32-key steps (A operand: row = query c, k-slot e = key pi(8 g + e))
+    h16x8_t ph[2], pl[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        _Float16 hh, ll;
+        f16x3_split1(sc[2 * u + (e >> 2)][e & 3] * kPScale, hh, ll);
+        ph[u][e] = hh;
+        pl[u][e] = ll;
+      }
+    float ar[4];                                      // alpha of query 4 g + r (held by lane c = 4 g + r)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) ar[r] = __shfl(alpha, 4 * g + r);
+    const float inv_pv = 1.f / (kPScale * sv);        // exact power of two
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      f32x4_t oc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const h16x8_t vh = *reinterpret_cast<const h16x8_t *>(vst + ((u * 4 + dt) * 2) * 512 + lane * 8);
+        const h16x8_t vl = *reinterpret_cast<const h16x8_t *>(vst + ((u * 4 + dt) * 2 + 1) * 512 + lane * 8);
+        oc = mfma3(ph[u], pl[u], vh, vl, oc);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o_run[dt][r] = o_run[dt][r] * ar[r] + oc[r] * inv_pv;
+    }
+  }
+  __syncthreads();                                    // every wave's last fragment reads are done
+  // ---- O / l * a_scale -> this wave's 16 x 64 image -> K10 planes (16-byte slots)
+  float *oimg = reinterpret_cast<float *>(lds) + wave * 16 * OST;
+  float lr[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) lr[r] = __shfl(l_run, 4 * g + r);
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      oimg[(4 * g + r) * OST + 16 * dt + c] = lr[r] > 0.f ? o_run[dt][r] / lr[r] * a_scale : 0.f;
+  __syncthreads();
+  const int kb32 = H * kAttnDh / 32;
+#pragma unroll
+  for (int u2 = 0; u2 < 2; ++u2) {
+    const int t = lane + 64 * u2, i = t >> 3, s8 = t & 7;
+    if (q0 + i < S) {
+      h16x8_t hh, ll;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        _Float16 a, b2;
+        f16x3_split1(oimg[i * OST + 8 * s8 + e], a, b2);
+        hh[e] = a;
+        ll[e] = b2;
+      }
+      const int64_t off = f16x3_plane_off(b * S + q0 + i, h * kAttnDh + 8 * s8, kb32);
+      *reinterpret_cast<h16x8_t *>(planes + off) = hh;
+      *reinterpret_cast<h16x8_t *>(planes + off + 512) = ll;
+    }
+  }
+}
+
 }  // namespace cm
 
 using namespace cm;
@@ -680,6 +904,21 @@ extern "C" int cm_short_attention_split(const float *qkv_dev, int32_t B, int32_t
   else
     hipLaunchKernelGGL((short_attention_kernel<float, true>), dim3((unsigned)((int64_t)B * H)), dim3(64), 0,
                        (hipStream_t)stream, qkv_dev, S, H, scale, nullptr, a_scale, (_Float16 *)planes_dev);
+  CM_HIP(hipGetLastError());
+  return CM_OK;
+}
+
+extern "C" int cm_long_attention_split(const float *qkv_dev, int32_t B, int32_t S, int32_t H, int32_t head_dim,
+                                       float scale, float a_scale, const int32_t *key_mask_dev, void *planes_dev,
+                                       void *stream) {
+  if (B <= 0) return CM_OK;
+  if (!qkv_dev || !planes_dev) CM_FAIL(CM_EINVAL, "NULL argument");
+  if (head_dim != kAttnDh) CM_FAIL(CM_EINVAL, "head_dim must be 64");
+  if (S <= 0 || S > 4096 || H <= 0) CM_FAIL(CM_EINVAL, "need 0 < S <= 4096 and H > 0");
+  const int64_t blocks = (int64_t)B * H * ((S + 63) / 64);
+  if (blocks > INT32_MAX) CM_FAIL(CM_EINVAL, "too many (sequence, head, query block) workgroups");
+  hipLaunchKernelGGL(long_attention_f16x3_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, qkv_dev,
+                     S, H, scale, a_scale, key_mask_dev, (_Float16 *)planes_dev);
   CM_HIP(hipGetLastError());
   return CM_OK;
 }

@@ -51,6 +51,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <utility>
 
 namespace cm {
 
@@ -72,6 +73,36 @@ __device__ __forceinline__ h16x8 as_h8(i32x4 v) { return __builtin_bit_cast(h16x
 #define K10_ABL 0
 #endif
 
+
+// Experiment knobs (variant builds, tools/build_k10_variant.sh; product values are the defaults):
+// K10_SCHED 1 = spread the second half's fragment reads and DMA pieces evenly over its MFMAs for
+// any counts (the default threads them only when they divide evenly); K10_PRIO 1 = s_setprio 1
+// for the second half of the waves (the arbitration losers of a lockstep workgroup); K10_H1 > 0
+// overrides the row tiles issued before the mid-step barrier.
+#ifndef K10_SCHED
+#define K10_SCHED 0
+#endif
+#ifndef K10_PRIO
+#define K10_PRIO 0
+#endif
+#ifndef K10_H1
+#define K10_H1 0
+#endif
+
+// one MFMA slot of the spread schedule: the MFMA, then its share of reads and DMA pieces (EARLY:
+// one read after each of the first NR MFMAs instead of an even spread)
+template <int NM, int NR, int ND, bool EARLY, int M>
+__device__ __forceinline__ void k10_slot() {
+  __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+  constexpr int r = EARLY ? (M < NR ? 1 : 0) : (M + 1) * NR / NM - M * NR / NM;
+  if constexpr (r > 0) __builtin_amdgcn_sched_group_barrier(0x100, r, 0);
+  constexpr int d = (M + 1) * ND / NM - M * ND / NM;
+  if constexpr (d > 0) __builtin_amdgcn_sched_group_barrier(0x020, d, 0);
+}
+template <int NM, int NR, int ND, bool EARLY, int... I>
+__device__ __forceinline__ void k10_spread(std::integer_sequence<int, I...>) {
+  (k10_slot<NM, NR, ND, EARLY, I>(), ...);
+}
 
 __device__ inline float gelu_erf(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
 
@@ -170,7 +201,7 @@ __global__ void __launch_bounds__(64 * NW)
   constexpr int PCS = (NBLK + NW - 1) / NW;           // DMA pieces per wave per stage (uniform count:
                                                       // pieces past NBLK re-load block 0 into a pad)
   constexpr int STAGE = PCS * NW * 1024;
-  constexpr int H1 = WMT / 2;                         // row tiles before the mid-step barrier
+  constexpr int H1 = (K10_H1 > 0 && K10_H1 < WMT) ? K10_H1 : WMT / 2;   // row tiles before the mid-step barrier
   constexpr int NMF2 = 3 * (WMT - H1) * WNT;          // MFMAs after it
   constexpr int NRD = 2 * (WMT + WNT);                // fragment reads per step
   static_assert(BMB % 2 == 0 && BNB % WGN == 0, "tile must split over the waves");
@@ -199,6 +230,7 @@ __global__ void __launch_bounds__(64 * NW)
   const int cn = q8 + (xcd < r8);
   const int my_n = slot < cn ? (cn - slot + sx - 1) / sx : 0;
   if (my_n == 0) return;                              // whole workgroup: no barrier is left waiting
+  if (K10_PRIO && wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
   // bias of every column into LDS once (no global load may sit between the counted DMA waits)
   for (int i = tid; i < N; i += 64 * NW) btab[i] = bias ? bias[i] : 0.f;
   __syncthreads();
@@ -294,13 +326,21 @@ __global__ void __launch_bounds__(64 * NW)
   do {                                                                                                       \
     const int cs_ = (g) % S, ns_ = ((g) + 1) % S;                                                            \
     K10_MFMA(0, H1, AH, AL, BH, BL)                                                                          \
+    if constexpr (K10_SCHED >= 2) __builtin_amdgcn_sched_barrier(0);   /* part-1 MFMAs stay before the wait */ \
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_waitcnt vmcnt(%0)" ::"n"(PCS * (S - 2)) : "memory");             \
     __builtin_amdgcn_s_barrier();                                                                            \
     __builtin_amdgcn_sched_barrier(0);                                                                       \
     K10_READ(ns_, NAH, NAL, NBH, NBL);                                                                       \
     K10_ISSUE(cs_);                                                                                          \
     K10_MFMA(H1, WMT, AH, AL, BH, BL)                                                                        \
-    if constexpr (THREAD) {                                                                                  \
+    if constexpr (K10_SCHED == 1) {                                                                          \
+      k10_spread<NMF2, NRD, PCS, false>(std::make_integer_sequence<int, NMF2>{});                            \
+    } else if constexpr (K10_SCHED == 2) {   /* every read first: they have the whole half-step to land */  \
+      __builtin_amdgcn_sched_group_barrier(0x100, NRD, 0);                                                   \
+      k10_spread<NMF2, 0, PCS, false>(std::make_integer_sequence<int, NMF2>{});                              \
+    } else if constexpr (K10_SCHED == 3) {                                                                   \
+      k10_spread<NMF2, NRD, PCS, true>(std::make_integer_sequence<int, NMF2>{});                             \
+    } else if constexpr (THREAD) {                                                                           \
       _Pragma("unroll") for (int q_ = 0; q_ < PCS; ++q_) {                                                   \
         _Pragma("unroll") for (int r_ = 0; r_ < NRD / PCS; ++r_) {                                           \
           __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                                                 \

@@ -394,6 +394,13 @@ int cm_short_attention_split(const float *qkv_dev, int32_t B, int32_t S, int32_t
 int cm_short_attention_split_masked(const float *qkv_dev, int32_t B, int32_t S, int32_t H, int32_t head_dim,
                                     float scale, float a_scale, const int32_t *key_mask_dev, void *planes_dev,
                                     void *stream);
+/* cm_long_attention_split: the same context planes for any 0 < S <= 4096 (passages; K9L, a
+ * flash-style split-precision MFMA kernel: 64-key chunks through LDS, online softmax in fp32);
+ * key_mask_dev (B x S int32, nonzero = attend) may be NULL (every key attends).  Replaces torch
+ * SDPA + cm_f16x3_split_rows for the reference's passage encode (rag/embeddings/__init__.py:96-105,
+ * truncation at 512 tokens). */
+int cm_long_attention_split(const float *qkv_dev, int32_t B, int32_t S, int32_t H, int32_t head_dim, float scale,
+                            float a_scale, const int32_t *key_mask_dev, void *planes_dev, void *stream);
 
 #ifdef __cplusplus
 }

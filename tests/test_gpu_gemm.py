@@ -175,3 +175,39 @@ def test_short_attention_split_masked_matches_fp64(S):
     p1 = engine.short_attention_split(qkv, H, 0.125, 2.0 ** 8, key_mask=torch.ones_like(mask))
     p0 = engine.short_attention_split(qkv, H, 0.125, 2.0 ** 8)
     assert all(torch.equal(a, b) for a, b in zip(p1.halves(), p0.halves()))
+
+
+@pytest.mark.parametrize("S", [1, 33, 64, 100, 256, 512])
+@pytest.mark.parametrize("masked", [False, True])
+def test_long_attention_split_matches_fp64(S, masked):
+    """K9L (cm_long_attention_split: 64-key chunks through LDS, online softmax, split-precision
+    MFMAs) -- the passage encode's attention, up to the reference's 512-token truncation -- against
+    an fp64 softmax(q k^T / 8) v, padded keys removed when masked, as accurate as torch's fp32."""
+    import torch
+    from classmate_hip import engine
+    torch.manual_seed(7 * S + masked)
+    B, H = (16 if S <= 256 else 6), 12
+    qkv = 2 * torch.randn(B, S, 3 * H * 64, device="cuda")
+    mask = None
+    keep = torch.ones(B, 1, 1, S, dtype=torch.bool, device="cuda")
+    if masked:
+        lens = torch.randint(1, S + 1, (B,), device="cuda")
+        lens[0] = S
+        mask = (torch.arange(S, device="cuda")[None, :] < lens[:, None]).to(torch.int32)
+        keep = mask.bool()[:, None, None, :]
+    q, k, v = qkv.double().view(B, S, 3, H, 64).permute(2, 0, 3, 1, 4)
+    sc = (q @ k.transpose(-1, -2) / 8.0).masked_fill(~keep, float("-inf"))
+    ref = (torch.softmax(sc, dim=-1) @ v).transpose(1, 2).reshape(B * S, H * 64)
+    q32, k32, v32 = qkv.view(B, S, 3, H, 64).permute(2, 0, 3, 1, 4)
+    s32 = (q32 @ k32.transpose(-1, -2) / 8.0).masked_fill(~keep, float("-inf"))
+    t32 = (torch.softmax(s32, dim=-1) @ v32).transpose(1, 2).reshape(B * S, H * 64)
+    p = engine.long_attention_split(qkv, H, 0.125, 2.0 ** 8, key_mask=mask)
+    hi, lo = p.halves()
+    got = (hi.double() + lo.double()) / 2.0 ** 8
+    e, e32 = float((got - ref).abs().max()), float((t32.double() - ref).abs().max())
+    print(f"\nlong attention S={S} masked={masked}: max err {e:.2e} (torch fp32 {e32:.2e})")
+    assert e <= 2 * e32 + 2e-6
+    if S <= 32 and not masked:          # the same math as K9s where both apply
+        ps = engine.short_attention_split(qkv, H, 0.125, 2.0 ** 8)
+        hs, ls = ps.halves()
+        assert float(((hs.double() + ls.double()) / 2.0 ** 8 - got).abs().max()) <= 2 * e32 + 2e-6
