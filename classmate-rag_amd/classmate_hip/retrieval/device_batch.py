@@ -89,18 +89,22 @@ def _query_vectors(embedder, questions: Sequence[str], dev):
 _ALLOW_CACHE_MAX = 64
 
 
+def _filter_key(meta, where, semantics: str):
+    """Cache key of a filter over one metadata version (None when ``where`` does not serialise)."""
+    import json
+    try:
+        return (id(meta), meta.version, semantics, json.dumps(where, sort_keys=True, default=str))
+    except (TypeError, ValueError):
+        return None
+
+
 def _allow(meta, where, semantics: str, device: int, n_words: int, cache: dict):
     """Device allow words + candidate count of ``where`` (engine.where_bits), cached per (metadata
     version, filter): a caller repeating one filter -- ask_question's to_dict() -- pays the filter
     program once per store change."""
-    import json
     import torch
-    try:
-        fkey = json.dumps(where, sort_keys=True, default=str)
-    except (TypeError, ValueError):
-        fkey = None
-    key = (id(meta), meta.version, semantics, fkey)
-    hit = cache.get(key) if fkey is not None else None
+    key = _filter_key(meta, where, semantics)
+    hit = cache.get(key) if key is not None else None
     if hit is not None:
         return hit
     from .. import engine as E
@@ -109,11 +113,38 @@ def _allow(meta, where, semantics: str, device: int, n_words: int, cache: dict):
         words = torch.from_numpy(np.ascontiguousarray(words).view(np.int32)).to(torch.device("cuda", device))
     if words.numel() < n_words:             # rows past the metadata (never written): not allowed
         words = torch.cat([words, torch.zeros(n_words - words.numel(), dtype=words.dtype, device=words.device)])
-    if fkey is not None:
+    if key is not None:
         if len(cache) >= _ALLOW_CACHE_MAX:
             cache.clear()
         cache[key] = (words, n)
     return words, n
+
+
+def _bm25_filtered(bm, q_terms, q_off, k: int, allow, where, cache: dict):
+    """Filtered BM25 top-k on the device (K2f: rank_bm25's statistics over the allowed candidates,
+    quirk Q2).  rank_bm25's epsilon floor (0.25 x the mean idf over the candidates' vocabulary,
+    needed when some query term's idf is negative) depends on the candidate set only, not on the
+    query, so it is computed once per (BM25 version, filter) -- a pass over every posting -- and
+    handed to later searches with the same filter."""
+    import torch
+    index = bm._index
+    index.prepare_filtered()                    # the device log table (once per index)
+    fk = _filter_key(bm._meta, where, "bm25")
+    ekey = None if fk is None else ("eps", id(bm), bm._version) + fk
+    eps_t = cache.get(ekey) if ekey is not None else None
+    s, r, st = index.search_filtered_dev(q_terms, q_off, k, allow, eps=eps_t)
+    code = int(st.item())
+    if code & index.FILT_EPS_MISSING:
+        eps_t = torch.tensor([index.filter_eps(allow)], dtype=torch.float64, device=q_terms.device)
+        if ekey is not None:
+            cache[ekey] = eps_t
+        s, r, st = index.search_filtered_dev(q_terms, q_off, k, allow, eps=eps_t)
+        code = int(st.item())
+    if code & index.FILT_ZERO_DIV:
+        raise ZeroDivisionError("float division by zero (candidate documents have no tokens)")
+    if code:
+        raise RuntimeError(f"filtered BM25 search status {code}")
+    return s, r
 
 
 def retrieve_batch(retr, questions: Sequence[str], top_k: int,
@@ -166,8 +197,7 @@ def retrieve_batch(retr, questions: Sequence[str], top_k: int,
     if allow_b is None:
         bs, br = bm._index.search_dev(q_terms, q_off, kb)
     elif kb > 0:
-        bm._index.prepare_filtered()            # the device log table (once per index)
-        bs, br = bm._index.search_filtered(q_terms, q_off, kb, allow_b)
+        bs, br = _bm25_filtered(bm, q_terms, q_off, kb, allow_b, filters, cache)
     else:
         bs = torch.zeros((nq, 1), dtype=torch.float64, device=dev)
         br = torch.full((nq, 1), -1, dtype=torch.int64, device=dev)
