@@ -40,9 +40,12 @@ METRIC = "hybrid queries/sec + recall@10 vs reference, 10M×768 chunks, 1/2/4/8 
 PEAK_F32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 matrix (dense)
 PEAK_F16_MFMA_TFLOPS = 2500.0  # MI355X_MICROARCH.md: BF16/F16 matrix, dense (no sparsity)
 PEAK_HBM_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E spec
+PEAK_I8_MFMA_TOPS = 5000.0     # cdna_hip_programming.md: i8 MFMA = 2x the bf16 rate (dense)
 DENSE_KINDS = {1: "K1 fp32 MFMA (dense_topk_kernel)",
                3: "K1c dense_coarse_scan_kernel (f16 plane, MFMA, 256-query resident passes) + certified fp64 re-rank",
-               4: "K1s dense_stream_scan_kernel (f16 plane, MFMA, per-wave HBM streams) + certified fp64 re-rank"}
+               4: "K1s dense_stream_scan_kernel (f16 plane, MFMA, per-wave HBM streams) + certified fp64 re-rank",
+               5: "K1q dense_q8_scan_kernel (int8 plane + per-row bounds, i8 MFMA, 256-query resident passes) + "
+                  "per-row certified fp64 re-rank"}
 
 
 def parse_args():
@@ -380,7 +383,7 @@ def main():
         + (f", bm25 search {bsearch_ms:.3f} ms (K2a tail pass {bm25_ms:.3f} ms, {rescored} (query, range) pairs "
            f"re-scored)" if bm25_ms is not None else ""))
 
-    roofs = {"dense": _dense_roofline(kind, N, D, B, dense_ms, _pmc_traffic(args, "dense"))}
+    roofs = {"dense": _dense_roofline(kind, N, D, B, dense_ms, _pmc_traffic(args, "dense" if kind != 5 else "dense_q8"))}
     if bm25 is not None:
         roofs["bm25"] = _bm25_roofline(bm25, q_terms, N, bm25_ms, _pmc_traffic(args, "bm25"), args.q_terms)
     dominant = max(roofs, key=lambda n: roofs[n]["avg_launch_ms"])
@@ -415,7 +418,9 @@ def main():
         "dtype": ("fp32-accurate E5 (K10 f16x3 MFMA) + f16/f64 dense + f64 BM25" if use_e5 and
                   args.e5_dtype == "float32" else "f16+f64"),
         "dtypes": {"dense_knn": {1: "f32 (MFMA)", 3: "f16 coarse (MFMA) + fp64 exact re-rank of the certified band",
-                                 4: "f16 coarse (MFMA) + fp64 exact re-rank of the certified band"}[kind],
+                                 4: "f16 coarse (MFMA) + fp64 exact re-rank of the certified band",
+                                 5: "int8 coarse (i8 MFMA, per-row scales) + fp64 exact re-rank of the per-row "
+                                    "certified band"}[kind],
                    "bm25": "f64", "fusion": "f64",
                    "e5_forward": ({"float32": "fp32 (K10: split-precision f16 hi/lo MFMA, fp32 accumulate)",
                                    "bfloat16": "bf16"}[args.e5_dtype] if use_e5 else None)},
@@ -470,6 +475,8 @@ def _dense_roofline(kind, N, D, B, ms, traffic):
     storage format + live bitmap + query planes; flops as executed on the MFMA units."""
     if kind == 1:      # fp32 rows + invc
         bytes_, flops, peak = N * D * 4 + N * 4 + N / 8 + B * D * 4, 2.0 * N * D * B, PEAK_F32_MFMA_TFLOPS
+    elif kind == 5:    # K1q: the int8 plane once + per-row {scale, bound} + live bits + the int8 queries
+        bytes_, flops, peak = N * D + N * 8 + N / 8 + B * D, 2.0 * N * D * B, PEAK_I8_MFMA_TOPS
     else:              # K1c / K1s: the f16 plane once + live bits + the f16 queries
         bytes_, flops, peak = N * D * 2 + N / 8 + B * D * 2, 2.0 * N * D * B, PEAK_F16_MFMA_TFLOPS
     r = _roof(bytes_, flops, peak, ms)
@@ -478,7 +485,7 @@ def _dense_roofline(kind, N, D, B, ms, traffic):
     # the other side of the same launch: at B = 256 the f16 scan's intensity (B flop/B = 256) sits
     # just under the nominal ridge (2.5 PF / 8 TB/s = 312), and under the chip's power limit the
     # MFMA clock drops, so the MFMA side is reported beside the HBM fraction
-    r["mfma_side"] = dict(achieved=flops / (ms * 1e-3) / 1e12, peak=peak, unit="TFLOP/s",
+    r["mfma_side"] = dict(achieved=flops / (ms * 1e-3) / 1e12, peak=peak, unit="TOP/s" if kind == 5 else "TFLOP/s",
                           frac=flops / (ms * 1e-3) / 1e12 / peak)
     return r
 

@@ -950,10 +950,14 @@ __global__ void __launch_bounds__(256, 1)
 // k-th smallest coarse distance of the whole corpus (k distinct rows lie at or under it); + 2E.
 // +inf when fewer than k groups hold an allowed row.
 // qs = queries per pass in the buffer layout (K1c: kBQPass, K1s: kSQ).
+#include "cm_dense_q8.inc"
+
+// seed[q] = the k-th smallest per-group minimum (+ 2E for K1c / K1s, whose minima are of the
+// coarse distance; K1q's minima already carry their rows' bounds: add_err = 0)
 __global__ void __launch_bounds__(256) dense_seed_kernel(const float *__restrict__ mins, int n_wg, int qs, int k,
                                                          int nq, const float *__restrict__ qnorm,
                                                          const float *__restrict__ row_norms, int dim,
-                                                         float *__restrict__ seed) {
+                                                         float *__restrict__ seed, int add_err) {
   const int qi = blockIdx.x;
   if (qi >= nq) return;
   const int qp = qi / qs, ql = qi - qp * qs;
@@ -973,8 +977,9 @@ __global__ void __launch_bounds__(256) dense_seed_kernel(const float *__restrict
     if (rank == k - 1) kth = x;
   }
   __syncthreads();
-  if (threadIdx.x == 0) seed[qi] = kth < __builtin_inff() ? kth + 2.0f * coarse_err(qnorm, qi, row_norms, dim)
-                                                           : __builtin_inff();
+  if (threadIdx.x == 0)
+    seed[qi] = kth < __builtin_inff() ? (add_err ? kth + 2.0f * coarse_err(qnorm, qi, row_norms, dim) : kth)
+                                      : __builtin_inff();
 }
 
 // Block-wide radix select: the k-th smallest (0-based kk) of n u32 values in LDS (4 x 8-bit digits).
@@ -1210,7 +1215,8 @@ __global__ void __launch_bounds__(256) dense_scatter_kernel(const float *__restr
                                                             int64_t row0, int64_t n, int dim, int ld,
                                                             float *__restrict__ C, float *__restrict__ invc,
                                                             uint32_t *__restrict__ live, _Float16 *__restrict__ Xh,
-                                                            uint32_t *__restrict__ rnorm) {
+                                                            uint32_t *__restrict__ rnorm, int8_t *__restrict__ Xq,
+                                                            float2 *__restrict__ rmeta) {
   const int64_t i = blockIdx.x;
   if (i >= n) return;
   const int64_t r = rows ? rows[i] : row0 + i;
@@ -1260,6 +1266,7 @@ __global__ void __launch_bounds__(256) dense_scatter_kernel(const float *__restr
     atomicMax(&rnorm[0], __float_as_uint(nh));
     atomicMax(&rnorm[1], __float_as_uint(nl));
   }
+  q8_row(s, inv, dim, ld, r, Xq, rmeta, rnorm);  // the int8 plane of K1q (from the same xn)
 }
 
 __global__ void dense_clear_live_kernel(const int64_t *__restrict__ rows, int64_t n, int64_t size,
@@ -1337,7 +1344,9 @@ struct cm_dense {
   float *C = nullptr;
   float *invc = nullptr;
   _Float16 *Xh = nullptr;                 // normalised f16 plane, fragment-major (K1c/K1s)
-  float *rnorm = nullptr;                  // device {max ||Xh_r||, max ||xn_r - Xh_r||} (K1c bound)
+  int8_t *Xq = nullptr;                    // normalised int8 plane, fragment-major (K1q)
+  float2 *rmeta = nullptr;                 // per row {s_r, e_r} of the int8 plane (K1q bound)
+  float *rnorm = nullptr;                  // device {max ||Xh_r||, max ||xn_r - Xh_r||, max ||s_r q8_r||, 0}
   int path = 0;                            // cm_dense_set_path (0 = automatic)
   int32_t last_fallbacks = -1;             // K1c queries re-run exactly by the last host search
   KernelTimer timer;                       // scan-kernel events (cm_dense_timing)
@@ -1453,8 +1462,8 @@ DenseWs dense_ws_layout(const cm_dense *h, const DenseCfg &c, int nq, int k, voi
   return w;
 }
 
-// Bytes of the four row arrays at `rows` rows (C fp32, invc, live bits, Xh plane).
-int64_t dense_row_bytes(const cm_dense *h, int64_t rows) { return rows * h->ld * 6 + rows * 4 + rows / 8; }
+// Bytes of the row arrays at `rows` rows (C fp32, invc, live bits, Xh f16 plane, Xq int8 plane + rmeta).
+int64_t dense_row_bytes(const cm_dense *h, int64_t rows) { return rows * h->ld * 7 + rows * 12 + rows / 8; }
 
 // Growth (dense_grow).  The arrays are reallocated at max(need, 1.5 x rows_alloc) rows.  When the
 // new arrays fit in the device's free memory next to the old ones (hipMemGetInfo, with kGrowSlack to
@@ -1497,27 +1506,42 @@ __global__ void __launch_bounds__(256) dense_replane_kernel(const float *__restr
   }
 }
 
-int dense_alloc_rows(cm_dense *h, int64_t cap, float **C2, float **ic2, uint32_t **lv2, _Float16 **xh2) {
-  *C2 = nullptr, *ic2 = nullptr, *lv2 = nullptr, *xh2 = nullptr;
+struct RowArrays {
+  float *C = nullptr, *invc = nullptr;
+  uint32_t *live = nullptr;
+  _Float16 *Xh = nullptr;
+  int8_t *Xq = nullptr;
+  float2 *rmeta = nullptr;
+};
+
+int dense_alloc_rows(cm_dense *h, int64_t cap, RowArrays &a) {
+  a = RowArrays{};
   const size_t nel = (size_t)cap * h->ld;
-  if (hipMalloc(C2, nel * 4) != hipSuccess || hipMalloc(ic2, (size_t)cap * 4) != hipSuccess ||
-      hipMalloc(lv2, (size_t)cap / 8) != hipSuccess || hipMalloc(xh2, nel * 2) != hipSuccess) {
-    for (void *p : {(void *)*C2, (void *)*ic2, (void *)*lv2, (void *)*xh2})
+  if (hipMalloc(&a.C, nel * 4) != hipSuccess || hipMalloc(&a.invc, (size_t)cap * 4) != hipSuccess ||
+      hipMalloc(&a.live, (size_t)cap / 8) != hipSuccess || hipMalloc(&a.Xh, nel * 2) != hipSuccess ||
+      hipMalloc(&a.Xq, nel) != hipSuccess || hipMalloc(&a.rmeta, (size_t)cap * 8) != hipSuccess) {
+    for (void *p : {(void *)a.C, (void *)a.invc, (void *)a.live, (void *)a.Xh, (void *)a.Xq, (void *)a.rmeta})
       if (p) (void)hipFree(p);
-    *C2 = nullptr, *ic2 = nullptr, *lv2 = nullptr, *xh2 = nullptr;
+    a = RowArrays{};
     CM_FAIL(CM_ENOMEM, "dense: out of device memory");
   }
-  CM_HIP(hipMemsetAsync(*C2, 0, nel * 4, h->stream));
-  CM_HIP(hipMemsetAsync(*ic2, 0, (size_t)cap * 4, h->stream));
-  CM_HIP(hipMemsetAsync(*lv2, 0, (size_t)cap / 8, h->stream));
-  CM_HIP(hipMemsetAsync(*xh2, 0, nel * 2, h->stream));
+  CM_HIP(hipMemsetAsync(a.C, 0, nel * 4, h->stream));
+  CM_HIP(hipMemsetAsync(a.invc, 0, (size_t)cap * 4, h->stream));
+  CM_HIP(hipMemsetAsync(a.live, 0, (size_t)cap / 8, h->stream));
+  CM_HIP(hipMemsetAsync(a.Xh, 0, nel * 2, h->stream));
+  CM_HIP(hipMemsetAsync(a.Xq, 0, nel, h->stream));
+  CM_HIP(hipMemsetAsync(a.rmeta, 0, (size_t)cap * 8, h->stream));
   return CM_OK;
 }
 
+void dense_set_rows(cm_dense *h, const RowArrays &a) {
+  h->C = a.C, h->invc = a.invc, h->live = a.live, h->Xh = a.Xh, h->Xq = a.Xq, h->rmeta = a.rmeta;
+}
+
 void dense_free_rows(cm_dense *h) {
-  for (void *p : {(void *)h->C, (void *)h->invc, (void *)h->live, (void *)h->Xh})
+  for (void *p : {(void *)h->C, (void *)h->invc, (void *)h->live, (void *)h->Xh, (void *)h->Xq, (void *)h->rmeta})
     if (p) (void)hipFree(p);
-  h->C = nullptr, h->invc = nullptr, h->live = nullptr, h->Xh = nullptr;
+  dense_set_rows(h, RowArrays{});
 }
 
 int dense_grow(cm_dense *h, int64_t need_rows) {
@@ -1525,9 +1549,7 @@ int dense_grow(cm_dense *h, int64_t need_rows) {
   int64_t cap = std::max<int64_t>(need_rows, h->rows_alloc + h->rows_alloc / 2);
   cap = round_up(std::max<int64_t>(cap, kStepRows), kStepRows);
   const int64_t keep = std::min<int64_t>(round_up(h->size, kStepRows), h->rows_alloc);  // rows holding data
-  float *C2, *ic2;
-  uint32_t *lv2;
-  _Float16 *xh2;
+  RowArrays a;
   int rc;
   bool staged = keep > 0 && h->mem_cur > kStageBytes;
   if (staged && h->grow_mode == 0) {   // auto: copy on the device when old + new fit with slack
@@ -1553,15 +1575,15 @@ int dense_grow(cm_dense *h, int64_t need_rows) {
     dense_free_rows(h);
     h->rows_alloc = 0;
     h->mem_cur = 0;
-    if ((rc = dense_alloc_rows(h, cap, &C2, &ic2, &lv2, &xh2))) {
+    if ((rc = dense_alloc_rows(h, cap, a))) {
       // put the old rows back (the size just freed, so this allocation fits where the larger failed)
       cap = keep;
-      if (dense_alloc_rows(h, cap, &C2, &ic2, &lv2, &xh2) != CM_OK) {
+      if (dense_alloc_rows(h, cap, a) != CM_OK) {
         // nothing fits any more: an empty minimal store (never a handle without arrays)
-        if (dense_alloc_rows(h, kStepRows, &C2, &ic2, &lv2, &xh2) != CM_OK)
+        if (dense_alloc_rows(h, kStepRows, a) != CM_OK)
           CM_FAIL(CM_ENOMEM, "dense: out of device memory; the handle is unusable");
         CM_HIP(hipStreamSynchronize(h->stream));
-        h->C = C2, h->invc = ic2, h->live = lv2, h->Xh = xh2;
+        dense_set_rows(h, a);
         h->rows_alloc = kStepRows;
         h->size = 0;
         h->mem_cur = dense_row_bytes(h, kStepRows);
@@ -1571,39 +1593,45 @@ int dense_grow(cm_dense *h, int64_t need_rows) {
     }
     // (cap may now be keep: the old rows go back into an array of their old size)
     int rc2;
-    if ((rc2 = staged_copy(h, host, reinterpret_cast<char *>(C2), cb, false, bounce)) ||
-        (rc2 = staged_copy(h, host + cb, reinterpret_cast<char *>(ic2), ib, false, bounce)) ||
-        (rc2 = staged_copy(h, host + cb + ib, reinterpret_cast<char *>(lv2), lb, false, bounce))) {
-      h->C = C2, h->invc = ic2, h->live = lv2, h->Xh = xh2;
+    if ((rc2 = staged_copy(h, host, reinterpret_cast<char *>(a.C), cb, false, bounce)) ||
+        (rc2 = staged_copy(h, host + cb, reinterpret_cast<char *>(a.invc), ib, false, bounce)) ||
+        (rc2 = staged_copy(h, host + cb + ib, reinterpret_cast<char *>(a.live), lb, false, bounce))) {
+      dense_set_rows(h, a);
       h->rows_alloc = cap;
       h->mem_cur = dense_row_bytes(h, cap);
       return rc2;
     }
-    hipLaunchKernelGGL(dense_replane_kernel, dim3((unsigned)keep), dim3(256), 0, h->stream, C2, ic2, keep, h->dim,
-                       h->ld, xh2);
+    // both coarse planes recomputed from the fp32 rows, bit-identical to the upserts'
+    hipLaunchKernelGGL(dense_replane_kernel, dim3((unsigned)keep), dim3(256), 0, h->stream, a.C, a.invc, keep, h->dim,
+                       h->ld, a.Xh);
+    CM_HIP(hipGetLastError());
+    hipLaunchKernelGGL(dense_q8_replane_kernel, dim3((unsigned)keep), dim3(256), 0, h->stream, a.C, a.invc, keep,
+                       h->dim, h->ld, a.Xq, a.rmeta, reinterpret_cast<uint32_t *>(h->rnorm));
     CM_HIP(hipGetLastError());
     CM_HIP(hipStreamSynchronize(h->stream));
     ++h->staged_growths;
-    h->C = C2, h->invc = ic2, h->live = lv2, h->Xh = xh2;
+    dense_set_rows(h, a);
     h->rows_alloc = cap;
     h->mem_cur = dense_row_bytes(h, cap);
     h->mem_peak = std::max(h->mem_peak, h->mem_cur);
     if (rc) CM_FAIL(CM_ENOMEM, "dense: out of device memory");
     return CM_OK;
   }
-  if ((rc = dense_alloc_rows(h, cap, &C2, &ic2, &lv2, &xh2))) return rc;
+  if ((rc = dense_alloc_rows(h, cap, a))) return rc;
   h->mem_peak = std::max(h->mem_peak, h->mem_cur + dense_row_bytes(h, cap));  // old + new at once
   if (keep > 0) {
-    // the plane is tile-major (64-row tiles, keep a multiple of 128): a prefix copy keeps it
+    // the planes are tile-major (64-row tiles, keep a multiple of 128): prefix copies keep them
     const size_t old = (size_t)keep * h->ld;
-    CM_HIP(hipMemcpyAsync(C2, h->C, old * 4, hipMemcpyDeviceToDevice, h->stream));
-    CM_HIP(hipMemcpyAsync(ic2, h->invc, (size_t)keep * 4, hipMemcpyDeviceToDevice, h->stream));
-    CM_HIP(hipMemcpyAsync(lv2, h->live, (size_t)keep / 8, hipMemcpyDeviceToDevice, h->stream));
-    CM_HIP(hipMemcpyAsync(xh2, h->Xh, old * 2, hipMemcpyDeviceToDevice, h->stream));
+    CM_HIP(hipMemcpyAsync(a.C, h->C, old * 4, hipMemcpyDeviceToDevice, h->stream));
+    CM_HIP(hipMemcpyAsync(a.invc, h->invc, (size_t)keep * 4, hipMemcpyDeviceToDevice, h->stream));
+    CM_HIP(hipMemcpyAsync(a.live, h->live, (size_t)keep / 8, hipMemcpyDeviceToDevice, h->stream));
+    CM_HIP(hipMemcpyAsync(a.Xh, h->Xh, old * 2, hipMemcpyDeviceToDevice, h->stream));
+    CM_HIP(hipMemcpyAsync(a.Xq, h->Xq, old, hipMemcpyDeviceToDevice, h->stream));
+    CM_HIP(hipMemcpyAsync(a.rmeta, h->rmeta, (size_t)keep * 8, hipMemcpyDeviceToDevice, h->stream));
   }
   CM_HIP(hipStreamSynchronize(h->stream));
   dense_free_rows(h);
-  h->C = C2, h->invc = ic2, h->live = lv2, h->Xh = xh2;
+  dense_set_rows(h, a);
   h->rows_alloc = cap;
   h->mem_cur = dense_row_bytes(h, cap);
   return CM_OK;
@@ -1636,15 +1664,23 @@ int dense_kind(const cm_dense *h, int nq, int k) {
     const char *e = getenv("CM_DENSE_PATH");
     if (!e) return 0;
     const std::string s(e);
-    return s == "f32" ? CM_DENSE_F32 : s == "coarse" ? CM_DENSE_COARSE : s == "stream" ? CM_DENSE_STREAM : 0;
+    return s == "f32" ? CM_DENSE_F32 : s == "coarse" ? CM_DENSE_COARSE : s == "stream" ? CM_DENSE_STREAM
+         : s == "q8" ? CM_DENSE_Q8 : 0;
+  }();
+  static const bool q8_auto = [] {
+    const char *e = getenv("CM_DENSE_Q8");
+    return !(e && e[0] == '0');
   }();
   const int force = h->path ? h->path : env_force;
   // coarse scans: resident-query instances for ld 768 / 384, a sample of >= 1024 rows for the seed
   const bool coarse_ok = k <= kBMaxK && (h->ld == 768 || h->ld == 384) && h->size >= 16384;
+  const bool q8_ok = coarse_ok && h->ld == 768;  // K1q: the 6-chunk (ld 768) instance
   if (force == CM_DENSE_F32 || !coarse_ok) return CM_DENSE_F32;
   if (force == CM_DENSE_COARSE) return CM_DENSE_COARSE;
   if (force == CM_DENSE_STREAM && nq <= kSQ) return CM_DENSE_STREAM;
-  return nq <= kSQ ? CM_DENSE_STREAM : CM_DENSE_COARSE;
+  if (force == CM_DENSE_Q8 && q8_ok) return CM_DENSE_Q8;
+  if (nq <= kSQ) return CM_DENSE_STREAM;
+  return (q8_ok && q8_auto) ? CM_DENSE_Q8 : CM_DENSE_COARSE;
 }
 
 // Coarse-scan geometry.  K1c: a pass of kBQPass queries per workgroup, one workgroup per CU and
@@ -1662,7 +1698,7 @@ bool k1c_paired() {
 }
 
 struct CoarseCfg {
-  bool stream, paired;
+  bool stream, paired, q8;
   int qs, n_pass, n_wg, n_wg_sample;
   int64_t rows_per_wg, rows_end, rows_per_wg_sample, rows_end_sample;
   // blocks of a K1c launch over n_wg ranges: the paired form maps blocks b, b + 8 to one (pass,
@@ -1672,10 +1708,12 @@ struct CoarseCfg {
     return (unsigned)(paired ? round_up(2 * m, 16) : m);
   }
 };
-CoarseCfg coarse_config(const cm_dense *h, int nq, bool stream) {
+CoarseCfg coarse_config(const cm_dense *h, int nq, int kind) {
   CoarseCfg c{};
+  const bool stream = kind == CM_DENSE_STREAM;
   c.stream = stream;
-  c.paired = !stream && k1c_paired();
+  c.q8 = kind == CM_DENSE_Q8;
+  c.paired = !stream && !c.q8 && k1c_paired();
   c.qs = stream ? kSQ : kBQPass;
   c.n_pass = stream ? 1 : (int)ceil_div(nq, kBQPass);
   c.rows_end = round_up(std::max<int64_t>(h->size, 1), kStepRows);
@@ -1687,13 +1725,16 @@ CoarseCfg coarse_config(const cm_dense *h, int nq, bool stream) {
     n = (int)ceil_div(rows_end, per);
   };
   split(c.rows_end, c.rows_per_wg, c.n_wg);
-  const int64_t frac = c.rows_end >= (1 << 20) ? 64 : 16;
+  // K1q's per-row bounds widen the candidate set: a denser seed sample keeps it near ~4k per query
+  const int64_t frac = c.q8 ? kQSampleFrac : c.rows_end >= (1 << 20) ? 64 : 16;
   c.rows_end_sample = round_up(std::max<int64_t>(c.rows_end / frac, 1), kRRows);
   split(c.rows_end_sample, c.rows_per_wg_sample, c.n_wg_sample);
   return c;
 }
 
 struct CoarseWs {
+  int8_t *qq;         // [nq_pad][ld] int8 query fragments (K1q)
+  float4 *qsc;        // [nq_pad] {s_q, a_q, b_q, ||q||} (K1q)
   _Float16 *qh;       // [nq_pad][ld] normalised f16 queries
   float *qnorm;       // [nq_pad][4]
   uint64_t *keys;     // candidate buffers [pass][group][qs][kCBufCap]
@@ -1715,9 +1756,14 @@ CoarseWs coarse_ws_layout(const cm_dense *h, const CoarseCfg &c, int nq, int k, 
     off += round_up(std::max<int64_t>(bytes, 1), 256);
     return r;
   };
+  const int cap = c.q8 ? kQCap : kCBufCap;
+  if (c.q8) {
+    w.qq = reinterpret_cast<int8_t *>(take(nq_pad * h->ld));
+    w.qsc = reinterpret_cast<float4 *>(take(nq_pad * 16));
+  }
   w.qh = reinterpret_cast<_Float16 *>(take(nq_pad * h->ld * 2));
   w.qnorm = reinterpret_cast<float *>(take(nq_pad * 16));
-  w.keys = reinterpret_cast<uint64_t *>(take((int64_t)c.n_pass * c.n_wg * c.qs * kCBufCap * 8));
+  w.keys = reinterpret_cast<uint64_t *>(take((int64_t)c.n_pass * c.n_wg * c.qs * cap * 8));
   w.cnt = reinterpret_cast<uint32_t *>(take((int64_t)c.n_pass * c.n_wg * c.qs * 4));
   w.mins = reinterpret_cast<float *>(take((int64_t)c.n_pass * c.n_wg_sample * c.qs * 4));
   w.seed = reinterpret_cast<float *>(take(nq_pad * 4));
@@ -1743,7 +1789,9 @@ int set_coarse_attrs() {
         {reinterpret_cast<const void *>(&dense_coarse_scan_kernel<12, 0, true, 4, 20, 128>), K1rLds<0, 20>::total},
         {reinterpret_cast<const void *>(&dense_coarse_scan_kernel<6, 0, false, 4, 20, 128>), K1rLds<0, 20>::total},
         {reinterpret_cast<const void *>(&dense_coarse_scan_kernel<6, 0, true, 4, 20, 128>), K1rLds<0, 20>::total},
-        {reinterpret_cast<const void *>(&dense_rerank_kernel), kGatherCap * 12}};
+        {reinterpret_cast<const void *>(&dense_rerank_kernel), kGatherCap * 12},
+        {reinterpret_cast<const void *>(&dense_q8_scan_kernel<false>), kQRing * 8192},
+        {reinterpret_cast<const void *>(&dense_q8_scan_kernel<true>), kQRing * 8192}};
     for (const auto &f : fs) {
       const hipError_t e = hipFuncSetAttribute(f.first, hipFuncAttributeMaxDynamicSharedMemorySize, f.second);
       if (e != hipSuccess) err = e;
@@ -1767,11 +1815,12 @@ StreamFn stream_kernel(int ld, int nq, bool minonly) {
 // K1c / K1s: sample pre-pass -> seed -> coarse scan -> certificate + exact re-rank; the queries
 // whose certificate fails (fb_mask) are re-searched by the exact fp32 K1 and merged (every
 // workgroup of those launches exits at once when there are none: graph-capturable, no host sync).
-int launch_coarse(cm_dense *h, const float *q_dev, int nq, int k, bool stream, const uint32_t *allow,
+int launch_coarse(cm_dense *h, const float *q_dev, int nq, int k, int kind, const uint32_t *allow,
                   float *dist_dev, int64_t *row_dev, void *ws, int64_t ws_bytes, hipStream_t st) {
   int rc;
   if ((rc = set_coarse_attrs())) return rc;
-  const CoarseCfg c = coarse_config(h, nq, stream);
+  const bool stream = kind == CM_DENSE_STREAM;
+  const CoarseCfg c = coarse_config(h, nq, kind);
   const CoarseWs w = coarse_ws_layout(h, c, nq, k, ws);
   if ((int64_t)w.total > ws_bytes || !ws) CM_FAIL(CM_EINVAL, "dense workspace too small");
   const int64_t n_words = ceil_div(h->size, 32);
@@ -1779,6 +1828,29 @@ int launch_coarse(cm_dense *h, const float *q_dev, int nq, int k, bool stream, c
                      w.qnorm);
   CM_HIP(hipGetLastError());
   CM_HIP(hipMemsetAsync(w.fb_count, 0, 4, st));
+  if (c.q8) {
+    // K1q: int8 queries -> 1/8-sample minima of d~ + E_r -> seed -> scan -> per-row certified re-rank
+    hipLaunchKernelGGL(dense_prep_q8, dim3(c.n_pass * c.qs), dim3(256), 0, st, q_dev, nq, h->dim, h->ld, w.qq, w.qsc,
+                       reinterpret_cast<const uint32_t *>(h->rnorm));
+    CM_HIP(hipGetLastError());
+    hipLaunchKernelGGL(dense_q8_scan_kernel<true>, dim3(c.n_pass * c.n_wg_sample), dim3(256), kQRing * 8192, st, h->Xq,
+                       h->rmeta, h->live, allow, n_words, w.qq, w.qsc, nq, (const float *)nullptr,
+                       c.rows_per_wg_sample, c.rows_end_sample, c.n_wg_sample, (uint64_t *)nullptr,
+                       (uint32_t *)nullptr, w.mins);
+    CM_HIP(hipGetLastError());
+    hipLaunchKernelGGL(dense_seed_kernel, dim3(nq), dim3(256), 0, st, w.mins, c.n_wg_sample, c.qs, k, nq, w.qnorm,
+                       h->rnorm, h->dim, w.seed, 0);
+    CM_HIP(hipGetLastError());
+    h->timer.begin(st);
+    hipLaunchKernelGGL(dense_q8_scan_kernel<false>, dim3(c.n_pass * c.n_wg), dim3(256), kQRing * 8192, st, h->Xq,
+                       h->rmeta, h->live, allow, n_words, w.qq, w.qsc, nq, (const float *)w.seed, c.rows_per_wg,
+                       c.rows_end, c.n_wg, w.keys, w.cnt, (float *)nullptr);
+    h->timer.end(st);
+    CM_HIP(hipGetLastError());
+    hipLaunchKernelGGL(dense_rerank_q8_kernel, dim3(nq), dim3(256), 0, st, w.keys, w.cnt, c.n_wg, k, nq, h->C, h->ld,
+                       h->dim, q_dev, w.qsc, h->rmeta, dist_dev, row_dev, w.fb_mask, w.fb_count);
+    CM_HIP(hipGetLastError());
+  } else {
   const bool d768 = h->ld == 768;
   const size_t slds = c.paired ? K1rLds<0, 20>::total : d768 ? K1rLds<kK1cNql>::total : K1rLds<0>::total;
   const int k1c_threads = c.paired ? 256 : 64 * kK1cWaves;
@@ -1805,7 +1877,7 @@ int launch_coarse(cm_dense *h, const float *q_dev, int nq, int k, bool stream, c
   }
   CM_HIP(hipGetLastError());
   hipLaunchKernelGGL(dense_seed_kernel, dim3(nq), dim3(256), 0, st, w.mins, c.n_wg_sample, c.qs, k, nq, w.qnorm,
-                     h->rnorm, h->dim, w.seed);
+                     h->rnorm, h->dim, w.seed, 1);
   CM_HIP(hipGetLastError());
   // 2. coarse scan: rows under the seed -> candidate buffers
   h->timer.begin(st);
@@ -1824,6 +1896,7 @@ int launch_coarse(cm_dense *h, const float *q_dev, int nq, int k, bool stream, c
   hipLaunchKernelGGL(dense_rerank_kernel, dim3(nq), dim3(256), kGatherCap * 12, st, w.keys, w.cnt, c.n_wg, c.qs, k,
                      nq, h->C, h->ld, h->dim, q_dev, w.qnorm, h->rnorm, dist_dev, row_dev, w.fb_mask, w.fb_count);
   CM_HIP(hipGetLastError());
+  }
   // 4. exact fp32 K1 for the rejected queries only, merged into their rows of the output
   const DenseCfg kc = dense_config(h, nq, k);
   if (kc.lds > 163840) CM_FAIL(CM_EUNSUPPORTED, "dim/k too large for the LDS-resident query tile");
@@ -1919,7 +1992,7 @@ int cm_dense_create(int device, int32_t dim, int64_t capacity, cm_dense **out) {
     delete h;
     CM_FAIL(CM_EDEVICE, "hipStreamCreate failed");
   }
-  if (hipMalloc(&h->rnorm, 8) != hipSuccess || hipMemset(h->rnorm, 0, 8) != hipSuccess) {
+  if (hipMalloc(&h->rnorm, 16) != hipSuccess || hipMemset(h->rnorm, 0, 16) != hipSuccess) {
     cm_dense_destroy(h);
     CM_FAIL(CM_ENOMEM, "dense: out of device memory");
   }
@@ -1976,7 +2049,7 @@ int cm_dense_upsert(cm_dense *h, const float *vecs, const int64_t *rows, int64_t
     CM_HIP(hipMemcpyAsync(h->rows_buf.ptr, rows + s, (size_t)m * 8, hipMemcpyHostToDevice, h->stream));
     hipLaunchKernelGGL(dense_scatter_kernel, dim3((unsigned)m), dim3(256), 0, h->stream, h->staging.as<float>(),
                        h->rows_buf.as<int64_t>(), (int64_t)0, m, h->dim, h->ld, h->C, h->invc, h->live, h->Xh,
-                       reinterpret_cast<uint32_t *>(h->rnorm));
+                       reinterpret_cast<uint32_t *>(h->rnorm), h->Xq, h->rmeta);
     CM_HIP(hipGetLastError());
     CM_HIP(hipStreamSynchronize(h->stream));
   }
@@ -2000,7 +2073,7 @@ int cm_dense_upsert_dev(cm_dense *h, const float *vecs_dev, int64_t row0, int64_
     const int64_t m = std::min(batch, n - s);
     hipLaunchKernelGGL(dense_scatter_kernel, dim3((unsigned)m), dim3(256), 0, st, vecs_dev + s * h->dim,
                        (const int64_t *)nullptr, row0 + s, m, h->dim, h->ld, h->C, h->invc, h->live, h->Xh,
-                       reinterpret_cast<uint32_t *>(h->rnorm));
+                       reinterpret_cast<uint32_t *>(h->rnorm), h->Xq, h->rmeta);
     CM_HIP(hipGetLastError());
   }
   h->size = std::max(h->size, row0 + n);
@@ -2029,7 +2102,9 @@ int cm_dense_reset(cm_dense *h) {
   CM_HIP(hipMemsetAsync(h->invc, 0, (size_t)h->rows_alloc * 4, h->stream));
   CM_HIP(hipMemsetAsync(h->C, 0, (size_t)h->rows_alloc * h->ld * 4, h->stream));
   CM_HIP(hipMemsetAsync(h->Xh, 0, (size_t)h->rows_alloc * h->ld * 2, h->stream));
-  CM_HIP(hipMemsetAsync(h->rnorm, 0, 8, h->stream));
+  CM_HIP(hipMemsetAsync(h->Xq, 0, (size_t)h->rows_alloc * h->ld, h->stream));
+  CM_HIP(hipMemsetAsync(h->rmeta, 0, (size_t)h->rows_alloc * 8, h->stream));
+  CM_HIP(hipMemsetAsync(h->rnorm, 0, 16, h->stream));
   CM_HIP(hipStreamSynchronize(h->stream));
   h->size = 0;
   return CM_OK;
@@ -2073,14 +2148,14 @@ int64_t cm_dense_search_workspace(cm_dense *h, int32_t nq, int32_t k) {
   if (!h || nq <= 0 || k <= 0 || k > kMaxTopK) return -1;
   const int kind = dense_kind(h, nq, k);
   if (kind != CM_DENSE_F32)
-    return (int64_t)coarse_ws_layout(h, coarse_config(h, nq, kind == CM_DENSE_STREAM), nq, k, nullptr).total;
+    return (int64_t)coarse_ws_layout(h, coarse_config(h, nq, kind), nq, k, nullptr).total;
   DenseCfg c = dense_config(h, nq, k);
   return (int64_t)dense_ws_layout(h, c, nq, k, nullptr).total;
 }
 
 int cm_dense_set_path(cm_dense *h, int32_t kind) {
   if (!h) CM_FAIL(CM_EINVAL, "null handle");
-  if (kind < 0 || kind > CM_DENSE_STREAM) CM_FAIL(CM_EINVAL, "unknown dense path");
+  if (kind < 0 || kind > CM_DENSE_Q8) CM_FAIL(CM_EINVAL, "unknown dense path");
   h->path = kind;
   return CM_OK;
 }
@@ -2090,7 +2165,7 @@ int32_t cm_dense_workspace_fallbacks(cm_dense *h, int32_t nq, int32_t k, const v
   const int kind = dense_kind(h, nq, k);
   if (kind == CM_DENSE_F32) return 0;
   DeviceGuard dg(h->dev);
-  const CoarseWs w = coarse_ws_layout(h, coarse_config(h, nq, kind == CM_DENSE_STREAM), nq, k,
+  const CoarseWs w = coarse_ws_layout(h, coarse_config(h, nq, kind), nq, k,
                                       const_cast<void *>(workspace_dev));
   int32_t c = -1;
   if (hipMemcpy(&c, w.fb_count, 4, hipMemcpyDeviceToHost) != hipSuccess) return -1;
@@ -2130,8 +2205,7 @@ int cm_dense_search_dev(cm_dense *h, const float *q_dev, int32_t nq, int32_t k, 
   hipStream_t st = (hipStream_t)stream;  // NULL = the null stream (torch default)
   const int kind = dense_kind(h, nq, k);
   if (kind != CM_DENSE_F32)
-    return launch_coarse(h, q_dev, nq, k, kind == CM_DENSE_STREAM, allow_dev, dist_dev, row_dev, workspace_dev,
-                         workspace_bytes, st);
+    return launch_coarse(h, q_dev, nq, k, kind, allow_dev, dist_dev, row_dev, workspace_dev, workspace_bytes, st);
   DenseCfg c = dense_config(h, nq, k);
   if (c.lds > 163840) CM_FAIL(CM_EUNSUPPORTED, "dim/k too large for the LDS-resident query tile");
   DenseWs w = dense_ws_layout(h, c, nq, k, workspace_dev);
@@ -2223,7 +2297,7 @@ int cm_dense_search(cm_dense *h, const float *q, int32_t nq, int32_t k, const ui
   h->last_fallbacks = 0;
   const int kind = dense_kind(h, nq, k);
   if (kind != CM_DENSE_F32) {
-    const CoarseWs w = coarse_ws_layout(h, coarse_config(h, nq, kind == CM_DENSE_STREAM), nq, k, h->ws.ptr);
+    const CoarseWs w = coarse_ws_layout(h, coarse_config(h, nq, kind), nq, k, h->ws.ptr);
     CM_HIP(hipMemcpyAsync(&h->last_fallbacks, w.fb_count, 4, hipMemcpyDeviceToHost, h->stream));
   }
   CM_HIP(hipStreamSynchronize(h->stream));

@@ -107,13 +107,17 @@ int64_t cm_dense_search_workspace(cm_dense *h, int32_t nq, int32_t k);
  * (K1, fp32 MFMA, reads 4 B/element: k > 32, other dims, small corpora),
  * CM_DENSE_COARSE (K1c, f16 plane, 2 B/element, 256-query resident passes,
  * certified exact re-rank), CM_DENSE_STREAM (K1s, f16 plane, 2 B/element,
- * nq <= 32, per-wave HBM streams, same re-rank); -1 on error.  Lets callers
- * price the launch against the right roofline.  CM_DENSE_F16X3 (the retired
- * split-plane K1b) is accepted by cm_dense_set_path and means automatic.  */
+ * nq <= 32, per-wave HBM streams, same re-rank), CM_DENSE_Q8 (K1q, int8 plane
+ * with per-row scales, 1 B/element, 256-query resident passes, per-row
+ * certified exact re-rank; the automatic choice for nq > 32 at dim 768 unless
+ * $CM_DENSE_Q8=0); -1 on error.  Lets callers price the launch against the
+ * right roofline.  CM_DENSE_F16X3 (the retired split-plane K1b) is accepted by
+ * cm_dense_set_path and means automatic.  */
 #define CM_DENSE_F32 1
 #define CM_DENSE_F16X3 2
 #define CM_DENSE_COARSE 3
 #define CM_DENSE_STREAM 4
+#define CM_DENSE_Q8 5
 int32_t cm_dense_search_kind(cm_dense *h, int32_t nq, int32_t k);
 /* force a scan kernel for this handle (0 = automatic; an ineligible forced
  * kind falls back to the automatic choice).  Results agree within the 1e-4
