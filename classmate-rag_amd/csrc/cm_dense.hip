@@ -566,14 +566,19 @@ __global__ void __launch_bounds__(64 * W, 1)
 #pragma unroll
     for (int qt = 0; qt < QT; ++qt)
 #pragma unroll
-      for (int sb = 0; sb < 2; ++sb) {
-        qres[c][qt][sb] = *qsrc(c, qt, sb);
-        // pin the first K1C_QAGPR chunks' fragments to AGPRs (the 256 of them hold 8 chunks): the
-        // MFMA reads its B operand from an AGPR directly, where a VGPR value the allocator parked
-        // in an AGPR is copied back before every use (16 v_accvgpr_read per chunk).  With the
-        // accumulators in VGPRs (-mllvm -amdgpu-mfma-vgpr-form, Makefile) nothing is copied.
+      for (int sb = 0; sb < 2; ++sb) qres[c][qt][sb] = *qsrc(c, qt, sb);
+  // pin the first K1C_QAGPR chunks' fragments to AGPRs (the 256 of them hold 8 chunks): the
+  // MFMA reads its B operand from an AGPR directly, where a VGPR value the allocator parked
+  // in an AGPR is copied back before every use (16 v_accvgpr_read per chunk).  With the
+  // accumulators in VGPRs (-mllvm -amdgpu-mfma-vgpr-form, Makefile) nothing is copied.  Pinned
+  // after all loads are issued (a pin per load serialised them behind vmcnt(0) waits).
+#pragma unroll
+  for (int c = 0; c < KR; ++c)
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+      for (int sb = 0; sb < 2; ++sb)
         if (c < K1C_QAGPR) asm volatile("" : "+a"(qres[c][qt][sb]));
-      }
 #pragma unroll
   for (int c = 0; c < NQL; ++c)
 #pragma unroll
@@ -1667,9 +1672,9 @@ int dense_kind(const cm_dense *h, int nq, int k) {
     return s == "f32" ? CM_DENSE_F32 : s == "coarse" ? CM_DENSE_COARSE : s == "stream" ? CM_DENSE_STREAM
          : s == "q8" ? CM_DENSE_Q8 : 0;
   }();
-  static const bool q8_auto = [] {
+  static const bool q8_auto = [] {  // K1q automatic for batched dim-768 searches: CM_DENSE_Q8=1
     const char *e = getenv("CM_DENSE_Q8");
-    return !(e && e[0] == '0');
+    return e && e[0] == '1';
   }();
   const int force = h->path ? h->path : env_force;
   // coarse scans: resident-query instances for ld 768 / 384, a sample of >= 1024 rows for the seed

@@ -37,7 +37,9 @@ def _grow(index, batches, rows_per_batch, seed):
 
 
 def _row_bytes(rows):
-    return rows * D * 6 + rows * 4 + rows // 8
+    """fp32 rows (4 B) + f16 plane (2 B) + int8 plane (1 B) per element; invc + K1q {scale, bound}
+    (12 B) and a live bit per row (cm_dense.hip dense_row_bytes)."""
+    return rows * D * 7 + rows * 12 + rows // 8
 
 
 def _check_search(index, probes):

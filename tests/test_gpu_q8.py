@@ -23,10 +23,19 @@ def store():
     idx.close()
 
 
-def test_q8_is_the_automatic_batched_kind(store):
+def test_q8_kind_selection(store):
+    """K1q is automatic for batched searches only with CM_DENSE_Q8=1 (K1c otherwise); a forced
+    set_path(Q8) always takes it; K1s keeps the small batches."""
+    import os
     _, idx = store
-    assert idx.search_kind(256, 24) == Q8 and idx.search_kind(64, 10) == Q8
-    assert idx.search_kind(16, 10) == 4          # K1s keeps the small batches
+    auto = Q8 if os.environ.get("CM_DENSE_Q8", "") == "1" else COARSE
+    assert idx.search_kind(256, 24) == auto and idx.search_kind(64, 10) == auto
+    assert idx.search_kind(16, 10) == 4
+    idx.set_path(Q8)
+    try:
+        assert idx.search_kind(256, 24) == Q8
+    finally:
+        idx.set_path(0)
 
 
 @pytest.mark.parametrize("nq", [256, 100, 40])
@@ -89,9 +98,13 @@ def test_q8_device_search_and_workspace(store):
     import torch
     C, idx = store
     Q = mixed_queries(C, 256, seed=77)
-    d_h, r_h = idx.search(Q, 24)
-    q = torch.from_numpy(Q).cuda()
-    d, r = idx.search_dev(q, 24)
-    torch.cuda.synchronize()
+    idx.set_path(Q8)
+    try:
+        d_h, r_h = idx.search(Q, 24)
+        q = torch.from_numpy(Q).cuda()
+        d, r = idx.search_dev(q, 24)
+        torch.cuda.synchronize()
+    finally:
+        idx.set_path(0)
     assert np.array_equal(r.cpu().numpy(), r_h)
     assert np.array_equal(d.cpu().numpy(), d_h)

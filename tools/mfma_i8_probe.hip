@@ -5,6 +5,9 @@
 //   H2: A[row i][k = 8 g + j (j < 8), 32 + 8 g + j - 8 (j >= 8)], B likewise
 // For each map, A and B fragments are packed from known matrices; the MFMA result is compared with
 // the host product (C/D map: col = l & 15, row = 4 (l >> 4) + r, dtype-independent on gfx950).
+// Measured: BOTH maps reproduce the product exactly -- a k permutation applied to A and B alike
+// leaves the dot product unchanged, so K1q's correctness needs only that rows and queries are
+// packed with the same map (they are: q8_plane_off / q8_query_off share q8_ge).
 //   hipcc --offload-arch=gfx950 -O2 tools/mfma_i8_probe.hip -o tools/mfma_i8_probe && ./tools/mfma_i8_probe
 #include <hip/hip_runtime.h>
 

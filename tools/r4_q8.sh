@@ -5,7 +5,7 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"; mkdir -p gpurun_out/q8; export TMPDIR=/tmp
 timeout -k 10 60 ./tools/mfma_i8_probe > gpurun_out/q8/probe.txt 2>&1 || { cat gpurun_out/q8/probe.txt; exit 1; }
 cat gpurun_out/q8/probe.txt
-if grep -q "map H1: ran, 0 of 256" gpurun_out/q8/probe.txt; then echo "map 1 (product build)";
+if grep -q "map H1: ran, 0 of 256" gpurun_out/q8/probe.txt; then echo "map 1 (product build; any k permutation shared by A and B is exact)";
 elif grep -q "map H2: ran, 0 of 256" gpurun_out/q8/probe.txt; then echo "map 2 (variant build)"; export CLASSMATE_HIP_LIB=$PWD/variants/lib_q8map2.so;
 else echo "neither operand map matches: stop"; exit 1; fi
 timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_q8.py tests/test_gpu_growth.py \
