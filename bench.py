@@ -889,10 +889,20 @@ def run_e2e(args, rank, ws, dev):
             for i in range(3):                             # batch-1 shapes: first-call setup
                 retr.retrieve(question=qs[-1 - i], filters=f, top_k=K)
             lat = []
+            lprof = None
+            if os.environ.get("CM_E2E_PROFILE_LAT"):       # host-side profile of the single-query calls
+                import cProfile
+                lprof = cProfile.Profile()
+                lprof.enable()
             for i in range(args.e2e_latency_queries):
                 t1 = time.perf_counter()
                 retr.retrieve(question=qs[i], filters=f, top_k=K)
                 lat.append((time.perf_counter() - t1) * 1e3)
+            if lprof is not None:
+                import pstats
+                lprof.disable()
+                print(f"---- host profile, retrieve() {name}", file=sys.stderr)
+                pstats.Stats(lprof, stream=sys.stderr).sort_stats("tottime").print_stats(25)
         finally:
             device_batch.retrieve_batch = real
         lat.sort()

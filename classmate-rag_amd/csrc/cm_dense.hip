@@ -1744,6 +1744,7 @@ struct CoarseWs {
   float *qnorm;       // [nq_pad][4]
   uint64_t *keys;     // candidate buffers [pass][group][qs][kCBufCap]
   uint32_t *cnt;      // buffer fill counts [pass][group][qs]
+  float *ups;         // K1q: d~ + E_r beside every candidate key [pass][group][qs][kQCap]
   float *mins;        // sample minima [pass][sample group][qs]
   float *seed;        // per-query insertion bound from the sample
   int32_t *fb_mask;   // queries sent to the exact K1 pass
@@ -1769,6 +1770,7 @@ CoarseWs coarse_ws_layout(const cm_dense *h, const CoarseCfg &c, int nq, int k, 
   w.qh = reinterpret_cast<_Float16 *>(take(nq_pad * h->ld * 2));
   w.qnorm = reinterpret_cast<float *>(take(nq_pad * 16));
   w.keys = reinterpret_cast<uint64_t *>(take((int64_t)c.n_pass * c.n_wg * c.qs * cap * 8));
+  if (c.q8) w.ups = reinterpret_cast<float *>(take((int64_t)c.n_pass * c.n_wg * c.qs * cap * 4));
   w.cnt = reinterpret_cast<uint32_t *>(take((int64_t)c.n_pass * c.n_wg * c.qs * 4));
   w.mins = reinterpret_cast<float *>(take((int64_t)c.n_pass * c.n_wg_sample * c.qs * 4));
   w.seed = reinterpret_cast<float *>(take(nq_pad * 4));
@@ -1795,8 +1797,9 @@ int set_coarse_attrs() {
         {reinterpret_cast<const void *>(&dense_coarse_scan_kernel<6, 0, false, 4, 20, 128>), K1rLds<0, 20>::total},
         {reinterpret_cast<const void *>(&dense_coarse_scan_kernel<6, 0, true, 4, 20, 128>), K1rLds<0, 20>::total},
         {reinterpret_cast<const void *>(&dense_rerank_kernel), kGatherCap * 12},
-        {reinterpret_cast<const void *>(&dense_q8_scan_kernel<false>), kQRing * 8192},
-        {reinterpret_cast<const void *>(&dense_q8_scan_kernel<true>), kQRing * 8192}};
+        {reinterpret_cast<const void *>(&dense_q8_scan_kernel<false>), kQLds},
+        {reinterpret_cast<const void *>(&dense_q8_scan_kernel<true>), kQLds},
+        {reinterpret_cast<const void *>(&dense_rerank_q8_kernel), kQRerankLds}};
     for (const auto &f : fs) {
       const hipError_t e = hipFuncSetAttribute(f.first, hipFuncAttributeMaxDynamicSharedMemorySize, f.second);
       if (e != hipSuccess) err = e;
@@ -1838,22 +1841,22 @@ int launch_coarse(cm_dense *h, const float *q_dev, int nq, int k, int kind, cons
     hipLaunchKernelGGL(dense_prep_q8, dim3(c.n_pass * c.qs), dim3(256), 0, st, q_dev, nq, h->dim, h->ld, w.qq, w.qsc,
                        reinterpret_cast<const uint32_t *>(h->rnorm));
     CM_HIP(hipGetLastError());
-    hipLaunchKernelGGL(dense_q8_scan_kernel<true>, dim3(c.n_pass * c.n_wg_sample), dim3(256), kQRing * 8192, st, h->Xq,
+    hipLaunchKernelGGL(dense_q8_scan_kernel<true>, dim3(c.n_pass * c.n_wg_sample), dim3(256), kQLds, st, h->Xq,
                        h->rmeta, h->live, allow, n_words, w.qq, w.qsc, nq, (const float *)nullptr,
                        c.rows_per_wg_sample, c.rows_end_sample, c.n_wg_sample, (uint64_t *)nullptr,
-                       (uint32_t *)nullptr, w.mins);
+                       (float *)nullptr, (uint32_t *)nullptr, w.mins);
     CM_HIP(hipGetLastError());
     hipLaunchKernelGGL(dense_seed_kernel, dim3(nq), dim3(256), 0, st, w.mins, c.n_wg_sample, c.qs, k, nq, w.qnorm,
                        h->rnorm, h->dim, w.seed, 0);
     CM_HIP(hipGetLastError());
     h->timer.begin(st);
-    hipLaunchKernelGGL(dense_q8_scan_kernel<false>, dim3(c.n_pass * c.n_wg), dim3(256), kQRing * 8192, st, h->Xq,
+    hipLaunchKernelGGL(dense_q8_scan_kernel<false>, dim3(c.n_pass * c.n_wg), dim3(256), kQLds, st, h->Xq,
                        h->rmeta, h->live, allow, n_words, w.qq, w.qsc, nq, (const float *)w.seed, c.rows_per_wg,
-                       c.rows_end, c.n_wg, w.keys, w.cnt, (float *)nullptr);
+                       c.rows_end, c.n_wg, w.keys, w.ups, w.cnt, (float *)nullptr);
     h->timer.end(st);
     CM_HIP(hipGetLastError());
-    hipLaunchKernelGGL(dense_rerank_q8_kernel, dim3(nq), dim3(256), 0, st, w.keys, w.cnt, c.n_wg, k, nq, h->C, h->ld,
-                       h->dim, q_dev, w.qsc, h->rmeta, dist_dev, row_dev, w.fb_mask, w.fb_count);
+    hipLaunchKernelGGL(dense_rerank_q8_kernel, dim3(nq), dim3(256), kQRerankLds, st, w.keys, w.ups, w.cnt, c.n_wg, k,
+                       nq, h->C, h->ld, h->dim, q_dev, w.qsc, dist_dev, row_dev, w.fb_mask, w.fb_count);
     CM_HIP(hipGetLastError());
   } else {
   const bool d768 = h->ld == 768;
