@@ -805,7 +805,10 @@ __global__ void bm25_filtered_stats_kernel(const int32_t *__restrict__ dl, const
 }
 
 // Per listed term: number of candidate postings and the first candidate
-// posting's (doc << 32 | first position) key (terms' dict order).
+// posting's (doc << 32 | first position) key (terms' dict order).  gridDim.y > 1 (the per-query
+// df of a filtered search, out_first unused): block (i, s) counts slice s of the term's postings
+// and adds it to out_df[i] (zeroed by the caller) -- one block per term walked a frequent term's
+// whole list alone (2.7 ms per single filtered query at 1M documents).
 __global__ void __launch_bounds__(256) bm25_term_df_kernel(const int32_t *__restrict__ terms, int n_terms,
                                                            int32_t vocab, const int64_t *__restrict__ term_off,
                                                            const int32_t *__restrict__ post_doc,
@@ -827,7 +830,9 @@ __global__ void __launch_bounds__(256) bm25_term_df_kernel(const int32_t *__rest
   __shared__ unsigned long long red_m[4];
   unsigned long long c = 0, m = ~0ull;
   const int64_t lo = term_off[t], hi = term_off[t + 1];
-  for (int64_t p = lo + threadIdx.x; p < hi; p += 256) {
+  const int64_t stride = 256 * (int64_t)gridDim.y;
+  if (gridDim.y > 1 && lo + (int64_t)blockIdx.y * 256 >= hi) return;  // nothing in this slice
+  for (int64_t p = lo + (int64_t)blockIdx.y * 256 + threadIdx.x; p < hi; p += stride) {
     const int32_t d = post_doc[p];
     if ((live[d >> 5] & allow[d >> 5]) >> (d & 31) & 1u) {
       c += 1;
@@ -851,8 +856,12 @@ __global__ void __launch_bounds__(256) bm25_term_df_kernel(const int32_t *__rest
       cc += red_c[w];
       mm = red_m[w] < mm ? red_m[w] : mm;
     }
-    out_df[i] = (int64_t)cc;
-    if (out_first) out_first[i] = mm;
+    if (gridDim.y > 1) {
+      if (cc) atomicAdd(reinterpret_cast<unsigned long long *>(out_df + i), cc);
+    } else {
+      out_df[i] = (int64_t)cc;
+      if (out_first) out_first[i] = mm;
+    }
   }
 }
 
@@ -1979,10 +1988,11 @@ int cm_bm25_filter_stats_dev(cm_bm25 *h, const uint32_t *allow_dev, const int32_
     CM_HIP(hipGetLastError());
   }
   if (n_terms > 0) {
-    if (h->npost == 0) {
-      CM_HIP(hipMemsetAsync(df_dev, 0, (size_t)n_terms * 8, st));
-    } else {
-      hipLaunchKernelGGL(bm25_term_df_kernel, dim3((unsigned)n_terms), dim3(256), 0, st, q_terms_dev, (int)n_terms,
+    CM_HIP(hipMemsetAsync(df_dev, 0, (size_t)n_terms * 8, st));
+    if (h->npost > 0) {
+      // slices per term: enough blocks for a single query's few terms, one for big batches
+      const unsigned sl = (unsigned)std::max(1, std::min(128, 4096 / n_terms));
+      hipLaunchKernelGGL(bm25_term_df_kernel, dim3((unsigned)n_terms, sl), dim3(256), 0, st, q_terms_dev, (int)n_terms,
                          h->vocab, h->term_off.as<int64_t>(), h->post_doc.as<int32_t>(), h->post_pos.as<uint32_t>(),
                          h->live.as<uint32_t>(), allow_dev, df_dev, (uint64_t *)nullptr);
       CM_HIP(hipGetLastError());

@@ -957,36 +957,6 @@ __global__ void __launch_bounds__(256, 1)
 // qs = queries per pass in the buffer layout (K1c: kBQPass, K1s: kSQ).
 #include "cm_dense_q8.inc"
 
-// seed[q] = the k-th smallest per-group minimum (+ 2E for K1c / K1s, whose minima are of the
-// coarse distance; K1q's minima already carry their rows' bounds: add_err = 0)
-__global__ void __launch_bounds__(256) dense_seed_kernel(const float *__restrict__ mins, int n_wg, int qs, int k,
-                                                         int nq, const float *__restrict__ qnorm,
-                                                         const float *__restrict__ row_norms, int dim,
-                                                         float *__restrict__ seed, int add_err) {
-  const int qi = blockIdx.x;
-  if (qi >= nq) return;
-  const int qp = qi / qs, ql = qi - qp * qs;
-  __shared__ float v[2048];
-  const int n = min(n_wg, 2048);
-  for (int i = threadIdx.x; i < n; i += 256) v[i] = mins[((int64_t)qp * n_wg + i) * qs + ql];
-  __syncthreads();
-  // the k-th smallest by rank counting (n <= 2048, ties broken by index)
-  __shared__ float kth;
-  if (threadIdx.x == 0) kth = __builtin_inff();
-  __syncthreads();
-  for (int i = threadIdx.x; i < n; i += 256) {
-    const float x = v[i];
-    if (!(x < __builtin_inff())) continue;
-    int rank = 0;
-    for (int m = 0; m < n; ++m) rank += (v[m] < x || (v[m] == x && m < i)) ? 1 : 0;
-    if (rank == k - 1) kth = x;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0)
-    seed[qi] = kth < __builtin_inff() ? (add_err ? kth + 2.0f * coarse_err(qnorm, qi, row_norms, dim) : kth)
-                                      : __builtin_inff();
-}
-
 // Block-wide radix select: the k-th smallest (0-based kk) of n u32 values in LDS (4 x 8-bit digits).
 __device__ inline uint32_t block_select_u32(const uint32_t *vals, int n, int kk, uint32_t *hist /*[256]*/) {
   __shared__ uint32_t s_prefix, s_rem;
@@ -1013,6 +983,28 @@ __device__ inline uint32_t block_select_u32(const uint32_t *vals, int n, int kk,
     __syncthreads();
   }
   return s_prefix;
+}
+
+// seed[q] = the k-th smallest per-group minimum (+ 2E for K1c / K1s, whose minima are of the
+// coarse distance; K1q's minima already carry their rows' bounds: add_err = 0)
+__global__ void __launch_bounds__(256) dense_seed_kernel(const float *__restrict__ mins, int n_wg, int qs, int k,
+                                                         int nq, const float *__restrict__ qnorm,
+                                                         const float *__restrict__ row_norms, int dim,
+                                                         float *__restrict__ seed, int add_err) {
+  const int qi = blockIdx.x;
+  if (qi >= nq) return;
+  const int qp = qi / qs, ql = qi - qp * qs;
+  __shared__ uint32_t v[2048];
+  __shared__ uint32_t hist[256];
+  const int n = min(n_wg, 2048);
+  for (int i = threadIdx.x; i < n; i += 256) v[i] = f32_order(mins[((int64_t)qp * n_wg + i) * qs + ql]);
+  __syncthreads();
+  // the k-th smallest minimum (radix select; +inf when fewer than k groups hold a finite one --
+  // the O(n^2) rank count it replaces took ~0.1 ms per single-query search)
+  const float kth = n >= k ? f32_unorder(block_select_u32(v, n, k - 1, hist)) : __builtin_inff();
+  if (threadIdx.x == 0)
+    seed[qi] = kth < __builtin_inff() ? (add_err ? kth + 2.0f * coarse_err(qnorm, qi, row_norms, dim) : kth)
+                                      : __builtin_inff();
 }
 
 // K1c certification + exact re-rank, one 256-thread workgroup per query.
