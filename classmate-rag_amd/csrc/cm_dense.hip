@@ -1664,9 +1664,9 @@ int dense_kind(const cm_dense *h, int nq, int k) {
     return s == "f32" ? CM_DENSE_F32 : s == "coarse" ? CM_DENSE_COARSE : s == "stream" ? CM_DENSE_STREAM
          : s == "q8" ? CM_DENSE_Q8 : 0;
   }();
-  static const bool q8_auto = [] {  // K1q automatic for batched dim-768 searches: CM_DENSE_Q8=1
+  static const bool q8_auto = [] {  // K1q automatic for batched dim-768 searches (CM_DENSE_Q8=0: K1c)
     const char *e = getenv("CM_DENSE_Q8");
-    return e && e[0] == '1';
+    return !(e && e[0] == '0');
   }();
   const int force = h->path ? h->path : env_force;
   // coarse scans: resident-query instances for ld 768 / 384, a sample of >= 1024 rows for the seed

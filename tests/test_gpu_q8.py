@@ -24,11 +24,11 @@ def store():
 
 
 def test_q8_kind_selection(store):
-    """K1q is automatic for batched searches only with CM_DENSE_Q8=1 (K1c otherwise); a forced
-    set_path(Q8) always takes it; K1s keeps the small batches."""
+    """K1q is the automatic batched kind (CM_DENSE_Q8=0 selects K1c); a forced set_path(Q8) always
+    takes it; K1s keeps the small batches."""
     import os
     _, idx = store
-    auto = Q8 if os.environ.get("CM_DENSE_Q8", "") == "1" else COARSE
+    auto = COARSE if os.environ.get("CM_DENSE_Q8", "") == "0" else Q8
     assert idx.search_kind(256, 24) == auto and idx.search_kind(64, 10) == auto
     assert idx.search_kind(16, 10) == 4
     idx.set_path(Q8)

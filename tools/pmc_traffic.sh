@@ -1,5 +1,5 @@
 #!/bin/bash
-# GPU: HBM traffic per launch of the dominant kernels (K1c B=256, K1s B=16, K2a B=256) at the bench
+# GPU: HBM traffic per launch of the dominant kernels (K1c / K1q B=256, K1s B=16, K2a B=256) at the bench
 # shape, from separate rocprofv3 --pmc passes (FETCH_SIZE; WRITE_SIZE + TCC hit/miss), each pass its
 # own run.  Writes gpurun_out/pmc_traffic_<round>.txt (per-launch averages) and .json.
 cd "${GRAFT_REPO_ROOT:-.}"; mkdir -p gpurun_out; export TMPDIR=/tmp
@@ -36,7 +36,8 @@ rm -f gpurun_out/pmc_traffic_${R}.txt gpurun_out/pmc_traffic_${R}.json
 W=${ONLY:-dense_B256 dense_B16 bm25_B256}   # ONLY="bm25_B256 ..." -> a subset
 for n in $W; do
   case $n in
-    dense_B256) run dense_B256 "dense_coarse_scan_kernelILi12ELi3ELb0" python3 tools/dense_probe.py --reps 3 --batch 256 || exit 1 ;;
+    dense_B256) run dense_B256 "dense_coarse_scan_kernelILi12ELi3ELb0" python3 tools/dense_probe.py --reps 3 --batch 256 --path 3 || exit 1 ;;
+    dense_q8_B256) run dense_q8_B256 "dense_q8_scan_kernelILb0" python3 tools/dense_probe.py --reps 3 --batch 256 --path 5 || exit 1 ;;
     dense_B16) run dense_B16 "dense_stream_scan_kernelILi12ELi1ELb0" python3 tools/dense_probe.py --reps 3 --batch 16 || exit 1 ;;
     bm25_B256) run bm25_B256 "bm25_tail_kernel" python3 tools/bm25_probe.py --paths 2 --reps 3 || exit 1 ;;
     bm25b_B256) run bm25b_B256 "bm25_block_kernel" python3 tools/bm25_probe.py --paths 2 --reps 3 || exit 1 ;;
