@@ -1212,8 +1212,7 @@ __global__ void __launch_bounds__(256) dense_scatter_kernel(const float *__restr
                                                             int64_t row0, int64_t n, int dim, int ld,
                                                             float *__restrict__ C, float *__restrict__ invc,
                                                             uint32_t *__restrict__ live, _Float16 *__restrict__ Xh,
-                                                            uint32_t *__restrict__ rnorm, int8_t *__restrict__ Xq,
-                                                            float2 *__restrict__ rmeta) {
+                                                            uint32_t *__restrict__ rnorm) {
   const int64_t i = blockIdx.x;
   if (i >= n) return;
   const int64_t r = rows ? rows[i] : row0 + i;
@@ -1263,8 +1262,7 @@ __global__ void __launch_bounds__(256) dense_scatter_kernel(const float *__restr
     atomicMax(&rnorm[0], __float_as_uint(nh));
     atomicMax(&rnorm[1], __float_as_uint(nl));
   }
-  q8_row(s, inv, dim, ld, r, Xq, rmeta, rnorm);  // the int8 plane of K1q (from the same xn)
-}
+}  // the int8 plane of K1q follows per row group (dense_q8_group_kernel, launched after the scatter)
 
 __global__ void dense_clear_live_kernel(const int64_t *__restrict__ rows, int64_t n, int64_t size,
                                         uint32_t *__restrict__ live) {
@@ -1602,8 +1600,9 @@ int dense_grow(cm_dense *h, int64_t need_rows) {
     hipLaunchKernelGGL(dense_replane_kernel, dim3((unsigned)keep), dim3(256), 0, h->stream, a.C, a.invc, keep, h->dim,
                        h->ld, a.Xh);
     CM_HIP(hipGetLastError());
-    hipLaunchKernelGGL(dense_q8_replane_kernel, dim3((unsigned)keep), dim3(256), 0, h->stream, a.C, a.invc, keep,
-                       h->dim, h->ld, a.Xq, a.rmeta, reinterpret_cast<uint32_t *>(h->rnorm));
+    hipLaunchKernelGGL(dense_q8_group_kernel, dim3((unsigned)(keep / 16)), dim3(256), 0, h->stream, a.C, a.invc,
+                       (const int64_t *)nullptr, (int64_t)0, keep / 16, h->dim, h->ld, a.Xq, a.rmeta,
+                       reinterpret_cast<uint32_t *>(h->rnorm));
     CM_HIP(hipGetLastError());
     CM_HIP(hipStreamSynchronize(h->stream));
     ++h->staged_growths;
@@ -2049,7 +2048,17 @@ int cm_dense_upsert(cm_dense *h, const float *vecs, const int64_t *rows, int64_t
     CM_HIP(hipMemcpyAsync(h->rows_buf.ptr, rows + s, (size_t)m * 8, hipMemcpyHostToDevice, h->stream));
     hipLaunchKernelGGL(dense_scatter_kernel, dim3((unsigned)m), dim3(256), 0, h->stream, h->staging.as<float>(),
                        h->rows_buf.as<int64_t>(), (int64_t)0, m, h->dim, h->ld, h->C, h->invc, h->live, h->Xh,
-                       reinterpret_cast<uint32_t *>(h->rnorm), h->Xq, h->rmeta);
+                       reinterpret_cast<uint32_t *>(h->rnorm));
+    CM_HIP(hipGetLastError());
+    // the int8 plane: every row group the batch touched, once (stream-ordered after the scatter)
+    std::vector<int64_t> gs((size_t)m);
+    for (int64_t i = 0; i < m; ++i) gs[(size_t)i] = q8_group_of(rows[s + i]);
+    std::sort(gs.begin(), gs.end());
+    gs.erase(std::unique(gs.begin(), gs.end()), gs.end());
+    CM_HIP(hipMemcpyAsync(h->rows_buf.ptr, gs.data(), gs.size() * 8, hipMemcpyHostToDevice, h->stream));
+    hipLaunchKernelGGL(dense_q8_group_kernel, dim3((unsigned)gs.size()), dim3(256), 0, h->stream, h->C, h->invc,
+                       h->rows_buf.as<int64_t>(), (int64_t)0, (int64_t)gs.size(), h->dim, h->ld, h->Xq, h->rmeta,
+                       reinterpret_cast<uint32_t *>(h->rnorm));
     CM_HIP(hipGetLastError());
     CM_HIP(hipStreamSynchronize(h->stream));
   }
@@ -2073,9 +2082,15 @@ int cm_dense_upsert_dev(cm_dense *h, const float *vecs_dev, int64_t row0, int64_
     const int64_t m = std::min(batch, n - s);
     hipLaunchKernelGGL(dense_scatter_kernel, dim3((unsigned)m), dim3(256), 0, st, vecs_dev + s * h->dim,
                        (const int64_t *)nullptr, row0 + s, m, h->dim, h->ld, h->C, h->invc, h->live, h->Xh,
-                       reinterpret_cast<uint32_t *>(h->rnorm), h->Xq, h->rmeta);
+                       reinterpret_cast<uint32_t *>(h->rnorm));
     CM_HIP(hipGetLastError());
   }
+  // the int8 plane of every row group in the written tiles (rows_alloc is a multiple of 128)
+  const int64_t g_lo = (row0 >> 6) * 4, g_hi = ((row0 + n - 1) >> 6) * 4 + 4;
+  hipLaunchKernelGGL(dense_q8_group_kernel, dim3((unsigned)(g_hi - g_lo)), dim3(256), 0, st, h->C, h->invc,
+                     (const int64_t *)nullptr, g_lo, g_hi - g_lo, h->dim, h->ld, h->Xq, h->rmeta,
+                     reinterpret_cast<uint32_t *>(h->rnorm));
+  CM_HIP(hipGetLastError());
   h->size = std::max(h->size, row0 + n);
   return CM_OK;
 }
