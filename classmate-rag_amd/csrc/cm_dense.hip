@@ -985,8 +985,10 @@ __device__ inline uint32_t block_select_u32(const uint32_t *vals, int n, int kk,
   return s_prefix;
 }
 
-// seed[q] = the k-th smallest per-group minimum (+ 2E for K1c / K1s, whose minima are of the
-// coarse distance; K1q's minima already carry their rows' bounds: add_err = 0)
+// seed[q] = the k-th smallest per-group minimum + add_err x E: K1c / K1s add 2E (their minima are
+// coarse f16 distances and their scans test the coarse distance against the seed), K1q seeded from
+// the same f16 sample adds E (its scan tests a lower bound of the true distance), K1q seeded from
+// its own int8 sample adds nothing (those minima already carry their rows' bounds)
 __global__ void __launch_bounds__(256) dense_seed_kernel(const float *__restrict__ mins, int n_wg, int qs, int k,
                                                          int nq, const float *__restrict__ qnorm,
                                                          const float *__restrict__ row_norms, int dim,
@@ -1003,7 +1005,7 @@ __global__ void __launch_bounds__(256) dense_seed_kernel(const float *__restrict
   // the O(n^2) rank count it replaces took ~0.1 ms per single-query search)
   const float kth = n >= k ? f32_unorder(block_select_u32(v, n, k - 1, hist)) : __builtin_inff();
   if (threadIdx.x == 0)
-    seed[qi] = kth < __builtin_inff() ? (add_err ? kth + 2.0f * coarse_err(qnorm, qi, row_norms, dim) : kth)
+    seed[qi] = kth < __builtin_inff() ? (add_err ? kth + (float)add_err * coarse_err(qnorm, qi, row_norms, dim) : kth)
                                       : __builtin_inff();
 }
 
@@ -1693,6 +1695,19 @@ bool k1c_paired() {
   return p;
 }
 
+// K1q's seed: by default the K1c MINONLY scan over a 1/16 row sample of the f16 plane (its bound E is
+// ~30x tighter than the int8 plane's, so the seed lands near the sample's k-th distance and the scan
+// appends ~3x fewer candidates: 4-14k -> ~3k per query at 10M, profiles/r04b_k1q_abl.txt);
+// CM_K1Q_SEED=q8 keeps the int8 MINONLY pass over a 1/8 sample (A/B).
+bool k1q_seed_q8() {
+  static const bool v = [] {
+    const char *e = getenv("CM_K1Q_SEED");
+    return e && std::string(e) == "q8";
+  }();
+  return v;
+}
+int64_t k1q_sample_frac() { return k1q_seed_q8() ? kQSampleFrac : 16; }
+
 struct CoarseCfg {
   bool stream, paired, q8;
   int qs, n_pass, n_wg, n_wg_sample;
@@ -1722,7 +1737,7 @@ CoarseCfg coarse_config(const cm_dense *h, int nq, int kind) {
   };
   split(c.rows_end, c.rows_per_wg, c.n_wg);
   // K1q's per-row bounds widen the candidate set: a denser seed sample keeps it near ~4k per query
-  const int64_t frac = c.q8 ? kQSampleFrac : c.rows_end >= (1 << 20) ? 64 : 16;
+  const int64_t frac = c.q8 ? k1q_sample_frac() : c.rows_end >= (1 << 20) ? 64 : 16;
   c.rows_end_sample = round_up(std::max<int64_t>(c.rows_end / frac, 1), kRRows);
   split(c.rows_end_sample, c.rows_per_wg_sample, c.n_wg_sample);
   return c;
@@ -1828,17 +1843,25 @@ int launch_coarse(cm_dense *h, const float *q_dev, int nq, int k, int kind, cons
   CM_HIP(hipGetLastError());
   CM_HIP(hipMemsetAsync(w.fb_count, 0, 4, st));
   if (c.q8) {
-    // K1q: int8 queries -> 1/8-sample minima of d~ + E_r -> seed -> scan -> per-row certified re-rank
+    // K1q: int8 queries -> seed from a row sample -> scan -> certified re-rank (int8 band -> f16 band
+    // -> fp64)
     hipLaunchKernelGGL(dense_prep_q8, dim3(c.n_pass * c.qs), dim3(256), 0, st, q_dev, nq, h->dim, h->ld, w.qq, w.qsc,
                        reinterpret_cast<const uint32_t *>(h->rnorm));
     CM_HIP(hipGetLastError());
-    hipLaunchKernelGGL(dense_q8_scan_kernel<true>, dim3(c.n_pass * c.n_wg_sample), dim3(256), kQLds, st, h->Xq,
-                       h->rmeta, h->live, allow, n_words, w.qq, w.qsc, nq, (const float *)nullptr,
-                       c.rows_per_wg_sample, c.rows_end_sample, c.n_wg_sample, (uint64_t *)nullptr,
-                       (float *)nullptr, (uint32_t *)nullptr, w.mins);
+    if (k1q_seed_q8()) {
+      hipLaunchKernelGGL(dense_q8_scan_kernel<true>, dim3(c.n_pass * c.n_wg_sample), dim3(256), kQLds, st, h->Xq,
+                         h->rmeta, h->live, allow, n_words, w.qq, w.qsc, nq, (const float *)nullptr,
+                         c.rows_per_wg_sample, c.rows_end_sample, c.n_wg_sample, (uint64_t *)nullptr,
+                         (float *)nullptr, (uint32_t *)nullptr, w.mins);
+    } else {   // K1c MINONLY over the f16 plane's sample (dim 768: the resident-query instance)
+      hipLaunchKernelGGL((dense_coarse_scan_kernel<12, kK1cNql, true, kK1cWaves>), dim3(c.grid(c.n_wg_sample)),
+                         dim3(64 * kK1cWaves), K1rLds<kK1cNql>::total, st, h->Xh, h->live, allow, n_words, w.qh, nq,
+                         (const float *)nullptr, c.rows_per_wg_sample, c.rows_end_sample, c.n_wg_sample,
+                         (uint64_t *)nullptr, (uint32_t *)nullptr, w.mins, 0);
+    }
     CM_HIP(hipGetLastError());
     hipLaunchKernelGGL(dense_seed_kernel, dim3(nq), dim3(256), 0, st, w.mins, c.n_wg_sample, c.qs, k, nq, w.qnorm,
-                       h->rnorm, h->dim, w.seed, 0);
+                       h->rnorm, h->dim, w.seed, k1q_seed_q8() ? 0 : 1);
     CM_HIP(hipGetLastError());
     h->timer.begin(st);
     hipLaunchKernelGGL(dense_q8_scan_kernel<false>, dim3(c.n_pass * c.n_wg), dim3(256), kQLds, st, h->Xq,
@@ -1847,7 +1870,8 @@ int launch_coarse(cm_dense *h, const float *q_dev, int nq, int k, int kind, cons
     h->timer.end(st);
     CM_HIP(hipGetLastError());
     hipLaunchKernelGGL(dense_rerank_q8_kernel, dim3(nq), dim3(256), kQRerankLds, st, w.keys, w.ups, w.cnt, c.n_wg, k,
-                       nq, h->C, h->ld, h->dim, q_dev, w.qsc, dist_dev, row_dev, w.fb_mask, w.fb_count);
+                       nq, h->C, h->ld, h->dim, q_dev, w.qsc, h->Xh, w.qh, w.qnorm, h->rnorm, dist_dev, row_dev,
+                       w.fb_mask, w.fb_count);
     CM_HIP(hipGetLastError());
   } else {
   const bool d768 = h->ld == 768;
@@ -1876,7 +1900,7 @@ int launch_coarse(cm_dense *h, const float *q_dev, int nq, int k, int kind, cons
   }
   CM_HIP(hipGetLastError());
   hipLaunchKernelGGL(dense_seed_kernel, dim3(nq), dim3(256), 0, st, w.mins, c.n_wg_sample, c.qs, k, nq, w.qnorm,
-                     h->rnorm, h->dim, w.seed, 1);
+                     h->rnorm, h->dim, w.seed, 2);
   CM_HIP(hipGetLastError());
   // 2. coarse scan: rows under the seed -> candidate buffers
   h->timer.begin(st);
