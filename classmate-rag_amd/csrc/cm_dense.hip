@@ -323,8 +323,12 @@ __host__ __device__ inline int64_t plane_off(int64_t row, int k, int ld) {
   const int64_t tile = row >> 6;
   const int rr = (int)(row & 63), rt = rr >> 4, j = rr & 15;
   const int c = k >> 6, cc = k & 63, sb = cc >> 5, g = (cc >> 3) & 3, e = cc & 7;
-  return (((tile * (ld >> 6) + c) * 8 + rt * 2 + sb) << 9) + ((g * 16 + j) << 3) + e;
+  return (((tile * (ld >> 6) + c) * 8 + rt * 2 + sb) << 9) + ((j * 4 + g) << 3) + e;
 }
+// The plane keeps each (row, k-half) of a block as one 64-B run (piece g of row j at (4 j + g) x 16 B),
+// so a single row reads as 24 whole sectors (K1q's f16 re-rank stage); the MFMA operand order of
+// lane (g, j) is restored by the loads: lane l fetches piece plane_lane(l) of its block.
+__device__ inline int plane_lane(int lane) { return ((lane & 15) << 2) | (lane >> 4); }
 constexpr int kBQPass = 256;                // K1c: queries per pass (4 waves x 64)
 constexpr int kSQ = 32;                     // K1s: queries per launch (<= 2 q-tiles of 16)
 constexpr int kBMaxK = 32;                  // coarse paths: k <= 32
@@ -610,7 +614,7 @@ __global__ void __launch_bounds__(64 * W, 1)
     int gl = min(gc, total - 1);  // clamped: one control path past the end
     if (dbg & 8192) gl &= 15;     // bit 13: ablation only (L2-resident source: LDS traffic without HBM)
     const int o = W * i + wave;
-    __builtin_amdgcn_global_load_lds(Xb + (((cb + gl) * 8 + o) << 10) + lane * 16,
+    __builtin_amdgcn_global_load_lds(Xb + (((cb + gl) * 8 + o) << 10) + plane_lane(lane) * 16,
                                      (__attribute__((address_space(3))) void *)(lds + LL::ring + (gc % RING) * 8192 +
                                                                                 o * 1024),
                                      16, 0, K1C_AUX);
@@ -893,7 +897,7 @@ __global__ void __launch_bounds__(256, 1)
     f16x8 xb[R][8];
     auto load = [&](f16x8 (&b)[8], int gc) __attribute__((always_inline)) {
       const int gl = min(gc, total - 1);  // clamped: one control path past the end
-      const f16x8 *p = Xv + (tile0 * KC + gl) * 512 + lane;  // the wave's chunks are contiguous
+      const f16x8 *p = Xv + (tile0 * KC + gl) * 512 + plane_lane(lane);  // the wave's chunks are contiguous
 #pragma unroll
       for (int i = 0; i < 8; ++i) b[i] = K1S_NT ? __builtin_nontemporal_load(p + i * 64) : p[i * 64];
     };

@@ -3,7 +3,7 @@
 # scan probe (Gaussian queries), headline bench without side legs
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"; mkdir -p gpurun_out/v6; export TMPDIR=/tmp
-timeout -k 10 400 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_q8.py tests/test_gpu_growth.py \
+timeout -k 10 400 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_q8.py tests/test_gpu_growth.py tests/test_gpu_scale.py::test_dense_1m_x_768 \
   "tests/test_gpu_scale.py::test_hybrid_10m_sample" > gpurun_out/v6/pytest_q8.log 2>&1 || { tail -40 gpurun_out/v6/pytest_q8.log; exit 1; }
 tail -2 gpurun_out/v6/pytest_q8.log
 for rep in 1 2; do
