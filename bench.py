@@ -415,12 +415,12 @@ def main():
         "value": qps, "unit": "queries/s", "n_gpus": ws, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None,
-        "dtype": ("fp32-accurate E5 (K10 f16x3 MFMA) + f16/f64 dense + f64 BM25" if use_e5 and
-                  args.e5_dtype == "float32" else "f16+f64"),
+        "dtype": (("fp32-accurate E5 (K10 f16x3 MFMA) + " + ("int8/f16/f64" if kind == 5 else "f16/f64")
+                   + " dense + f64 BM25") if use_e5 and args.e5_dtype == "float32" else "f16+f64"),
         "dtypes": {"dense_knn": {1: "f32 (MFMA)", 3: "f16 coarse (MFMA) + fp64 exact re-rank of the certified band",
                                  4: "f16 coarse (MFMA) + fp64 exact re-rank of the certified band",
-                                 5: "int8 coarse (i8 MFMA, per-row scales) + fp64 exact re-rank of the per-row "
-                                    "certified band"}[kind],
+                                 5: "int8 coarse (i8 MFMA, 16-row group scales) -> certified int8 band -> "
+                                    "certified f16 band -> fp64 exact re-rank"}[kind],
                    "bm25": "f64", "fusion": "f64",
                    "e5_forward": ({"float32": "fp32 (K10: split-precision f16 hi/lo MFMA, fp32 accumulate)",
                                    "bfloat16": "bf16"}[args.e5_dtype] if use_e5 else None)},
@@ -917,7 +917,7 @@ def run_e2e(args, rank, ws, dev):
         "metric": f"drop-in HybridRetriever.retrieve_batch queries/sec (strings -> result dicts), {N} chunks",
         "value": qps, "unit": "queries/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
-        "vs_baseline": None, "dtype": "fp32 E5 + f16/f64 dense + f64 BM25",
+        "vs_baseline": None, "dtype": "fp32 E5 + int8/f16/f64 dense + f64 BM25",
         "data": "synthetic (seeded): Zipf-word chunks, random unit embeddings, random-init E5-base weights",
         "config": {"workload": "drop-in retrieve_batch (E5 query encode + cosine pool 24 + MMR 8 + BM25 8 + RRF)",
                    "chunks": N, "words_per_chunk": args.e2e_words, "global_batch": B, "top_k": K, "dim": D},
