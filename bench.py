@@ -80,7 +80,10 @@ def parse_args():
     ap.add_argument("--no-graph", action="store_true", help="run the E5 query encode eagerly (no hipGraph)")
     ap.add_argument("--serial", action="store_true", help="run BM25 on the main stream (no overlap with E5 + dense)")
     ap.add_argument("--bm25-priority", type=int, default=0, help="HIP stream priority of the BM25 stream (-1 = high)")
-    ap.add_argument("--bm25-after-e5", action="store_true", help="launch BM25 after the E5 encode (overlap with dense)")
+    ap.add_argument("--bm25-with-e5", dest="bm25_after_e5", action="store_false",
+                    help="launch BM25 beside the E5 encode (the round-3 schedule); default: after the encode, "
+                         "beside the dense search, whose seed / re-rank / fusion kernels leave CUs to it "
+                         "(31.2k vs 30.5k q/s with K1q, profiles/r04b_sched_ab.txt)")
     ap.add_argument("--bm25-cus", default="", help="run the BM25 stream on a CU subset: 'first:N', 'stride:S' "
                     "(every S-th CU) or '' (all CUs)")
     ap.add_argument("--seq-len", type=int, default=256, help="ingest mode: tokens per chunk")
