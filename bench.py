@@ -408,7 +408,12 @@ def main():
         del e5
         e5 = main_e5
     if args.mode == "hybrid" and args.dense_legs:
-        legs.update(dense_legs(args, dense, N, D, dev, ws))
+        legs.update(dense_legs(args, dense, N, D, dev, ws, q_main, P))
+        # the in-step launch shares its CUs with the BM25 stream (launched after the encode, beside
+        # the dense search, since round 4), so its HIP-event time includes that time-sharing; the
+        # same launch alone (the step's own queries, same shard) is the kernel's own roofline
+        if "c4_dense_10m_b256" in legs:
+            roof["standalone"] = legs["c4_dense_10m_b256"]["roofline"]
     if use_e5 and args.ingest_leg:
         legs["ingest_fp32"], roofs["e5_ingest"] = ingest_leg(args, e5["emb"] if e5["dtype"] == "float32" else None,
                                                            dev, ws, rank)
@@ -539,23 +544,27 @@ def _e5_roofline(bq, S, layers, ms, dtype):
             "vs_fp32_mfma_peak": alg / (ms * 1e-3) / 1e12 / PEAK_F32_MFMA_TFLOPS}
 
 
-def dense_legs(args, dense, N, D, dev, ws):
+def dense_legs(args, dense, N, D, dev, ws, q_step=None, pool=None):
     """north_star's dense configurations, timed in the same run (side fields, not the headline):
     C2' = this rank's 10M shard at B = 16, k = 10 (the HBM-bound case the >= 80 % target names);
-    C2 = a 1M-chunk shard (its own index), B = 256, k = 10.  Queries: unit Gaussian."""
+    C2 = a 1M-chunk shard (its own index), B = 256, k = 10 (queries: unit Gaussian); and the
+    headline's dense search alone -- the step's own query embeddings and pool size on this shard,
+    without the BM25 stream beside it."""
     import torch
     from classmate_hip import engine, parallel
     legs = {}
 
-    def leg(index, n, b, name):
-        g = torch.Generator(device="cuda").manual_seed(args.seed * 31 + b)
-        q = torch.randn(b, D, device=dev, generator=g)
-        q /= q.norm(dim=1, keepdim=True)
-        ws_buf = torch.empty(index.workspace_bytes(b, args.k), dtype=torch.uint8, device=dev)
-        o = (torch.empty((b, args.k), dtype=torch.float32, device=dev),
-             torch.empty((b, args.k), dtype=torch.int64, device=dev))
+    def leg(index, n, b, name, q=None, kk=None):
+        kk = kk or args.k
+        if q is None:
+            g = torch.Generator(device="cuda").manual_seed(args.seed * 31 + b)
+            q = torch.randn(b, D, device=dev, generator=g)
+            q /= q.norm(dim=1, keepdim=True)
+        ws_buf = torch.empty(index.workspace_bytes(b, kk), dtype=torch.uint8, device=dev)
+        o = (torch.empty((b, kk), dtype=torch.float32, device=dev),
+             torch.empty((b, kk), dtype=torch.int64, device=dev))
         for _ in range(args.warmup):
-            index.search_dev(q, args.k, out=o, workspace=ws_buf)
+            index.search_dev(q, kk, out=o, workspace=ws_buf)
         torch.cuda.synchronize()
         index.timing(True)
         if ws > 1:
@@ -563,20 +572,24 @@ def dense_legs(args, dense, N, D, dev, ws):
         t0 = time.perf_counter()
         steps = max(args.steps, 10)
         for _ in range(steps):
-            index.search_dev(q, args.k, out=o, workspace=ws_buf)
+            index.search_dev(q, kk, out=o, workspace=ws_buf)
         torch.cuda.synchronize()
         if ws > 1:
             torch.distributed.barrier()
         el = parallel.max_over_ranks(time.perf_counter() - t0, device=dev)
         kt = index.timing_drain()
         index.timing(False)
-        kind = index.search_kind(b, args.k)
-        r = _dense_roofline(kind, n, D, b, sum(kt) / len(kt), None)
+        kind = index.search_kind(b, kk)
+        r = _dense_roofline(kind, n, D, b, sum(kt) / len(kt),
+                            _pmc_traffic(args, "dense_q8" if kind == 5 else "dense") if n == args.docs_per_gpu
+                            and b == args.batch else None)
         legs[name] = {"value": b * steps * ws / el, "unit": "queries/s", "ms_per_step": el / steps * 1e3,
-                      "config": {"chunks_per_gpu": n, "batch": b, "k": args.k, "dim": D},
+                      "config": {"chunks_per_gpu": n, "batch": b, "k": kk, "dim": D},
                       "roofline": r}
         log(f"{name}: {b * steps * ws / el:.0f} q/s, scan {r['avg_launch_ms']:.3f} ms = {r['frac']:.3f} of {r['bound']}")
 
+    if q_step is not None and q_step.shape[0] == args.batch:
+        leg(dense, N, args.batch, "c4_dense_10m_b256", q=q_step.contiguous(), kk=pool)
     leg(dense, N, 16, "c2p_dense_10m_b16")
     n1 = min(1_000_000, N)
     d1 = engine.DenseIndex(D, device=dev.index, capacity=n1)
