@@ -84,6 +84,9 @@ def parse_args():
                     help="launch BM25 beside the E5 encode (the round-3 schedule); default: after the encode, "
                          "beside the dense search, whose seed / re-rank / fusion kernels leave CUs to it "
                          "(31.2k vs 30.5k q/s with K1q, profiles/r04b_sched_ab.txt)")
+    ap.add_argument("--pipeline", type=int, default=0,
+                    help="1 (2: on a high-priority stream) = encode batch i+1 (its own hipGraph + output buffer, its own stream) while batch i is "
+                         "searched; every step still runs one whole encode and one whole search")
     ap.add_argument("--bm25-cus", default="", help="run the BM25 stream on a CU subset: 'first:N', 'stride:S' "
                     "(every S-th CU) or '' (all CUs)")
     ap.add_argument("--seq-len", type=int, default=256, help="ingest mode: tokens per chunk")
@@ -234,6 +237,13 @@ def main():
             return dict(emb=m, graph=gr, qbuf=out_buf, ids=g_ids, mask=g_mask, dtype=dtype)
 
         e5 = make_e5(args.e5_dtype)
+        if args.pipeline and e5["graph"] is not None:
+            # the second batch slot: its own graph (own memory pool), inputs and output buffer
+            g_ids, g_mask, out_buf, gr = e5["emb"].capture_graph(bq, args.q_tokens, unpadded=True)
+            g_ids.copy_(ids[blk])
+            g_mask.copy_(mask[blk])
+            e5["slots"] = [dict(graph=e5["graph"], qbuf=e5["qbuf"]), dict(graph=gr, qbuf=out_buf, ids=g_ids,
+                                                                          mask=g_mask)]
     else:
         g = torch.Generator(device="cuda").manual_seed(args.seed * 17)
         qfix = torch.randn(B, D, device=dev, generator=g)
@@ -274,8 +284,40 @@ def main():
                 e["b1"].record()
         return out
 
+    pipe = dict(it=0, stream=None, ready=None)
+    if use_e5 and "slots" in e5:
+        # a stream of another priority gets its own hardware queue (same-priority streams may share
+        # one of the GPU_MAX_HW_QUEUES = 4 round-robin queues and then run in submission order)
+        pipe["stream"] = torch.cuda.Stream(device=dev, priority=-1 if args.pipeline == 2 else 0)
+        pipe["ready"] = [torch.cuda.Event(), torch.cuda.Event()]
+
+    def encode_pipelined(e):
+        """--pipeline: replay the NEXT batch's graph on the encode stream (after the previous step's
+        search, the last reader of that slot, has run on main), return THIS batch's embeddings."""
+        es, it = pipe["stream"], pipe["it"]
+        cur, nxt = it % 2, (it + 1) % 2
+        es.wait_stream(main)
+        with torch.cuda.stream(es):
+            if it == 0:                      # first call: this batch's encode too
+                e5["slots"][cur]["graph"].replay()
+                pipe["ready"][cur].record(es)
+            if e:
+                e["e0"].record(es)
+            e5["slots"][nxt]["graph"].replay()
+            if e:
+                e["e1"].record(es)
+            pipe["ready"][nxt].record(es)
+        main.wait_event(pipe["ready"][cur])
+        pipe["it"] = it + 1
+        q_local = e5["slots"][cur]["qbuf"]
+        if ws == 1:
+            return q_local
+        return parallel.all_gather_into(qfull, q_local)
+
     def encode(e):
         """This rank's E5 block -> (B, D) query embeddings on the main stream."""
+        if pipe["stream"] is not None:
+            return encode_pipelined(e)
         if e:
             e["e0"].record()
         if e5["graph"] is not None:
@@ -326,6 +368,7 @@ def main():
         if record:
             ev.append(e)
         last_lists["pool"] = (rg, dm, brg, bsm, order, vecs)
+        last_lists["q"] = q
         # MMR-ordered vector list + list counts in one device pass, then the fused merge
         vk, vd, vn, bn = engine.rrf_pool_prep_dev(rg[blk].contiguous(), dm[blk].contiguous(), order,
                                                   brg[blk].contiguous(), out=pbuf)
@@ -359,7 +402,7 @@ def main():
     elapsed, res = timed(args.steps)
     # the recall check compares `res` with the oracle on the SAME step's inputs: keep this run's
     # query embeddings and merged lists before the side legs reuse the buffers (qfull at N > 1)
-    q_main = ((qfull if ws > 1 else e5["qbuf"]) if use_e5 else qfix).clone()
+    q_main = ((qfull if ws > 1 else last_lists.get("q", e5["qbuf"])) if use_e5 else qfix).clone()
     lists_main = tuple(t.clone() for t in last_lists["pool"]) if "pool" in last_lists else None
     mean_ms = lambda a, b: sum(x[a].elapsed_time(x[b]) for x in ev) / len(ev)   # noqa: E731
     search_ms = mean_ms("d0", "d1")
@@ -399,7 +442,9 @@ def main():
     if use_e5 and args.e5_other_leg:
         other = "bfloat16" if args.e5_dtype == "float32" else "float32"
         main_e5, e5 = e5, make_e5(other)
+        pipe_stream, pipe["stream"] = pipe["stream"], None     # the other precision's leg runs unpipelined
         el2, _ = timed(args.steps)
+        pipe["stream"] = pipe_stream
         ev.clear()
         legs["e5_" + {"bfloat16": "bf16", "float32": "fp32"}[other]] = {
             "value": B * args.steps / el2, "unit": "queries/s", "ms_per_step": el2 / args.steps * 1e3,
@@ -440,7 +485,9 @@ def main():
                    "bm25_vocab": args.vocab, "zipf_s": args.zipf, "chunk_len_mean": args.avg_len,
                    "query_terms": args.q_terms, "e5_query_tokens": args.q_tokens if use_e5 else None,
                    "e5_queries_per_rank": bq if use_e5 else None,
-                   "parallelism": f"corpus-shard x{ws}"},
+                   "parallelism": f"corpus-shard x{ws}",
+                   "schedule": ("pipelined: batch i+1 encoded beside batch i's search" if pipe["stream"] is not None
+                                else "serial: encode, then search")},
         "breakdown_ms": {"e5_encode": e5_ms, "dense_search": search_ms, "dense_scan_kernel": dense_ms,
                          "bm25_search": bsearch_ms, "bm25_tail_kernel": bm25_ms},
         "dense_exact_reruns": fallbacks,

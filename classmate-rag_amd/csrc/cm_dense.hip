@@ -1710,7 +1710,14 @@ bool k1q_seed_q8() {
   }();
   return v;
 }
-int64_t k1q_sample_frac() { return k1q_seed_q8() ? kQSampleFrac : 16; }
+int64_t k1q_sample_frac() {
+  static const int64_t v = [] {   // $CM_K1Q_SAMPLE = 1/fraction of the rows in the seed sample (A/B knob)
+    const char *e = getenv("CM_K1Q_SAMPLE");
+    const int64_t f = e ? atoll(e) : 0;
+    return f >= 2 && f <= 256 ? f : (k1q_seed_q8() ? (int64_t)kQSampleFrac : 16);
+  }();
+  return v;
+}
 
 struct CoarseCfg {
   bool stream, paired, q8;

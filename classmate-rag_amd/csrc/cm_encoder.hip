@@ -436,7 +436,6 @@ __global__ void __launch_bounds__(64) short_attention_f16x3_kernel(const float *
   constexpr int VT = 40;  // V^T row stride (keys, halves): 80 B keeps the 8-byte reads aligned
   constexpr float kPScale = 16384.f;  // P in [0, 1] -> [0, 2^14]
   __shared__ __attribute__((aligned(16))) _Float16 vt[2][kAttnDh * VT];
-  __shared__ __attribute__((aligned(16))) float oimg[32 * (kAttnDh + 4)];
   const int lane = threadIdx.x;
   const int g = lane >> 4, c = lane & 15;
   const int h = blockIdx.x % H;
@@ -549,6 +548,12 @@ __global__ void __launch_bounds__(64) short_attention_f16x3_kernel(const float *
   }
   __syncthreads();  // V^T staged
   const float oscale = a_scale / (kPScale * sv);  // exact power-of-two ratio
+  // O straight from the accumulators into the planes (no LDS transpose: the block's LDS is V^T alone,
+  // twice the resident blocks per CU): lane (g, c) holds rows 16 it + 4 g + r of column d = 16 dt + c;
+  // lanes c and c ^ 1 swap half their rows (DPP quad_perm 1,0,3,2) so each stores 4-byte column pairs
+  // (c even: rows 0-1, c odd: rows 2-3 of its group) -- K10's planes epilogue
+  const int kb32 = H * kAttnDh / 32;
+  const bool odd = c & 1;
 #pragma unroll
   for (int dt = 0; dt < kAttnDh / 16; ++dt) {
     const int d = 16 * dt + c;
@@ -563,28 +568,35 @@ __global__ void __launch_bounds__(64) short_attention_f16x3_kernel(const float *
     for (int it = 0; it < 2; ++it) {
       f32x4_t o = {0.f, 0.f, 0.f, 0.f};
       o = mfma3(ph[it], pl[it], vh, vl, o);
+      uint32_t hh[4], ll[4];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) oimg[(16 * it + 4 * g + r) * (kAttnDh + 4) + d] = o[r] * oscale;
-    }
-  }
-  __syncthreads();
-  // planes: query row i, dims h*64 + 8 s .. + 7 -> one 16-byte slot per plane
-  const int kb32 = H * kAttnDh / 32;
-#pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    const int t = lane + 64 * u, i = t >> 3, s8 = t & 7;
-    if (i < S) {
-      h16x8_t hh, ll;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
+      for (int r = 0; r < 4; ++r) {
         _Float16 a, b2;
-        f16x3_split1(oimg[i * (kAttnDh + 4) + 8 * s8 + e], a, b2);
-        hh[e] = a;
-        ll[e] = b2;
+        f16x3_split1(o[r] * oscale, a, b2);
+        hh[r] = __builtin_bit_cast(uint16_t, a);
+        ll[r] = __builtin_bit_cast(uint16_t, b2);
       }
-      const int64_t off = f16x3_plane_off(b * S + i, h * kAttnDh + 8 * s8, kb32);
-      *reinterpret_cast<h16x8_t *>(planes + off) = hh;
-      *reinterpret_cast<h16x8_t *>(planes + off + 512) = ll;
+      // even lane keeps rows 0-1 and sends 2-3; odd lane keeps 2-3 and sends 0-1
+      const uint32_t sh = odd ? (hh[0] | hh[1] << 16) : (hh[2] | hh[3] << 16);
+      const uint32_t sl = odd ? (ll[0] | ll[1] << 16) : (ll[2] | ll[3] << 16);
+      const uint32_t rh = (uint32_t)__builtin_amdgcn_mov_dpp((int)sh, 0xB1, 0xF, 0xF, false);
+      const uint32_t rl = (uint32_t)__builtin_amdgcn_mov_dpp((int)sl, 0xB1, 0xF, 0xF, false);
+      const int r0 = odd ? 2 : 0;
+      const int c0 = h * kAttnDh + (d & ~1);
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int i = 16 * it + 4 * g + r0 + q;
+        const uint32_t mine_h = hh[r0 + q], mine_l = ll[r0 + q];
+        const uint32_t oth_h = (rh >> (16 * q)) & 0xffffu, oth_l = (rl >> (16 * q)) & 0xffffu;
+        // column c0 (even) in the low half, c0 + 1 in the high half
+        const uint32_t wh = odd ? (oth_h | mine_h << 16) : (mine_h | oth_h << 16);
+        const uint32_t wl = odd ? (oth_l | mine_l << 16) : (mine_l | oth_l << 16);
+        if (i < S) {
+          const int64_t off = f16x3_plane_off(b * S + i, c0, kb32);
+          *reinterpret_cast<uint32_t *>(planes + off) = wh;
+          *reinterpret_cast<uint32_t *>(planes + off + 512) = wl;
+        }
+      }
     }
   }
 }
