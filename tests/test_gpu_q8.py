@@ -108,3 +108,42 @@ def test_q8_device_search_and_workspace(store):
         idx.set_path(0)
     assert np.array_equal(r.cpu().numpy(), r_h)
     assert np.array_equal(d.cpu().numpy(), d_h)
+
+
+def test_q8_band_overflow_takes_exact_fallback():
+    """Near-duplicate chunks (real corpora hold them; the synthetic bench never does): 12 000 rows
+    within 5e-4 of one base row put far more rows inside the int8 certificate than its 8192-row
+    band holds, so the re-rank hands those queries to the exact fp32 K1 pass (fb_mask) and the
+    merge writes only their rows.  Every list -- cluster and ordinary queries in one batch -- must
+    still equal the exact fp64 oracle, on K1q and on K1c."""
+    from classmate_hip import engine
+    rng = np.random.default_rng(91)
+    C = unit_rows(200_000, 768, seed=90)
+    base = C[7].astype(np.float64)
+    n_c = 12_000
+    at = rng.choice(np.arange(8, C.shape[0]), n_c, replace=False)
+    d_c = rng.permutation(np.linspace(1e-5, 5e-4, n_c))
+    u = rng.standard_normal((n_c, 768))
+    u -= np.outer(u @ base, base)                       # orthogonal to the base row
+    u /= np.linalg.norm(u, axis=1, keepdims=True)
+    t = np.sqrt(2.0 * d_c - d_c ** 2)                   # 1 - cos = d for x = cos.base + sin.u
+    x = np.sqrt(1.0 - t ** 2)[:, None] * base + t[:, None] * u
+    C[at] = x.astype(np.float32)
+    n_near = 8
+    Q = mixed_queries(C, 64, seed=92)
+    Q[:n_near] = (base + 1e-4 * rng.standard_normal((n_near, 768)) / np.sqrt(768)).astype(np.float32)
+    k, slack = 24, 600                                  # cluster gaps ~4e-8: the tie analysis needs a long tail
+    o_d, o_r = exact_topk(C, Q, k + slack)
+    idx = engine.DenseIndex(768, capacity=C.shape[0])
+    try:
+        idx.upsert(C, np.arange(C.shape[0], dtype=np.int64))
+        for kind in (Q8, COARSE):
+            idx.set_path(kind)
+            d, r = idx.search(Q, k)
+            fb = idx.last_fallbacks()
+            check_dense(d, r, o_d, o_r, k)
+            if kind == Q8:
+                assert 1 <= fb <= n_near, fb             # only the cluster queries re-run exactly
+    finally:
+        idx.set_path(0)
+        idx.close()
