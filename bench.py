@@ -92,6 +92,8 @@ def parse_args():
     ap.add_argument("--seq-len", type=int, default=256, help="ingest mode: tokens per chunk")
     ap.add_argument("--e2e-words", type=int, default=40, help="e2e mode: words per synthetic chunk")
     ap.add_argument("--e2e-latency-queries", type=int, default=32, help="e2e mode: single-query retrieve() calls timed")
+    ap.add_argument("--e2e-ab-same-stream", type=int, default=0,
+                    help="e2e mode: also time retrieve() with BM25 on the main stream (the pre-side-stream schedule)")
     ap.add_argument("--cpu-baseline", type=int, default=1)
     ap.add_argument("--cpu-queries", type=int, default=128)
     ap.add_argument("--seed", type=int, default=1)
@@ -938,42 +940,54 @@ def run_e2e(args, rank, ws, dev):
     none_keys = {"course": None, "unit": None, "author": None, "semester": None, "source_path": None,
                  "created_at": None}
     shapes = {"unfiltered": None, "to_dict_default": none_keys, "to_dict_course": dict(none_keys, course="C3")}
-    lat_all, paths = {}, {}
-    for name, f in shapes.items():
-        calls = []
-        real = device_batch.retrieve_batch
 
-        def spy(*a, **kw):
-            out = real(*a, **kw)
-            calls.append(out is not None)
-            return out
-        device_batch.retrieve_batch = spy
+    def latencies():
+        lat_all, paths = {}, {}
+        for name, f in shapes.items():
+            calls = []
+            real = device_batch.retrieve_batch
+
+            def spy(*a, **kw):
+                out = real(*a, **kw)
+                calls.append(out is not None)
+                return out
+            device_batch.retrieve_batch = spy
+            try:
+                for i in range(3):                             # batch-1 shapes: first-call setup
+                    retr.retrieve(question=qs[-1 - i], filters=f, top_k=K)
+                lat = []
+                lprof = None
+                if os.environ.get("CM_E2E_PROFILE_LAT"):       # host-side profile of the single-query calls
+                    import cProfile
+                    lprof = cProfile.Profile()
+                    lprof.enable()
+                for i in range(args.e2e_latency_queries):
+                    t1 = time.perf_counter()
+                    retr.retrieve(question=qs[i], filters=f, top_k=K)
+                    lat.append((time.perf_counter() - t1) * 1e3)
+                if lprof is not None:
+                    import pstats
+                    lprof.disable()
+                    print(f"---- host profile, retrieve() {name}", file=sys.stderr)
+                    pstats.Stats(lprof, stream=sys.stderr).sort_stats("tottime").print_stats(25)
+            finally:
+                device_batch.retrieve_batch = real
+            lat.sort()
+            lat_all[name] = {"p50": lat[len(lat) // 2], "p99": lat[min(len(lat) - 1, int(len(lat) * 0.99))],
+                             "n": len(lat), "filters": f}
+            paths[name] = "device chain" if calls and all(calls) else "host (per-stage dicts)"
+            log(f"retrieve() {name}: p50 {lat_all[name]['p50']:.2f} ms, p99 {lat_all[name]['p99']:.2f} ms ({paths[name]})")
+        return lat_all, paths
+
+    lat, paths = latencies()
+    lat_same = None
+    if args.e2e_ab_same_stream:       # A/B: BM25 on the main stream behind the dense search (the old schedule)
+        os.environ["CLASSMATE_BM25_SAME_STREAM"] = "1"
         try:
-            for i in range(3):                             # batch-1 shapes: first-call setup
-                retr.retrieve(question=qs[-1 - i], filters=f, top_k=K)
-            lat = []
-            lprof = None
-            if os.environ.get("CM_E2E_PROFILE_LAT"):       # host-side profile of the single-query calls
-                import cProfile
-                lprof = cProfile.Profile()
-                lprof.enable()
-            for i in range(args.e2e_latency_queries):
-                t1 = time.perf_counter()
-                retr.retrieve(question=qs[i], filters=f, top_k=K)
-                lat.append((time.perf_counter() - t1) * 1e3)
-            if lprof is not None:
-                import pstats
-                lprof.disable()
-                print(f"---- host profile, retrieve() {name}", file=sys.stderr)
-                pstats.Stats(lprof, stream=sys.stderr).sort_stats("tottime").print_stats(25)
+            log("A/B: BM25 on the main stream")
+            lat_same, _ = latencies()
         finally:
-            device_batch.retrieve_batch = real
-        lat.sort()
-        lat_all[name] = {"p50": lat[len(lat) // 2], "p99": lat[min(len(lat) - 1, int(len(lat) * 0.99))],
-                         "n": len(lat), "filters": f}
-        paths[name] = "device chain" if calls and all(calls) else "host (per-stage dicts)"
-        log(f"retrieve() {name}: p50 {lat_all[name]['p50']:.2f} ms, p99 {lat_all[name]['p99']:.2f} ms ({paths[name]})")
-    lat = lat_all
+            del os.environ["CLASSMATE_BM25_SAME_STREAM"]
     qps = B * args.steps / elapsed
     log(f"{args.steps} retrieve_batch calls in {elapsed:.3f}s -> {qps:.1f} q/s")
     out = {
@@ -986,6 +1000,7 @@ def run_e2e(args, rank, ws, dev):
                    "chunks": N, "words_per_chunk": args.e2e_words, "global_batch": B, "top_k": K, "dim": D},
         "retrieve_latency_ms": lat["unfiltered"],
         "retrieve_latency_ms_by_filter": lat,
+        "retrieve_latency_ms_bm25_same_stream": lat_same,
         "retrieve_paths": paths,
         "results_returned": n_res, "setup_s": time.perf_counter() - t_setup,
         "retrieve_batch_path": ("device-resident (retrieval/device_batch.py)"

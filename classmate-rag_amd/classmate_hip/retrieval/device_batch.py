@@ -24,6 +24,8 @@ from __future__ import annotations
 
 from typing import Any, Dict, List, Optional, Sequence
 
+import os
+
 import numpy as np
 
 from .. import _lib as L
@@ -178,6 +180,17 @@ def retrieve_batch(retr, questions: Sequence[str], top_k: int,
         km = (key, _KeyMap(vs, bm, index.device))
         retr._device_keymap = km
     km = km[1]
+    # BM25 runs on a side stream that waits only for the allow bitmaps / key map above, so it
+    # overlaps the encode and the dense search (a filtered search's status read then waits for the
+    # BM25 kernels alone, not for the dense scan queued ahead of it)
+    main = torch.cuda.current_stream(dev)
+    side = retr.__dict__.get("_device_bm25_stream")
+    if os.environ.get("CLASSMATE_BM25_SAME_STREAM") == "1":     # A/B: the serial schedule
+        side = main
+    elif side is None or side.device != dev:
+        side = retr._device_bm25_stream = torch.cuda.Stream(device=dev)
+    ready = torch.cuda.Event()
+    ready.record(main)
     # E5 encode first (its launches return at once), so the host tokenizes the BM25 queries while
     # the device encodes; then dense pool + MMR
     q = _query_vectors(retr.embedder, questions, dev)
@@ -189,22 +202,26 @@ def retrieve_batch(retr, questions: Sequence[str], top_k: int,
     off = np.zeros(nq + 1, np.int32)
     off[1:] = np.cumsum([len(x) for x in qids])
     flat = np.asarray([t for x in qids for t in x] or [0], np.int32)
-    # pinned, stream-ordered copies: a pageable copy would wait here for the encode and search
-    q_terms = torch.from_numpy(flat).pin_memory().to(dev, non_blocking=True)
-    q_off = torch.from_numpy(off).pin_memory().to(dev, non_blocking=True)
-    # BM25 top-k (whitespace-only queries: no BM25 list, bm25.py:178); with a filter, rank_bm25's
-    # statistics over the allowed candidates (K2f; no candidate: empty lists, bm25.py:187)
-    if allow_b is None:
-        bs, br = bm._index.search_dev(q_terms, q_off, kb)
-    elif kb > 0:
-        bs, br = _bm25_filtered(bm, q_terms, q_off, kb, allow_b, filters, cache)
-    else:
-        bs = torch.zeros((nq, 1), dtype=torch.float64, device=dev)
-        br = torch.full((nq, 1), -1, dtype=torch.int64, device=dev)
-    bkeys = torch.where(br >= 0, km.bm2key_dev[br.clamp(min=0)], torch.full_like(br, -1))
-    if blank.any():
-        blank_dev = torch.from_numpy(blank).pin_memory().to(dev, non_blocking=True)
-        bkeys = torch.where(blank_dev[:, None], torch.full_like(bkeys, -1), bkeys)   # no boolean-index sync
+    with torch.cuda.stream(side):
+        side.wait_event(ready)
+        # pinned, stream-ordered copies: a pageable copy would wait here for the encode and search
+        q_terms = torch.from_numpy(flat).pin_memory().to(dev, non_blocking=True)
+        q_off = torch.from_numpy(off).pin_memory().to(dev, non_blocking=True)
+        # BM25 top-k (whitespace-only queries: no BM25 list, bm25.py:178); with a filter, rank_bm25's
+        # statistics over the allowed candidates (K2f; no candidate: empty lists, bm25.py:187)
+        if allow_b is None:
+            bs, br = bm._index.search_dev(q_terms, q_off, kb)
+        elif kb > 0:
+            bs, br = _bm25_filtered(bm, q_terms, q_off, kb, allow_b, filters, cache)
+        else:
+            bs = torch.zeros((nq, 1), dtype=torch.float64, device=dev)
+            br = torch.full((nq, 1), -1, dtype=torch.int64, device=dev)
+        bkeys = torch.where(br >= 0, km.bm2key_dev[br.clamp(min=0)], torch.full_like(br, -1))
+        if blank.any():
+            blank_dev = torch.from_numpy(blank).pin_memory().to(dev, non_blocking=True)
+            bkeys = torch.where(blank_dev[:, None], torch.full_like(bkeys, -1), bkeys)   # no boolean-index sync
+    main.wait_stream(side)
+    # (side-stream tensors read on main: the .cpu() copies below synchronise main before they are freed)
     vk, vd, vn, bn = engine.rrf_pool_prep_dev(r.contiguous(), d.contiguous(), order, bkeys.contiguous())
     k_dev = top_k if top_k > 0 else kv + kb
     ok, of, ov, ob, ofl, on = engine.rrf_merge_dev(vk, vd, vn, bkeys.contiguous(), bs.contiguous(), bn,
