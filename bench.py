@@ -595,7 +595,8 @@ def _e5_roofline(bq, S, layers, ms, dtype):
 
 def dense_legs(args, dense, N, D, dev, ws, q_step=None, pool=None):
     """north_star's dense configurations, timed in the same run (side fields, not the headline):
-    C2' = this rank's 10M shard at B = 16, k = 10 (the HBM-bound case the >= 80 % target names);
+    C2' = this rank's 10M shard at B = 16, k = 10 (the HBM-bound case the >= 80 % target names; K1q
+    since late round 4 -- the f16 K1s stream it replaced reached 0.84 of HBM on twice the bytes);
     C2 = a 1M-chunk shard (its own index), B = 256, k = 10 (queries: unit Gaussian); and the
     headline's dense search alone -- the step's own query embeddings and pool size on this shard,
     without the BM25 stream beside it."""

@@ -1654,13 +1654,15 @@ int dense_debug_flags() { return 0; }
 #endif
 
 // Scan kernel for (nq, k), the "search kind":
-//   CM_DENSE_STREAM (K1s)  nq <= kSQ queries: per-wave HBM streams of the f16 plane + re-rank;
+//   CM_DENSE_Q8    (K1q)   dim-768 batches (any nq from kQSmallMinRows rows): int8 plane + re-rank;
+//   CM_DENSE_STREAM (K1s)  nq <= kSQ queries on smaller stores: per-wave HBM streams of the f16 plane;
 //   CM_DENSE_COARSE (K1c)  larger batches: 256-query resident passes + re-rank;
 //   CM_DENSE_F32   (K1)    exact fp32 scan: k > 32, dims other than 384 / 768, corpora under
 //                          16384 rows (and the certificate's fallback).
 // CM_DENSE_PATH=f32|coarse|stream (or cm_dense_set_path) forces a kind for A/B probes; an
 // ineligible forced kind falls back to the automatic rule.  The retired K1b (f16x3 split planes,
 // kind 2) maps to the automatic rule.
+constexpr int64_t kQSmallMinRows = 4 << 20;   // K1q for nq <= kSQ from this many rows
 int dense_kind(const cm_dense *h, int nq, int k) {
   static const int env_force = [] {
     const char *e = getenv("CM_DENSE_PATH");
@@ -1681,7 +1683,10 @@ int dense_kind(const cm_dense *h, int nq, int k) {
   if (force == CM_DENSE_COARSE) return CM_DENSE_COARSE;
   if (force == CM_DENSE_STREAM && nq <= kSQ) return CM_DENSE_STREAM;
   if (force == CM_DENSE_Q8 && q8_ok) return CM_DENSE_Q8;
-  if (nq <= kSQ) return CM_DENSE_STREAM;
+  // small batches: K1q too on large stores -- half the bytes of K1s's f16 stream outweigh its fixed
+  // 256-slot MFMA work and seed pass (10M x 768: B = 1 2.0 vs 2.47 ms, B = 16 2.06 vs 2.50 ms,
+  // profiles/r04c_small_batch_q8_ab.txt); K1s below kQSmallMinRows
+  if (nq <= kSQ) return (q8_ok && q8_auto && h->size >= kQSmallMinRows) ? CM_DENSE_Q8 : CM_DENSE_STREAM;
   return (q8_ok && q8_auto) ? CM_DENSE_Q8 : CM_DENSE_COARSE;
 }
 

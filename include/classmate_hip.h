@@ -109,8 +109,8 @@ int64_t cm_dense_search_workspace(cm_dense *h, int32_t nq, int32_t k);
  * certified exact re-rank), CM_DENSE_STREAM (K1s, f16 plane, 2 B/element,
  * nq <= 32, per-wave HBM streams, same re-rank), CM_DENSE_Q8 (K1q, int8 plane
  * with per-row scales, 1 B/element, 256-query resident passes, per-row
- * certified exact re-rank; the automatic choice for nq > 32 at dim 768 unless
- * $CM_DENSE_Q8=0, which keeps K1c); -1 on error.  Lets callers price the launch against the
+ * certified exact re-rank; the automatic choice at dim 768 for nq > 32, and for
+ * nq <= 32 from 4M rows, unless $CM_DENSE_Q8=0, which keeps K1c / K1s); -1 on error.  Lets callers price the launch against the
  * right roofline.  CM_DENSE_F16X3 (the retired split-plane K1b) is accepted by
  * cm_dense_set_path and means automatic.  */
 #define CM_DENSE_F32 1

@@ -25,7 +25,7 @@ def store():
 
 def test_q8_kind_selection(store):
     """K1q is the automatic batched kind (CM_DENSE_Q8=0 selects K1c); a forced set_path(Q8) always
-    takes it; K1s keeps the small batches."""
+    takes it; K1s keeps the small batches below 4M rows (this store: 1M)."""
     import os
     _, idx = store
     auto = COARSE if os.environ.get("CM_DENSE_Q8", "") == "0" else Q8

@@ -154,8 +154,8 @@ def _device_step(engine, dense, bm, q_dev, qt, K, P):
 
 
 def test_hybrid_10m_sample():
-    """The headline shape (10M-chunk shard, B = 256: K1c and K2a/K2b with 64 query groups and a
-    contended running threshold) and the single-stream shape (B = 16: K1s), checked on the first
+    """The headline shape (10M-chunk shard, B = 256: K1q and K2a/K2b with 64 query groups and a
+    contended running threshold) and the small-batch shape (B = 16: K1q, and K1s forced), checked on the first
     64 queries against the exact fp64 dense scan, the C BM25 oracle (bit for bit) and the CPU
     restatement of the fusion (VERDICT r2 "next" 3)."""
     import torch
@@ -185,6 +185,15 @@ def test_hybrid_10m_sample():
     for nb, (d, r, _, _, _) in runs.items():
         m = min(nb, NCHK)
         check_dense(d[:m], r[:m], o_d[:m], o_r[:m], P)
+    # B = 16 takes K1q at this size; K1s (the small-batch kind below 4M rows) forced on the same shard
+    assert dense.search_kind(16, P) == 5
+    dense.set_path(4)
+    try:
+        assert dense.search_kind(16, P) == 4
+        d_s, r_s = _device_step(engine, dense, bm, q_dev[:16].contiguous(), qt[:16].contiguous(), K, P)[:2]
+    finally:
+        dense.set_path(0)
+    check_dense(d_s, r_s, o_d[:16], o_r[:16], P)
     # BM25 bit-exact vs the C oracle
     csr = bm.export()
     term_off = csr["term_off"]
