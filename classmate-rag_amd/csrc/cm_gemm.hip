@@ -410,6 +410,10 @@ static TileCfg pick_tile(int64_t M, int N, int n_cu) {
   // FFN-up (N = 3072): 192 x 192 measured 98.3 -> 90.5 us at M = 6144 (tools/k10_tiles.sh); the
   // other E5 shapes are faster at 96 x 192 (qkv 67 vs 75 us, o 25 vs 34, down 73 vs 95)
   if (N >= 3072 && N % 192 == 0 && ceil_div(M, 192) * (N / 192) >= n_cu) return TileCfg{12, 12};
+  // single short queries (M <= 32 rows, e.g. one retrieve() call): the GEMM is a weight stream spread
+  // over N / (tile width) workgroups, so a 64 x 32 tile puts twice the CUs of 64 x 64 on it (the
+  // per-element k order, hence every output bit, does not depend on the tile)
+  if (M <= 32 && N % 32 == 0) return TileCfg{4, 2};
   const TileCfg cands[4] = {{6, 12}, {8, 8}, {4, 8}, {4, 4}};
   TileCfg best = {0, 0};
   double best_cost = 0;
@@ -515,5 +519,7 @@ extern "C" int cm_linear_f16x3(const void *a_planes, int64_t M, int32_t K, const
     return launch_tile<8, 8, 4, 8>(A, M, K, W, bias_dev, out_scale, N, epilogue, c_dev, next_scale, Cp, g_n_cu, st);
   if (t.bnb == 8)
     return launch_tile<4, 8, 4, 8>(A, M, K, W, bias_dev, out_scale, N, epilogue, c_dev, next_scale, Cp, g_n_cu, st);
+  if (t.bmb == 4 && t.bnb == 2)
+    return launch_tile<4, 2, 4, 4>(A, M, K, W, bias_dev, out_scale, N, epilogue, c_dev, next_scale, Cp, g_n_cu, st);
   return launch_tile<4, 4, 4, 8>(A, M, K, W, bias_dev, out_scale, N, epilogue, c_dev, next_scale, Cp, g_n_cu, st);
 }

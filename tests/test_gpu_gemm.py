@@ -24,7 +24,8 @@ def _case(M, K, N, seed, xs=1.0, ws=0.02):
 
 @pytest.mark.parametrize("M,K,N", [(6144, 768, 2304), (6144, 768, 768), (1000, 768, 3072), (37, 3072, 768),
                                    (1, 768, 64), (129, 64, 192), (20000, 768, 3072), (8192, 3072, 768),
-                                   (9216, 768, 3072), (12288, 3072, 768)])
+                                   (9216, 768, 3072), (12288, 3072, 768), (8, 768, 2304), (24, 3072, 768),
+                                   (32, 768, 3072)])
 def test_linear_f16x3_fp32_accuracy(M, K, N):
     import torch
     from classmate_hip import engine
@@ -56,6 +57,22 @@ def test_linear_f16x3_gelu_epilogue_and_scales():
         f32 = torch.nn.functional.gelu(torch.nn.functional.linear(x, w, b)).double()
         e_ours, e_f32 = (got.double() - ref).abs(), (f32 - ref).abs()
         assert float(e_ours.max()) <= 2 * float(e_f32.max()) + 1e-7, (xs, float(e_ours.max()), float(e_f32.max()))
+
+
+def test_linear_f16x3_tile_independent_bits():
+    """A single short query's rows (M <= 32: the 64 x 32 tile) are bit-identical to the same rows
+    inside a batch (M = 6144: the 96 x 192 / 192 x 192 tiles) -- the per-element k order does not
+    depend on the tile, so a query embeds the same alone or batched; with and without GELU."""
+    import torch
+    from classmate_hip import engine
+    for K, N in ((768, 2304), (768, 768), (3072, 768), (768, 3072)):
+        x, w, b = _case(6144, K, N, seed=K + 3 * N)
+        W = engine.F16x3Weight(w, b)
+        for gelu in (False, True):
+            big = engine.linear_f16x3(x, W, gelu=gelu)
+            for m in (1, 13, 32):
+                small = engine.linear_f16x3(x[:m].contiguous(), W, gelu=gelu)
+                assert torch.equal(small, big[:m]), (K, N, gelu, m)
 
 
 def test_linear_f16x3_rejects_bad_shapes():
