@@ -62,6 +62,9 @@ typedef float g32x4 __attribute__((ext_vector_type(4)));
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ h16x8 as_h8(i32x4 v) { return __builtin_bit_cast(h16x8, v); }
 
+#ifndef K10_SMALL_S
+#define K10_SMALL_S 6          // ring stages of the 64 x 32 tile (M <= 32): 6 vs 4 = 1.03 vs 1.08 ms batch-1 encode
+#endif
 #ifndef K10_W6
 #define K10_W6 12              // waves per workgroup at the 96 x 192 tile (2 x 6: three per SIMD)
 #endif
@@ -520,6 +523,6 @@ extern "C" int cm_linear_f16x3(const void *a_planes, int64_t M, int32_t K, const
   if (t.bnb == 8)
     return launch_tile<4, 8, 4, 8>(A, M, K, W, bias_dev, out_scale, N, epilogue, c_dev, next_scale, Cp, g_n_cu, st);
   if (t.bmb == 4 && t.bnb == 2)
-    return launch_tile<4, 2, 4, 4>(A, M, K, W, bias_dev, out_scale, N, epilogue, c_dev, next_scale, Cp, g_n_cu, st);
+    return launch_tile<4, 2, K10_SMALL_S, 4>(A, M, K, W, bias_dev, out_scale, N, epilogue, c_dev, next_scale, Cp, g_n_cu, st);
   return launch_tile<4, 4, 4, 8>(A, M, K, W, bias_dev, out_scale, N, epilogue, c_dev, next_scale, Cp, g_n_cu, st);
 }
