@@ -45,6 +45,8 @@ DENSE_KINDS = {1: "K1 fp32 MFMA (dense_topk_kernel)",
                3: "K1c dense_coarse_scan_kernel (f16 plane, MFMA, 256-query resident passes) + certified fp64 re-rank",
                4: "K1s dense_stream_scan_kernel (f16 plane, MFMA, per-wave HBM streams) + certified fp64 re-rank",
                5: "K1q dense_q8_scan_kernel (int8 plane + per-row bounds, i8 MFMA, 256-query resident passes) + "
+                  "per-row certified fp64 re-rank",
+               6: "K1q-s dense_q8_stream_kernel (int8 plane + per-row bounds, i8 MFMA, per-wave HBM streams) + "
                   "per-row certified fp64 re-rank"}
 
 
@@ -346,16 +348,23 @@ def main():
             bs, br = run_bm25(e)
         if record:
             e["d0"].record()
-        d, r = dense.search_dev(q, P, out=dout, workspace=dws)
+        # the certificate's exact pass (queries whose band overflowed; device-gated, normally none)
+        # is deferred behind the BM25 join: its ~150 KiB-LDS grid would wait for the BM25 kernels'
+        # CUs anyway and hold the stream's later work
+        defer = bm25 is not None and side is not main
+        d, r = dense.search_dev(q, P, out=dout, workspace=dws, defer_exact=defer)
         if record:
             e["d1"].record()
         if args.mode == "dense":
             if record:
                 ev.append(e)
             return r
+        if defer:
+            main.wait_stream(side)
+            dense.exact_fallback_dev(q, P, dout, workspace=dws)
         if ws == 1:
             vecs = dense.gather_dev(r.reshape(-1), out=vbuf).view(B, P, D)
-            order = engine.mmr_dev(q, vecs, K, 0.5, out=obuf)     # overlaps the BM25 tail
+            order = engine.mmr_dev(q, vecs, K, 0.5, out=obuf)
             main.wait_stream(side)
             rg, dm, brg, bsm = r, d, br, bs
         else:
@@ -431,7 +440,8 @@ def main():
         + (f", bm25 search {bsearch_ms:.3f} ms (K2a tail pass {bm25_ms:.3f} ms, {rescored} (query, range) pairs "
            f"re-scored)" if bm25_ms is not None else ""))
 
-    roofs = {"dense": _dense_roofline(kind, N, D, B, dense_ms, _pmc_traffic(args, "dense" if kind != 5 else "dense_q8"))}
+    roofs = {"dense": _dense_roofline(kind, N, D, B, dense_ms,
+                                      _pmc_traffic(args, {5: "dense_q8", 6: "dense_q8s"}.get(kind, "dense")))}
     if bm25 is not None:
         roofs["bm25"] = _bm25_roofline(bm25, q_terms, N, bm25_ms, _pmc_traffic(args, "bm25"), args.q_terms)
     dominant = max(roofs, key=lambda n: roofs[n]["avg_launch_ms"])
@@ -470,11 +480,13 @@ def main():
         "value": qps, "unit": "queries/s", "n_gpus": ws, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None,
-        "dtype": (("fp32-accurate E5 (K10 f16x3 MFMA) + " + ("int8/f16/f64" if kind == 5 else "f16/f64")
+        "dtype": (("fp32-accurate E5 (K10 f16x3 MFMA) + " + ("int8/f16/f64" if kind in (5, 6) else "f16/f64")
                    + " dense + f64 BM25") if use_e5 and args.e5_dtype == "float32" else "f16+f64"),
         "dtypes": {"dense_knn": {1: "f32 (MFMA)", 3: "f16 coarse (MFMA) + fp64 exact re-rank of the certified band",
                                  4: "f16 coarse (MFMA) + fp64 exact re-rank of the certified band",
                                  5: "int8 coarse (i8 MFMA, 16-row group scales) -> certified int8 band -> "
+                                    "certified f16 band -> fp64 exact re-rank",
+                                 6: "int8 coarse (i8 MFMA, 16-row group scales) -> certified int8 band -> "
                                     "certified f16 band -> fp64 exact re-rank"}[kind],
                    "bm25": "f64", "fusion": "f64",
                    "e5_forward": ({"float32": "fp32 (K10: split-precision f16 hi/lo MFMA, fp32 accumulate)",
@@ -532,7 +544,7 @@ def _dense_roofline(kind, N, D, B, ms, traffic):
     storage format + live bitmap + query planes; flops as executed on the MFMA units."""
     if kind == 1:      # fp32 rows + invc
         bytes_, flops, peak = N * D * 4 + N * 4 + N / 8 + B * D * 4, 2.0 * N * D * B, PEAK_F32_MFMA_TFLOPS
-    elif kind == 5:    # K1q: the int8 plane once + per-row {scale, bound} + live bits + the int8 queries
+    elif kind in (5, 6):   # K1q / K1q-s: the int8 plane once + per-row {scale, bound} + live bits + int8 queries
         bytes_, flops, peak = N * D + N * 8 + N / 8 + B * D, 2.0 * N * D * B, PEAK_I8_MFMA_TOPS
     else:              # K1c / K1s: the f16 plane once + live bits + the f16 queries
         bytes_, flops, peak = N * D * 2 + N / 8 + B * D * 2, 2.0 * N * D * B, PEAK_F16_MFMA_TFLOPS
@@ -542,7 +554,7 @@ def _dense_roofline(kind, N, D, B, ms, traffic):
     # the other side of the same launch: at B = 256 the f16 scan's intensity (B flop/B = 256) sits
     # just under the nominal ridge (2.5 PF / 8 TB/s = 312), and under the chip's power limit the
     # MFMA clock drops, so the MFMA side is reported beside the HBM fraction
-    r["mfma_side"] = dict(achieved=flops / (ms * 1e-3) / 1e12, peak=peak, unit="TOP/s" if kind == 5 else "TFLOP/s",
+    r["mfma_side"] = dict(achieved=flops / (ms * 1e-3) / 1e12, peak=peak, unit="TOP/s" if kind in (5, 6) else "TFLOP/s",
                           frac=flops / (ms * 1e-3) / 1e12 / peak)
     return r
 
@@ -631,8 +643,8 @@ def dense_legs(args, dense, N, D, dev, ws, q_step=None, pool=None):
         index.timing(False)
         kind = index.search_kind(b, kk)
         r = _dense_roofline(kind, n, D, b, sum(kt) / len(kt),
-                            _pmc_traffic(args, "dense_q8" if kind == 5 else "dense") if n == args.docs_per_gpu
-                            and b == args.batch else None)
+                            _pmc_traffic(args, {5: "dense_q8", 6: "dense_q8s"}.get(kind, "dense"), b)
+                            if n == args.docs_per_gpu else None)
         legs[name] = {"value": b * steps * ws / el, "unit": "queries/s", "ms_per_step": el / steps * 1e3,
                       "config": {"chunks_per_gpu": n, "batch": b, "k": kk, "dim": D},
                       "roofline": r}
@@ -700,13 +712,13 @@ def ingest_leg(args, emb, dev, ws, rank):
     return leg, roof
 
 
-def _pmc_traffic(args, which):
+def _pmc_traffic(args, which, batch=None):
     """HBM bytes per launch (FETCH_SIZE x 2, the gfx950 correction) from a committed rocprofv3
     --pmc summary of this config (profiles/pmc_traffic.json), or None."""
     p = REPO / "profiles" / "pmc_traffic.json"
     try:
         d = json.loads(p.read_text())
-        return d.get(f"{which}_{args.docs_per_gpu}x{args.dim}_B{args.batch}")
+        return d.get(f"{which}_{args.docs_per_gpu}x{args.dim}_B{batch or args.batch}")
     except Exception:
         return None
 

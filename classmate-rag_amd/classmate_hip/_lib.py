@@ -77,6 +77,8 @@ SIGNATURES = {
     "cm_bm25_timing": (c_int, c_vp, c_i32),
     "cm_bm25_timing_drain": (c_i32, c_vp, c_vp, c_i32),
     "cm_dense_search_dev": (c_int, c_vp, c_vp, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp),
+    "cm_dense_search_dev_deferred": (c_int, c_vp, c_vp, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp),
+    "cm_dense_exact_fallback_dev": (c_int, c_vp, c_vp, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp),
     "cm_dense_export": (c_int, c_vp, c_i64, c_i64, c_vp, c_vp),
     "cm_dense_gather_dev": (c_int, c_vp, c_vp, c_i64, c_vp, c_vp),
     "cm_dense_live_bits_dev": (c_vp, c_vp),

@@ -26,6 +26,7 @@ import contextlib
 import hashlib
 import math
 import os
+import threading
 import re
 import warnings
 from typing import Iterable, List, Optional
@@ -133,6 +134,16 @@ def _f16x3_layers(layers, emb_ln, D: int):
     return out
 
 
+# Loaded embedders by (model_name, device, dtype, normalize): the reference constructs
+# E5MultilingualEmbedder on every ask / ingest call (rag/pipeline/rag.py:334,533), and loading the
+# weights, splitting them into K10's planes and capturing the query graphs is seconds of work; a
+# construction with a key already loaded in this process attaches to that instance's state instead
+# (VERDICT r4 #3).  ``share_as`` registers an instance under another name (offline benchmarks
+# register the random-init model under the production model name).
+_LOADED: dict = {}
+_LOADED_LOCK = threading.Lock()
+
+
 class E5MultilingualEmbedder:
     def __init__(self, model_name: str = "intfloat/multilingual-e5-base", device: Optional[str] = None,
                  normalize: bool = True, dtype: Optional[str] = None, _model=None, _tokenizer=None):
@@ -145,12 +156,41 @@ class E5MultilingualEmbedder:
             # build's pooling epilogue is a HIP kernel and there is no CPU fallback
             raise RuntimeError("E5MultilingualEmbedder needs a ROCm GPU (the pooling epilogue is a HIP kernel); "
                                f"device={device!r} is not supported")
+        if self.device.index is None:
+            self.device = torch.device("cuda", torch.cuda.current_device())
         self.dtype = getattr(torch, _resolve_dtype(dtype))
         if _model is None:
+            key = self._key(model_name)
+            with _LOADED_LOCK:
+                prim = _LOADED.get(key)
+            if prim is not None:
+                self.__dict__ = prim.__dict__   # the loaded model, K10 planes, graphs and caches
+                return
             _model, _tokenizer = self._load(model_name)
+            self.model = _model.to(self.device, self.dtype).eval()
+            self.tokenizer = _tokenizer
+            self._graphs = {}
+            with _LOADED_LOCK:
+                _LOADED.setdefault(key, self)
+            return
         self.model = _model.to(self.device, self.dtype).eval()
         self.tokenizer = _tokenizer
         self._graphs = {}
+
+    def _key(self, model_name: str):
+        return (str(model_name), str(self.device), str(self.dtype), self.normalize)
+
+    def share_as(self, model_name: str) -> "E5MultilingualEmbedder":
+        """Later ``E5MultilingualEmbedder(model_name, device, dtype=..., normalize=...)`` calls with
+        this instance's device / dtype / normalize attach to it instead of loading ``model_name``."""
+        with _LOADED_LOCK:
+            _LOADED[self._key(model_name)] = self
+        return self
+
+    @staticmethod
+    def release_all() -> None:
+        with _LOADED_LOCK:
+            _LOADED.clear()
 
     # ------------------------------------------------------------------
     @staticmethod
@@ -265,12 +305,24 @@ class E5MultilingualEmbedder:
                 return None
             ent = cache[key] = (g_ids, g_mask, g_out, graph, pad)
         g_ids, g_mask, g_out, graph, pad = ent
-        g_ids.fill_(pad)
-        g_mask.zero_()
-        g_ids[:, :S].copy_(ids)
-        g_mask[:, :S].copy_(mask)
-        graph.replay()
-        return g_out.clone()
+        # the graph's buffers are shared: one host thread at a time from the input fill to the output
+        # copy, and each use ordered after the previous one on the device (callers on other streams)
+        # 
+        with self.__dict__.setdefault("_small_graph_lock", threading.Lock()):
+            cur = torch.cuda.current_stream(ids.device)
+            last = self.__dict__.get("_small_graph_done")
+            if last is not None:
+                cur.wait_event(last)
+            g_ids.fill_(pad)
+            g_mask.zero_()
+            g_ids[:, :S].copy_(ids)
+            g_mask[:, :S].copy_(mask)
+            graph.replay()
+            res = g_out.clone()
+            done = torch.cuda.Event()
+            done.record(cur)
+            self._small_graph_done = done
+        return res
 
     def _encode_hf(self, input_ids, attention_mask, out=None):
         """The Hugging Face XLM-R module forward + K6 pooling."""

@@ -113,5 +113,55 @@ class CachingEmbedder:
     def encode_queries(self, queries: Iterable[str]) -> np.ndarray:
         return self._encode("query", queries)
 
+    def encode_queries_dev(self, queries: Iterable[str]):
+        """encode_queries with the result left on the device, for the device retrieval chain
+        (retrieval/device_batch.py): hits come from their .npy files, the misses go to the base
+        embedder's device path as ONE batch, as in ``_encode``.  The misses' files are written from a
+        non-blocking device-to-host copy by ``flush_pending`` -- the chain calls it once its results
+        are on the host, and the next call here flushes anything left -- so the query encode is not
+        serialised behind a host round trip.  None when the base embedder has no device path."""
+        import torch
+        base_dev = getattr(self.base, "encode_queries_dev", None)
+        if base_dev is None:
+            return None
+        self.flush_pending()
+        items = list(queries)
+        if not items:
+            raise ValueError("need at least one array to concatenate")   # np.vstack([]), as _encode
+        hits, misses, paths = self._lookup("query", items)
+        if not misses:
+            return torch.from_numpy(np.vstack(hits).astype(np.float32, copy=False)).to(self.base.device)
+        fresh = base_dev([items[i] for i in misses])
+        host = torch.empty(fresh.shape, dtype=torch.float32, pin_memory=True)
+        host.copy_(fresh, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(fresh.device))
+        self._pending.append((host, ev, paths))
+        if len(misses) == len(items):
+            return fresh
+        out = torch.empty((len(items), fresh.shape[1]), dtype=torch.float32, device=fresh.device)
+        out[torch.as_tensor(misses, device=fresh.device)] = fresh
+        hit_idx = [i for i, h in enumerate(hits) if h is not None]
+        out[torch.as_tensor(hit_idx, device=fresh.device)] = torch.from_numpy(
+            np.vstack([hits[i] for i in hit_idx]).astype(np.float32, copy=False)).to(fresh.device)
+        return out
+
+    @property
+    def _pending(self) -> list:
+        return self.__dict__.setdefault("_pending_writes", [])
+
+    def flush_pending(self) -> None:
+        """Write the .npy files of encode_queries_dev's misses (errors swallowed, as ``_encode``)."""
+        pend, self.__dict__["_pending_writes"] = self._pending, []
+        for host, ev, paths in pend:
+            ev.synchronize()
+            arr = host.numpy()
+            for j, fp in enumerate(paths):
+                try:
+                    fp.parent.mkdir(parents=True, exist_ok=True)
+                    np.save(fp, arr[j])
+                except Exception:
+                    pass
+
     def encode_passages(self, texts: Iterable[str]) -> np.ndarray:
         return self._encode("passage", texts)

@@ -175,11 +175,12 @@ class DenseIndex:
         return out, mask
 
     # scan kernels (cm_dense_search_kind / cm_dense_set_path)
-    PATH_AUTO, PATH_F32, PATH_COARSE, PATH_STREAM = 0, 1, 3, 4
+    PATH_AUTO, PATH_F32, PATH_COARSE, PATH_STREAM, PATH_Q8, PATH_Q8S = 0, 1, 3, 4, 5, 6
 
     def set_path(self, kind: int):
-        """Force the scan kernel (0 auto, 1 fp32 K1, 3 K1c coarse + re-rank, 4 K1s <= 32-query streams
-        + re-rank; 2 = the retired K1b, automatic)."""
+        """Force the scan kernel (0 auto, 1 fp32 K1, 3 K1c coarse + re-rank, 4 K1s <= 32-query f16
+        streams, 5 K1q int8 resident passes, 6 K1q-s <= 32-query int8 streams -- the coarse kinds with
+        the certified re-rank; 2 = the retired K1b, automatic)."""
         L.check(L.fn["cm_dense_set_path"](self._h, int(kind)), "cm_dense_set_path")
 
     def search_kind(self, nq: int, k: int) -> int:
@@ -211,8 +212,11 @@ class DenseIndex:
             raise ValueError("bad (nq, k) for dense search")
         return n
 
-    def search_dev(self, q, k: int, allow=None, out=None, workspace=None):
-        """q: (nq, dim) float32 device tensor. Returns (dist f32 (nq,k), rows i64 (nq,k)) device tensors."""
+    def search_dev(self, q, k: int, allow=None, out=None, workspace=None, defer_exact: bool = False):
+        """q: (nq, dim) float32 device tensor. Returns (dist f32 (nq,k), rows i64 (nq,k)) device tensors.
+        defer_exact: leave the certificate's exact pass (queries whose certified band overflowed) to a
+        later ``exact_fallback_dev`` call with the same arguments on the same stream -- enqueued after
+        other streams' work has joined, so its large-LDS grid does not wait behind their kernels."""
         nq = q.shape[0]
         dev = q.device
         wsb = self.workspace_bytes(nq, k)
@@ -223,9 +227,20 @@ class DenseIndex:
         if out is None:
             out = (torch.empty((nq, k), dtype=torch.float32, device=dev),
                    torch.empty((nq, k), dtype=torch.int64, device=dev))
-        L.check(L.fn["cm_dense_search_dev"](self._h, L.ptr(q), nq, int(k), L.ptr(allow), L.ptr(out[0]),
-                                            L.ptr(out[1]), L.ptr(workspace), int(workspace.numel()),
-                                            _stream(self.device)), "cm_dense_search_dev")
+        name = "cm_dense_search_dev_deferred" if defer_exact else "cm_dense_search_dev"
+        L.check(L.fn[name](self._h, L.ptr(q), nq, int(k), L.ptr(allow), L.ptr(out[0]), L.ptr(out[1]),
+                           L.ptr(workspace), int(workspace.numel()), _stream(self.device)), name)
+        return out
+
+    def exact_fallback_dev(self, q, k: int, out, workspace=None, allow=None):
+        """Second part of ``search_dev(..., defer_exact=True)``: the exact fp32 pass for the queries
+        whose certificate failed, merged into ``out`` (device-gated: nothing runs when none failed)."""
+        if workspace is None:
+            workspace = self._ws
+        L.check(L.fn["cm_dense_exact_fallback_dev"](self._h, L.ptr(q), q.shape[0], int(k), L.ptr(allow),
+                                                    L.ptr(out[0]), L.ptr(out[1]), L.ptr(workspace),
+                                                    int(workspace.numel()), _stream(self.device)),
+                "cm_dense_exact_fallback_dev")
         return out
 
     def gather_dev(self, rows, out=None):

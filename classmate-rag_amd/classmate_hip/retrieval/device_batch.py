@@ -22,7 +22,7 @@ scores, in the same order.
 """
 from __future__ import annotations
 
-from typing import Any, Dict, List, Optional, Sequence
+from typing import Any, Dict, List, Mapping, Optional, Sequence
 
 import os
 
@@ -82,20 +82,41 @@ def _query_vectors(embedder, questions: Sequence[str], dev):
     enc = getattr(embedder, "encode_queries_dev", None)
     if enc is not None:
         q = enc(questions)
-        if q.device == dev and q.dtype == torch.float32:
+        if q is not None and q.device == dev and q.dtype == torch.float32:
             return q.contiguous()
     q = np.ascontiguousarray(np.asarray(embedder.encode_queries(list(questions)), np.float32))
     return torch.from_numpy(q).to(dev)
 
 
 _ALLOW_CACHE_MAX = 64
+# Process-level device caches, keyed by the stores' never-reused uids and version counters rather
+# than held by one HybridRetriever: the reference builds a new retriever (and new stores) for every
+# ask_question call (rag/pipeline/rag.py:531-545), so caches on the retriever object would be rebuilt
+# per question -- the key map alone is O(corpus).
+_ALLOW_CACHE: dict = {}
+_KEYMAPS: dict = {}
+_KEYMAPS_MAX = 4
+_SIDE_STREAMS: dict = {}
+
+
+def _canon(v):
+    """Hashable, type-exact form of a where clause (True, 1 and "1" stay distinct; None when a
+    value has no stable form)."""
+    if isinstance(v, Mapping):
+        return ("d", tuple(sorted(((str(type(k).__name__), k), _canon(x)) for k, x in v.items())))
+    if isinstance(v, (list, tuple)):
+        return (type(v).__name__, tuple(_canon(x) for x in v))
+    if v is None or isinstance(v, (bool, int, float, str)):
+        return (type(v).__name__, v)
+    raise TypeError(type(v).__name__)
 
 
 def _filter_key(meta, where, semantics: str):
-    """Cache key of a filter over one metadata version (None when ``where`` does not serialise)."""
-    import json
+    """Cache key of a filter over one metadata object and version: the object's uid (never reused,
+    unlike id()), its version and the typed canonical clause (None when ``where`` has no stable
+    form)."""
     try:
-        return (id(meta), meta.version, semantics, json.dumps(where, sort_keys=True, default=str))
+        return (meta.uid, meta.version, semantics, _canon(where))
     except (TypeError, ValueError):
         return None
 
@@ -107,7 +128,7 @@ def _allow(meta, where, semantics: str, device: int, n_words: int, cache: dict):
     import torch
     key = _filter_key(meta, where, semantics)
     hit = cache.get(key) if key is not None else None
-    if hit is not None:
+    if hit is not None and hit[0].numel() >= n_words:
         return hit
     from .. import engine as E
     words, n = E.where_bits(meta, where, semantics, device)
@@ -132,7 +153,7 @@ def _bm25_filtered(bm, q_terms, q_off, k: int, allow, where, cache: dict):
     index = bm._index
     index.prepare_filtered()                    # the device log table (once per index)
     fk = _filter_key(bm._meta, where, "bm25")
-    ekey = None if fk is None else ("eps", id(bm), bm._version) + fk
+    ekey = None if fk is None else ("eps", bm._uid, bm._version) + fk
     eps_t = cache.get(ekey) if ekey is not None else None
     s, r, st = index.search_filtered_dev(q_terms, q_off, k, allow, eps=eps_t)
     code = int(st.item())
@@ -164,8 +185,8 @@ def retrieve_batch(retr, questions: Sequence[str], top_k: int,
     pool = max(kv, retr.mmr_max_pool)
     bm._ensure_index()
     allow_v = allow_b = None
+    cache = _ALLOW_CACHE
     if filters:
-        cache = retr.__dict__.setdefault("_device_allow_cache", {})
         chroma_where = build_where_filter(filters)
         if chroma_where:
             allow_v, n_ok = _allow(vs._meta, chroma_where, "chroma", index.device, (index.size + 31) // 32, cache)
@@ -174,29 +195,31 @@ def retrieve_batch(retr, questions: Sequence[str], top_k: int,
         bm._ensure_meta()
         allow_b, n_cand = _allow(bm._meta, filters, "bm25", index.device, (len(bm._id_list) + 31) // 32, cache)
         kb = min(kb, n_cand)
-    key = (id(vs), vs._version, id(bm), bm._version)   # the stores themselves, not only their counters
-    km = getattr(retr, "_device_keymap", None)
-    if km is None or km[0] != key:
-        km = (key, _KeyMap(vs, bm, index.device))
-        retr._device_keymap = km
-    km = km[1]
+    key = (vs._uid, vs._version, bm._uid, bm._version)   # the stores themselves (never-reused uids)
+    km = _KEYMAPS.get(key)
+    if km is None:
+        km = _KeyMap(vs, bm, index.device)
+        if len(_KEYMAPS) >= _KEYMAPS_MAX:
+            _KEYMAPS.clear()
+        _KEYMAPS[key] = km
     # BM25 runs on a side stream that waits only for the allow bitmaps / key map above, so it
     # overlaps the encode and the dense search (a filtered search's status read then waits for the
     # BM25 kernels alone, not for the dense scan queued ahead of it)
     main = torch.cuda.current_stream(dev)
-    side = retr.__dict__.get("_device_bm25_stream")
     if os.environ.get("CLASSMATE_BM25_SAME_STREAM") == "1":     # A/B: the serial schedule
         side = main
-    elif side is None or side.device != dev:
-        side = retr._device_bm25_stream = torch.cuda.Stream(device=dev)
+    else:
+        side = _SIDE_STREAMS.get(dev)
+        if side is None:
+            side = _SIDE_STREAMS[dev] = torch.cuda.Stream(device=dev)
     ready = torch.cuda.Event()
     ready.record(main)
     # E5 encode first (its launches return at once), so the host tokenizes the BM25 queries while
     # the device encodes; then dense pool + MMR
     q = _query_vectors(retr.embedder, questions, dev)
-    d, r = index.search_dev(q, pool, allow=allow_v)
-    vecs = index.gather_dev(r.reshape(-1)).view(nq, pool, index.dim)
-    order = engine.mmr_dev(q, vecs, kv, float(retr.mmr_lambda))
+    # the certificate's exact pass (device-gated; normally nothing runs) waits for the BM25 join
+    # below: its large-LDS grid would otherwise queue behind the BM25 kernels on the CUs
+    d, r = index.search_dev(q, pool, allow=allow_v, defer_exact=True)
     blank = np.array([not q_.strip() for q_ in questions], bool)
     qids = [[] if blank[i] else bm._query_ids(q_) for i, q_ in enumerate(questions)]
     off = np.zeros(nq + 1, np.int32)
@@ -221,7 +244,13 @@ def retrieve_batch(retr, questions: Sequence[str], top_k: int,
             blank_dev = torch.from_numpy(blank).pin_memory().to(dev, non_blocking=True)
             bkeys = torch.where(blank_dev[:, None], torch.full_like(bkeys, -1), bkeys)   # no boolean-index sync
     main.wait_stream(side)
-    # (side-stream tensors read on main: the .cpu() copies below synchronise main before they are freed)
+    index.exact_fallback_dev(q, pool, (d, r), allow=allow_v)
+    vecs = index.gather_dev(r.reshape(-1)).view(nq, pool, index.dim)
+    order = engine.mmr_dev(q, vecs, kv, float(retr.mmr_lambda))
+    # side-stream tensors read on main: tell the caching allocator, so an exception
+    # between here and the host copies below cannot recycle their blocks under main's kernels
+    for t in (bs, br, bkeys, q_terms, q_off):
+        t.record_stream(main)
     vk, vd, vn, bn = engine.rrf_pool_prep_dev(r.contiguous(), d.contiguous(), order, bkeys.contiguous())
     k_dev = top_k if top_k > 0 else kv + kb
     ok, of, ov, ob, ofl, on = engine.rrf_merge_dev(vk, vd, vn, bkeys.contiguous(), bs.contiguous(), bn,
@@ -229,6 +258,9 @@ def retrieve_batch(retr, questions: Sequence[str], top_k: int,
                                                    rrf_k=retr.rrf_k, top_k=k_dev)
     # Python lists once (per-element numpy indexing + float() costs ~40 % of the dict loop)
     ok, of, ov, ob, ofl, on = (t.cpu().tolist() for t in (ok, of, ov, ob, ofl, on))
+    flush = getattr(retr.embedder, "flush_pending", None)     # CachingEmbedder: the misses' .npy files
+    if flush is not None:
+        flush()
     # result dicts of the final top_k items only (fusion.py:132-167 field rules)
     out: List[List[Dict[str, Any]]] = []
     nvr, vs2bm = km.nvr, km.vs2bm

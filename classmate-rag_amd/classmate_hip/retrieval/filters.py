@@ -22,6 +22,7 @@ values -- are evaluated here and enter the program as bitmaps.
 """
 from __future__ import annotations
 
+import itertools
 import re
 from typing import Any, Dict, List, Mapping, Optional
 
@@ -85,6 +86,15 @@ def _typed(v):
     return (type(v).__name__, v)
 
 
+# identities of MetaIndex / BM25Store objects for device caches: never reused (id() of a freed
+# object is, and a fresh MetaIndex restarts its version at 0 -- ADVICE r4)
+_UIDS = itertools.count(1)
+
+
+def next_uid() -> int:
+    return next(_UIDS)
+
+
 class _Column:
     __slots__ = ("py", "ty", "py_map", "ty_map", "n_odd")
 
@@ -114,6 +124,7 @@ class MetaIndex:
         self.tags: Dict[Any, set] = {}
         self._cap = 0
         self.version = 0          # bumped by every set/remove: device copies compare against it
+        self.uid = next_uid()     # this object's identity in device caches (never reused)
         self._dev_cache = None    # engine.filter_bits' device copies of columns / live bits
 
     def __len__(self):

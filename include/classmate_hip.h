@@ -109,8 +109,8 @@ int64_t cm_dense_search_workspace(cm_dense *h, int32_t nq, int32_t k);
  * certified exact re-rank), CM_DENSE_STREAM (K1s, f16 plane, 2 B/element,
  * nq <= 32, per-wave HBM streams, same re-rank), CM_DENSE_Q8 (K1q, int8 plane
  * with per-row scales, 1 B/element, 256-query resident passes, per-row
- * certified exact re-rank; the automatic choice at dim 768 for nq > 32, and for
- * nq <= 32 from 4M rows, unless $CM_DENSE_Q8=0, which keeps K1c / K1s); -1 on error.  Lets callers price the launch against the
+ * certified exact re-rank; the automatic choice at dim 768 for nq > 32, unless
+ * $CM_DENSE_Q8=0, which keeps K1c / K1s), CM_DENSE_Q8S (below); -1 on error.  Lets callers price the launch against the
  * right roofline.  CM_DENSE_F16X3 (the retired split-plane K1b) is accepted by
  * cm_dense_set_path and means automatic.  */
 #define CM_DENSE_F32 1
@@ -118,6 +118,10 @@ int64_t cm_dense_search_workspace(cm_dense *h, int32_t nq, int32_t k);
 #define CM_DENSE_COARSE 3
 #define CM_DENSE_STREAM 4
 #define CM_DENSE_Q8 5
+/* K1q-s: the int8 plane streamed per wave (register ring, no LDS) for nq <= 32,
+ * the same certified re-rank as K1q; the automatic choice at dim 768 for nq <= 32
+ * (unless $CM_DENSE_Q8=0, which keeps K1s) */
+#define CM_DENSE_Q8S 6
 int32_t cm_dense_search_kind(cm_dense *h, int32_t nq, int32_t k);
 /* force a scan kernel for this handle (0 = automatic; an ineligible forced
  * kind falls back to the automatic choice).  Results agree within the 1e-4
@@ -138,6 +142,21 @@ int32_t cm_dense_timing_drain(cm_dense *h, float *ms_out, int32_t cap);
 int cm_dense_search_dev(cm_dense *h, const float *q_dev, int32_t nq, int32_t k, const uint32_t *allow_dev,
                         float *dist_dev, int64_t *row_dev, void *workspace_dev, int64_t workspace_bytes,
                         void *stream);
+/* cm_dense_search_dev in two parts (same arguments, same stream order): the
+ * scan + certified re-rank, then the exact fp32 pass for the queries whose
+ * certificate failed (gated on the device: every workgroup leaves at once when
+ * none did).  A caller enqueues the second part after its concurrent streams'
+ * work has joined (ChromaVectorStore.query, vector_chroma.py:204-253, within
+ * HybridRetriever.retrieve, fusion.py:124-125): the exact pass's workgroups ask
+ * for ~150 KiB of LDS each and would otherwise wait behind the other stream's
+ * kernels.  For CM_DENSE_F32 the first part is the whole search and the second
+ * does nothing.                                                            */
+int cm_dense_search_dev_deferred(cm_dense *h, const float *q_dev, int32_t nq, int32_t k, const uint32_t *allow_dev,
+                                 float *dist_dev, int64_t *row_dev, void *workspace_dev, int64_t workspace_bytes,
+                                 void *stream);
+int cm_dense_exact_fallback_dev(cm_dense *h, const float *q_dev, int32_t nq, int32_t k, const uint32_t *allow_dev,
+                                float *dist_dev, int64_t *row_dev, void *workspace_dev, int64_t workspace_bytes,
+                                void *stream);
 /* copy rows [row0, row0+n) to host (n x dim fp32) and/or their live bits
  * (row0 % 32 == 0; ceil(n/32) words).  Persistence and verification. */
 int cm_dense_export(cm_dense *h, int64_t row0, int64_t n, float *out, uint32_t *live_out);

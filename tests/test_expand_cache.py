@@ -55,8 +55,11 @@ def test_expansion_over_resident_bm25_store(tmp_path, reopen):
     st.upsert_many(ids=[r["id"] for r in recs], texts=[r["text"] for r in recs],
                    metadatas=[r["metadata"] for r in recs])
     if reopen:
+        from classmate_hip.retrieval import bm25
         st.save()
+        bm25.release_all()                  # a new process: the sidecar-opened store, not the attached state
         st = BM25Store.load_or_create(tmp_path / "bm25")
+        assert st._entries.pending
     for c in GOLD["cases"]:
         got = expand_with_neighbors(GOLD["results"], radius=c["radius"], max_per_doc=c["max_per_doc"],
                                     neighbor_penalty=c["neighbor_penalty"], catalog=st)

@@ -22,6 +22,15 @@ FILTERS = {
 }
 
 
+def _new_process():
+    """Forget this process's attached stores (registries): the next construction reads the files,
+    as a new process would (without it a construction on the same directory attaches to the
+    resident state -- the construct-per-call path, tests/test_registry.py)."""
+    from classmate_hip.retrieval import bm25, vector_store
+    bm25.release_all()
+    vector_store.release_all()
+
+
 class PresetEmbedder:
     def __init__(self, qtexts, qvecs):
         self.t = dict(zip(qtexts, qvecs))
@@ -77,6 +86,7 @@ def test_bm25store_sidecar_reload_matches_goldens(stores, corpus, golden, tmp_pa
     _, bm, _ = stores
     bm.index_dir = tmp_path
     bm.save()
+    _new_process()
     again = BM25Store.load_or_create(tmp_path)
     assert again._entries.pending and again._csr is not None
     for fname in FILTERS:
@@ -105,6 +115,7 @@ def test_vector_store_query(stores, corpus, golden, fname):
 def test_vector_store_persistence_and_delete(stores, corpus):
     from classmate_hip.retrieval import GpuVectorStore
     vs, _, d = stores
+    _new_process()
     again = GpuVectorStore(persist_dir=d / "chroma")          # a new process-style reload
     assert again.count() == len(corpus["ids"])
     q = corpus["qvecs"][0]
@@ -133,6 +144,7 @@ def test_vector_store_incremental_log(corpus, tmp_path):
     log = (d / "rows.log.jsonl").read_text().splitlines()
     assert len(log) == 200 + 150 + 10 and json.loads(log[-1])["id"] is None
     assert (d / "vectors.f32").stat().st_size == 300 * emb.shape[1] * 4
+    _new_process()
     again = GpuVectorStore(persist_dir=tmp_path)
     assert again.count() == 290
     q = corpus["qvecs"][0]
@@ -143,6 +155,7 @@ def test_vector_store_incremental_log(corpus, tmp_path):
     assert {r["document"] for r in b if r["id"] in ids[200:]} <= {"new"}
     again.save()
     assert len((d / "rows.log.jsonl").read_text().splitlines()) == 300
+    _new_process()
     third = GpuVectorStore(persist_dir=tmp_path)
     assert [r["id"] for r in third.query(query_embeddings=q, top_k=20)] == [r["id"] for r in a]
 
@@ -300,20 +313,25 @@ def test_vector_store_save_after_trailing_deletes(corpus, tmp_path):
     vs = GpuVectorStore(persist_dir=tmp_path)
     vs.upsert(ids=ids, documents=corpus["texts"][:64], metadatas=corpus["metas"][:64], embeddings=emb)
     vs.delete(ids[40:])                                   # trailing tombstones
+    _new_process()
     again = GpuVectorStore(persist_dir=tmp_path)
     assert again.count() == 40
     again.save()                                          # device copy holds 40 rows, meta says 64
+    _new_process()
     third = GpuVectorStore(persist_dir=tmp_path)
     assert third.count() == 40
     q = corpus["qvecs"][0]
     assert [r["id"] for r in third.query(query_embeddings=q, top_k=10)] == \
         [r["id"] for r in vs.query(query_embeddings=q, top_k=10)]
     third.delete(ids[:40])                                # every row a tombstone
+    _new_process()
     fourth = GpuVectorStore(persist_dir=tmp_path)
     assert fourth.count() == 0
     fourth.save()
+    _new_process()
     assert GpuVectorStore(persist_dir=tmp_path).count() == 0
     fourth.upsert(ids=["new"], documents=["x"], metadatas=[{}], embeddings=emb[:1])
+    _new_process()
     assert [r["id"] for r in GpuVectorStore(persist_dir=tmp_path).query(query_embeddings=emb[0], top_k=3)] == ["new"]
 
 

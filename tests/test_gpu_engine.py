@@ -65,7 +65,9 @@ def test_dense_golden_corpus(eng, corpus, golden):
         np.testing.assert_allclose(dist[i], [w[1] for w in want], atol=DIST_TOL)
 
 
-PATHS = [0, 1, 3, 4]   # auto, K1 fp32, K1c coarse (256-query passes), K1s coarse (<= 32-query streams)
+# auto, K1 fp32, K1c coarse (256-query passes), K1s coarse (<= 32-query streams), K1q (int8 resident
+# passes), K1q-s (int8 <= 32-query streams); forced kinds a shape cannot take run the automatic rule
+PATHS = [0, 1, 3, 4, 5, 6]
 
 
 @pytest.mark.parametrize("path", PATHS[1:])
@@ -110,7 +112,7 @@ def test_dense_shapes(eng, n, nq, k, dim, path):
 
 @pytest.mark.parametrize("n,nq,k,dim", [(30000, 64, 24, 768), (12345, 100, 10, 384), (5000, 300, 32, 100),
                                         (40000, 256, 1, 768), (257, 80, 32, 64)])
-@pytest.mark.parametrize("path", [2, 3, 4])
+@pytest.mark.parametrize("path", [2, 3, 4, 5, 6])
 def test_dense_batched_split_paths(eng, n, nq, k, dim, path):
     """K1c (coarse f16 scan, all queries of a pass resident) and K1s (<= 32 queries, per-wave
     streams), both + certified exact re-rank; path 2 (the retired K1b) means automatic:
@@ -134,15 +136,15 @@ def test_dense_batched_split_paths(eng, n, nq, k, dim, path):
     _check_dense(dist, rows, emb, q, k, live)
 
 
-@pytest.mark.parametrize("path", [3, 4])
+@pytest.mark.parametrize("path", [3, 4, 5, 6])
 def test_dense_coarse_certificate(eng, path):
-    """K1c / K1s: on well-separated data every query is certified (no exact re-run); on a
-    cluster of near-duplicates wider than the coarse lists the certificate fails and the
+    """K1c / K1s / K1q / K1q-s: on well-separated data every query is certified (no exact re-run);
+    on a cluster of near-duplicates wider than the coarse lists the certificate fails and the
     exact fp32 K1 pass takes over for those queries -- results stay within tolerance."""
     rng = np.random.default_rng(77)
     n, dim = 30000, 768
     emb = rng.standard_normal((n, dim)).astype(np.float32)
-    nq = 64 if path == 3 else 16
+    nq = 64 if path in (3, 5) else 16
     q = rng.standard_normal((nq, dim)).astype(np.float32)
     idx = eng.DenseIndex(dim)
     idx.set_path(path)
@@ -153,8 +155,9 @@ def test_dense_coarse_certificate(eng, path):
     assert idx.last_fallbacks() == 0
     # near-duplicates of one vector (cosine gaps ~1e-8, far inside the 2E band): 600 overflow
     # K1c's 64-slot (range, query) buffers; K1s's 1024 small groups hold them, so it gets a
-    # cluster wider than the re-rank band cap (1024 rows) instead
-    nd = 600 if path == 3 else 1500
+    # cluster wider than the re-rank band cap (1024 rows) instead; the int8 kinds get one wider
+    # than their 8192-row band
+    nd = {3: 600, 4: 1500, 5: 9000, 6: 9000}[path]
     base = rng.standard_normal(dim).astype(np.float32)
     dup = base + 1e-4 * rng.standard_normal((nd, dim)).astype(np.float32)
     emb2 = np.concatenate([emb, dup])

@@ -10,7 +10,7 @@ from test_gpu_scale import check_dense, exact_topk, mixed_queries, unit_rows
 
 pytestmark = pytest.mark.gpu
 
-Q8, COARSE, F32 = 5, 3, 1
+Q8, COARSE, F32, STREAM, Q8S = 5, 3, 1, 4, 6
 
 
 @pytest.fixture(scope="module")
@@ -24,18 +24,80 @@ def store():
 
 
 def test_q8_kind_selection(store):
-    """K1q is the automatic batched kind (CM_DENSE_Q8=0 selects K1c); a forced set_path(Q8) always
-    takes it; K1s keeps the small batches below 4M rows (this store: 1M)."""
+    """K1q is the automatic batched kind and K1q-s the automatic small-batch kind (CM_DENSE_Q8=0
+    selects K1c / K1s); a forced set_path(Q8) takes the batched K1q for any batch, a forced Q8S the
+    stream for nq <= 32."""
     import os
     _, idx = store
-    auto = COARSE if os.environ.get("CM_DENSE_Q8", "") == "0" else Q8
-    assert idx.search_kind(256, 24) == auto and idx.search_kind(64, 10) == auto
-    assert idx.search_kind(16, 10) == 4
-    idx.set_path(Q8)
+    off = os.environ.get("CM_DENSE_Q8", "") == "0"
+    assert idx.search_kind(256, 24) == (COARSE if off else Q8) and idx.search_kind(64, 10) == (COARSE if off else Q8)
+    for nq in (1, 16, 32):
+        assert idx.search_kind(nq, 10) == (STREAM if off else Q8S)
+    assert idx.search_kind(33, 10) == (COARSE if off else Q8)
     try:
-        assert idx.search_kind(256, 24) == Q8
+        idx.set_path(Q8)
+        assert idx.search_kind(256, 24) == Q8 and idx.search_kind(16, 24) == Q8
+        idx.set_path(Q8S)
+        assert idx.search_kind(16, 24) == Q8S and idx.search_kind(32, 10) == Q8S
+        assert idx.search_kind(64, 10) == (COARSE if off else Q8)     # ineligible: the automatic rule
+        idx.set_path(STREAM)
+        assert idx.search_kind(16, 24) == STREAM
     finally:
         idx.set_path(0)
+
+
+@pytest.mark.parametrize("nq", [1, 7, 16, 17, 32])
+def test_q8s_matches_exact_fp64(store, nq):
+    """K1q-s (the int8 per-wave stream, one or two 16-query tiles) against the exact fp64 scan, no
+    query sent to the exact fallback, and the same lists as the batched K1q on the same queries (the
+    two share the int8 plane, the bounds and the re-rank, so the distances are bit-identical)."""
+    C, idx = store
+    Q = mixed_queries(C, nq, seed=130 + nq)
+    o_d, o_r = exact_topk(C, Q, 24 + 40)
+    try:
+        idx.set_path(0)
+        assert idx.search_kind(nq, 24) == Q8S
+        d, r = idx.search(Q, 24)
+        assert idx.last_fallbacks() == 0
+        idx.set_path(Q8)
+        d8, r8 = idx.search(Q, 24)
+    finally:
+        idx.set_path(0)
+    check_dense(d, r, o_d, o_r, 24)
+    assert np.array_equal(r, r8) and np.array_equal(d, d8)
+
+
+def test_q8s_gaussian_k10_deletes_filters_and_device_entry(store):
+    """Random directions at k = 10 (the C2' shape), then deletes + an allow bitmap, and the device
+    entry (search_dev, graph-capturable) equal to the host-array search, all on K1q-s."""
+    import torch
+    C, idx = store
+    g = torch.Generator().manual_seed(15)
+    Q = torch.randn(16, 768, generator=g).numpy().astype(np.float32)
+    o_d, o_r = exact_topk(C, Q, 10 + 40)
+    d, r = idx.search(Q, 10)
+    assert idx.search_kind(16, 10) == Q8S and idx.last_fallbacks() == 0
+    check_dense(d, r, o_d, o_r, 10)
+    q = torch.from_numpy(Q).cuda()
+    dd, rd = idx.search_dev(q, 10)
+    torch.cuda.synchronize()
+    assert np.array_equal(rd.cpu().numpy(), r) and np.array_equal(dd.cpu().numpy(), d)
+    drop = np.unique(r[:, :3].ravel())
+    allow = np.ones(C.shape[0], bool)
+    allow[::3] = False
+    words = np.packbits(allow, bitorder="little").view(np.uint32)
+    idx.delete(drop)
+    try:
+        d2, r2 = idx.search(Q, 10, words)
+        assert not np.isin(r2, drop).any() and (r2 % 3 != 0).all()
+        keep = allow.copy()
+        keep[drop] = False
+        rows = np.nonzero(keep)[0]
+        o_d2, o_r2 = exact_topk(C[rows], Q, 10 + 40)
+        check_dense(d2, r2, o_d2, rows[o_r2], 10)
+        assert idx.last_fallbacks() == 0
+    finally:
+        idx.upsert(C[drop], drop.astype(np.int64))       # restore the module store
 
 
 @pytest.mark.parametrize("nq", [256, 100, 40])
@@ -144,6 +206,24 @@ def test_q8_band_overflow_takes_exact_fallback():
             check_dense(d, r, o_d, o_r, k)
             if kind == Q8:
                 assert 1 <= fb <= n_near, fb             # only the cluster queries re-run exactly
+        # the small-batch stream on the cluster queries + 8 ordinary ones: same certificate, same fallback
+        idx.set_path(0)
+        assert idx.search_kind(16, k) == Q8S
+        d, r = idx.search(Q[:16], k)
+        fb = idx.last_fallbacks()
+        check_dense(d, r, o_d[:16], o_r[:16], k)
+        assert 1 <= fb <= n_near, fb
+        # the deferred device entry: scan + re-rank, then the gated exact pass (what the bench step and
+        # retrieve() enqueue behind the BM25 join) == the one-call search
+        import torch
+        q = torch.from_numpy(Q).cuda()
+        idx.set_path(Q8)
+        d1, r1 = idx.search_dev(q, k)
+        out = idx.search_dev(q, k, defer_exact=True)
+        idx.exact_fallback_dev(q, k, out)
+        torch.cuda.synchronize()
+        assert np.array_equal(out[1].cpu().numpy(), r1.cpu().numpy())
+        assert np.array_equal(out[0].cpu().numpy(), d1.cpu().numpy())
     finally:
         idx.set_path(0)
         idx.close()

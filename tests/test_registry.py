@@ -1,0 +1,136 @@
+"""Construct-per-call attach and the device-cache keys, host side.
+
+The reference builds its stores on every ask_question call (rag/pipeline/rag.py:531-534):
+``ChromaVectorStore.from_config()``, ``BM25Store.load_or_create("./indexes/bm25")``.  Here a
+construction attaches to the state this process already holds for the same files when nothing
+changed them since; the semantics must stay the reference's:
+
+* BM25 (one JSONL file, each reference instance an independent copy of it): an attached instance
+  sees exactly what ``load()`` from disk would give; an unsaved mutation through one instance is
+  invisible to later ``load_or_create`` calls (they re-read the file) and to instances sharing the
+  state (copy on write); ``save()`` makes the state attachable again.
+* vector store (a Chroma collection, shared by every client of the directory): constructions on
+  one directory share one collection.
+* another writer of the files (size / mtime change) forces a re-read.
+
+No GPU: BM25 mutations, save and load are host work (the device index is built on first search);
+the vector-store part checks attach/refresh on directories without rows.
+"""
+import json
+import os
+
+import pytest
+
+from classmate_hip.retrieval import bm25 as B
+from classmate_hip.retrieval import device_batch as DB
+from classmate_hip.retrieval import filters as F
+from classmate_hip.retrieval import vector_store as VS
+
+
+def _docs(n, tag):
+    ids = [f"{tag}{i}" for i in range(n)]
+    texts = [f"alpha{tag} beta gamma delta{i % 7} word{i}" for i in range(n)]
+    metas = [{"language": "en", "course": f"C{i % 3}"} for i in range(n)]
+    return ids, texts, metas
+
+
+def test_bm25_attach_copy_on_write_and_save(tmp_path):
+    B.release_all()
+    d = tmp_path / "bm25"
+    s1 = B.BM25Store.load_or_create(d)
+    ids, texts, metas = _docs(20, "a")
+    s1.upsert_many(ids=ids, texts=texts, metadatas=metas)
+    s1.save()
+    # attach: same state object, no parse
+    s2 = B.BM25Store.load_or_create(d)
+    assert s2._st is s1._st and s2._id_list == ids
+    # an unsaved mutation through s1 copies the shared state first: s2 keeps the file's view
+    ids2, texts2, metas2 = _docs(5, "b")
+    s1.upsert_many(ids=ids2, texts=texts2, metadatas=metas2)
+    assert s1._st is not s2._st
+    assert s2._id_list == ids and s1._id_list == ids + ids2
+    # a new load sees the file (not s1's unsaved rows) -- s2's clean state is still attachable
+    s3 = B.BM25Store.load_or_create(d)
+    assert s3._id_list == ids and s3._st is s2._st
+    # after the save, the next construction attaches to s1's state and sees the upserts
+    s1.save()
+    s4 = B.BM25Store.load_or_create(d)
+    assert s4._st is s1._st and s4._id_list == ids + ids2
+    # a sole holder mutates in place (no copy), but the state stops being attachable until saved
+    del s2, s3
+    st = s4._st
+    s4.delete_many([ids[0]])
+    assert s4._st is st or len(st.holders) >= 1
+    s5 = B.BM25Store.load_or_create(d)
+    assert s5._id_list == ids + ids2                   # the file, not the unsaved delete
+
+
+def test_bm25_external_writer_forces_reload(tmp_path):
+    B.release_all()
+    d = tmp_path / "bm25"
+    s1 = B.BM25Store.load_or_create(d)
+    ids, texts, metas = _docs(10, "x")
+    s1.upsert_many(ids=ids, texts=texts, metadatas=metas)
+    s1.save()
+    # another process appends a record to the JSONL (the reference's format, bm25.py:220-231)
+    with open(s1.index_path, "a", encoding="utf-8") as f:
+        f.write(json.dumps({"id": "ext", "text": "external words here", "tokens": ["external", "words"],
+                            "metadata": {"language": "en"}}) + "\n")
+    s2 = B.BM25Store.load_or_create(d)
+    assert s2._st is not s1._st and s2._id_list == ids + ["ext"]
+
+
+def test_bm25_attached_state_searches_like_a_fresh_load(tmp_path):
+    """The attached state and a from-disk load hold the same catalog in the same order (what the
+    device index and the result dicts are built from)."""
+    B.release_all()
+    d = tmp_path / "bm25"
+    s1 = B.BM25Store.load_or_create(d)
+    ids, texts, metas = _docs(30, "q")
+    s1.upsert_many(ids=ids, texts=texts, metadatas=metas)
+    s1.save()
+    s2 = B.BM25Store.load_or_create(d)
+    B.release_all()
+    s3 = B.BM25Store.load_or_create(d)                # forced re-read
+    assert s3._st is not s2._st
+    assert s2._id_list == s3._id_list
+    assert [s2._entries[i].tokens for i in ids] == [s3._entries[i].tokens for i in ids]
+    assert [s2._entries[i].metadata for i in ids] == [s3._entries[i].metadata for i in ids]
+
+
+def test_vector_store_constructions_share_the_collection(tmp_path):
+    VS.release_all()
+    a = VS.GpuVectorStore(persist_dir=tmp_path / "chroma", collection_name="c1")
+    b = VS.GpuVectorStore(persist_dir=tmp_path / "chroma", collection_name="c1")
+    c = VS.GpuVectorStore(persist_dir=tmp_path / "chroma", collection_name="c2")
+    assert a._st is b._st and a._st is not c._st
+    assert a._uid == b._uid != c._uid
+    # another writer creates files in the directory: the next construction starts a fresh state
+    d = tmp_path / "chroma" / "c1"
+    d.mkdir(parents=True)
+    (d / "meta.json").write_text(json.dumps({"format": 2, "dim": 4, "rows": 0}))
+    (d / "rows.log.jsonl").write_text("")
+    e = VS.GpuVectorStore(persist_dir=tmp_path / "chroma", collection_name="c1")
+    assert e._st is not a._st
+    f = VS.GpuVectorStore(persist_dir=tmp_path / "chroma", collection_name="c1")
+    assert f._st is e._st
+    # in-memory stores (persist_dir=None) never share
+    g, h = VS.GpuVectorStore(persist_dir=None), VS.GpuVectorStore(persist_dir=None)
+    assert g._st is not h._st
+
+
+def test_filter_cache_keys_are_typed_and_never_reused():
+    """keys on a never-reused uid (a fresh MetaIndex restarts its version at 0
+    and id() values are recycled) and on the typed clause (True, 1 and "1" differ)."""
+    m1 = F.MetaIndex()
+    k1 = DB._filter_key(m1, {"course": "C1"}, "bm25")
+    uid1 = m1.uid
+    del m1
+    m2 = F.MetaIndex()
+    assert m2.uid != uid1 and m2.version == 0
+    assert DB._filter_key(m2, {"course": "C1"}, "bm25") != k1
+    keys = {DB._filter_key(m2, {"week": v}, "chroma") for v in (True, 1, "1", 1.0)}
+    assert len(keys) == 4
+    assert DB._filter_key(m2, {"$and": [{"a": 1}, {"b": None}]}, "chroma") == \
+        DB._filter_key(m2, {"$and": [{"a": 1}, {"b": None}]}, "chroma")
+    assert DB._filter_key(m2, {"a": object()}, "chroma") is None
