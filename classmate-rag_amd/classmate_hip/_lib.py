@@ -77,6 +77,7 @@ SIGNATURES = {
     "cm_bm25_timing": (c_int, c_vp, c_i32),
     "cm_bm25_timing_drain": (c_i32, c_vp, c_vp, c_i32),
     "cm_dense_search_dev": (c_int, c_vp, c_vp, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp),
+    "cm_shard_merge_topk_dev": (c_int, c_vp, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp),
     "cm_dense_search_dev_deferred": (c_int, c_vp, c_vp, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp),
     "cm_dense_exact_fallback_dev": (c_int, c_vp, c_vp, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp),
     "cm_dense_export": (c_int, c_vp, c_i64, c_i64, c_vp, c_vp),

@@ -338,6 +338,26 @@ def exchange_topk(d, r, bs, br, group=None):
     pack = torch.cat([d.contiguous().view(torch.int32).to(torch.int64), r.to(torch.int64),
                       bs.contiguous().view(torch.int64), br.to(torch.int64)], 1)
     allp = _all_gather_cat(pack, group)                                    # (ws, B, 2P + 2K)
+    return merge_packed(allp, P, K)
+
+
+def merge_packed(allp, P: int, K: int):
+    """The merge of exchange_topk: allp (ws, B, 2P + 2K) int64 packed shard lists -> the global dense
+    (B, P) and BM25 (B, K) lists.  Device tensors: the hand-written kernel (cm_shard_merge_topk_dev,
+    one launch, stream-ordered); host tensors (the gloo CPU tests): the same order through torch
+    sorts (merge_dense_topk / merge_bm25_topk's rules)."""
+    ws, B = allp.shape[0], allp.shape[1]
+    if allp.is_cuda:
+        from . import _lib as L
+        from .engine import _stream
+        allp = allp.contiguous()
+        d_m = torch.empty((B, P), dtype=torch.float32, device=allp.device)
+        r_m = torch.empty((B, P), dtype=torch.int64, device=allp.device)
+        s_m = torch.empty((B, K), dtype=torch.float64, device=allp.device)
+        b_m = torch.empty((B, K), dtype=torch.int64, device=allp.device)
+        L.check(L.fn["cm_shard_merge_topk_dev"](L.ptr(allp), ws, B, P, K, L.ptr(d_m), L.ptr(r_m), L.ptr(s_m),
+                                                L.ptr(b_m), _stream(allp.device.index)), "cm_shard_merge_topk_dev")
+        return d_m, r_m, s_m, b_m
     D = allp[:, :, :P].to(torch.int32).view(torch.float32).permute(1, 0, 2).reshape(B, ws * P)
     R = allp[:, :, P:2 * P].permute(1, 0, 2).reshape(B, ws * P)
     S = allp[:, :, 2 * P:2 * P + K].contiguous().view(torch.float64).permute(1, 0, 2).reshape(B, ws * K)
@@ -353,6 +373,19 @@ def exchange_topk(d, r, bs, br, group=None):
     i2 = torch.argsort(-torch.gather(Sk, 1, i1), dim=1, stable=True)
     idx = torch.gather(i1, 1, i2)[:, :K]
     return d_m, r_m, torch.gather(S, 1, idx), torch.gather(BR, 1, idx)
+
+
+_STARTS: dict = {}
+
+
+def _starts_tensor(shard_starts, dev):
+    key = (tuple(int(x) for x in shard_starts), str(dev))
+    t = _STARTS.get(key)
+    if t is None:
+        if len(_STARTS) > 16:
+            _STARTS.clear()
+        t = _STARTS[key] = torch.as_tensor(list(key[0]), dtype=torch.int64, device=dev)
+    return t
 
 
 def fetch_pool_vectors(rows, q_lo: int, bq: int, gather_local, shard_starts, dim: int, group=None):
@@ -382,7 +415,7 @@ def fetch_pool_vectors(rows, q_lo: int, bq: int, gather_local, shard_starts, dim
     send = gather_local(torch.where(mine, rows - lo, torch.full_like(rows, -1)).reshape(-1)).reshape(B * P, D)
     recv = torch.empty((B * P, D), dtype=torch.float32, device=dev)
     all_to_all(recv, send, None, None, group)
-    starts = torch.as_tensor(list(shard_starts), dtype=torch.int64, device=dev)
+    starts = _starts_tensor(shard_starts, dev)          # resident: no per-step host-to-device copy
     blk = rows[q_lo:q_lo + bq].reshape(-1)
     owner = (torch.searchsorted(starts, blk, right=True) - 1).clamp_(0, ws - 1)    # pads: any slice is zero
     pool = recv.view(ws, bq * P, D)[owner, torch.arange(bq * P, device=dev)]

@@ -167,6 +167,63 @@ class MetaIndex:
                 except TypeError:
                     pass
 
+    # ---- snapshot (vector_store.py's cold open) ----------------------------
+    _JSON_SCALARS = (str, int, float, bool, type(None))
+
+    def snapshot(self):
+        """(info, arrays) describing the columns, tags and live bits -- JSON-able info plus numpy
+        arrays -- or None when a value cannot be restored exactly from JSON (map keys that are not
+        JSON scalars).  Rows holding unhashable values keep their marker code; they are evaluated
+        from ``metas`` row by row, as before."""
+        n = len(self.metas)
+        ok = self._JSON_SCALARS
+        cols, arrays = [], {"live": np.asarray(self.live[:n], bool)}
+        for i, (key, c) in enumerate(self.cols.items()):
+            if not isinstance(key, str):
+                return None
+            if not all(type(v) in ok for v in c.py_map) or not all(type(t[1]) in ok for t in c.ty_map):
+                return None
+            cols.append({"key": key, "n_odd": c.n_odd, "py": [[v, code] for v, code in c.py_map.items()],
+                         "ty": [[t[0], t[1], code] for t, code in c.ty_map.items()]})
+            arrays[f"col{i}_py"] = np.asarray(c.py[:n], np.int32)
+            arrays[f"col{i}_ty"] = np.asarray(c.ty[:n], np.int32)
+        tags = []
+        off = [0]
+        rows = []
+        for t, rs in self.tags.items():
+            if type(t) not in ok:
+                return None
+            tags.append(t)
+            rows.append(np.fromiter(sorted(rs), np.int64, count=len(rs)))
+            off.append(off[-1] + len(rs))
+        arrays["tag_off"] = np.asarray(off, np.int64)
+        arrays["tag_rows"] = np.concatenate(rows) if rows else np.zeros(0, np.int64)
+        return {"rows": n, "cols": cols, "tags": tags}, arrays
+
+    @classmethod
+    def from_snapshot(cls, info, arrays, metas) -> "MetaIndex":
+        """The inverse of ``snapshot``; ``metas`` is the row-aligned metadata list (a lazily
+        parsed one for a cold open)."""
+        m = cls()
+        n = int(info["rows"])
+        cap = max(n, 1024)
+        m._cap = cap
+        m.metas = metas
+        m.live = np.zeros(cap, bool)
+        m.live[:n] = arrays["live"][:n]
+        for i, c in enumerate(info["cols"]):
+            col = _Column(cap)
+            col.py[:n] = arrays[f"col{i}_py"][:n]
+            col.ty[:n] = arrays[f"col{i}_ty"][:n]
+            col.py_map = {v: code for v, code in c["py"]}
+            col.ty_map = {(tn, v): code for tn, v, code in c["ty"]}
+            col.n_odd = int(c.get("n_odd", 0))
+            m.cols[c["key"]] = col
+        off, rows = arrays["tag_off"], arrays["tag_rows"]
+        for j, t in enumerate(info["tags"]):
+            m.tags[t] = set(rows[off[j]: off[j + 1]].tolist())
+        return m
+
     def remove(self, row: int):
         if row >= len(self.metas) or not self.live[row]:
             return

@@ -13,11 +13,22 @@ Chroma persistent dir):
 * ``rows.log.jsonl`` -- an append-only log of ``{"row", "id", "document",
   "metadata"}`` records (``"id": null`` = tombstone), replayed on load, last
   record per row wins;
-* ``meta.json`` -- ``{"format", "dim", "rows"}``, rewritten after every append.
+* ``meta.json`` -- ``{"format", "dim", "rows"}``, rewritten after every append;
+* ``snapshot/`` -- the ids, each row's latest record offset in the log and the
+  metadata filter columns, valid for a prefix of the log (same inode): a cold
+  open reads it plus the records appended after it, and parses a row's
+  document / metadata only when a result needs them (10M rows: seconds instead
+  of a 10M-record JSON replay).
 
 With ``autosave`` (the reference persists every ``upsert``/``delete``) a call
-writes only its own rows and log records: O(batch), not O(collection).
-``save()`` writes everything from the device copy and compacts the log.
+writes only its own rows and log records: O(batch), not O(collection); the
+snapshot is refreshed once the log tail since it passes half the rows.
+``save()`` writes everything from the device copy, compacts the log and writes
+the snapshot.
+
+Constructions on one directory in one process share the collection (``_State``:
+the reference's per-call ``ChromaVectorStore.from_config()`` attaches to the
+resident index while the directory is unchanged).
 
 String ids, documents and metadata stay on the host; rows are assigned in
 insertion order and re-upserting an id overwrites its row in place.
@@ -61,6 +72,8 @@ class _State:
         self.uid = next_uid()       # identity in device caches (never reused)
         self.sig = None             # on-disk signature this state matches
         self.unsaved = False        # changed without a write (autosave=False): not attachable
+        self.line_off = None        # per row: byte offset of its latest record in rows.log.jsonl
+        self.tail = 0               # records appended since the last snapshot
 
 
 def _disk_sig(d: Optional[Path]):
@@ -91,6 +104,72 @@ def release_all() -> None:
 
 def _proxy(name: str):
     return property(lambda self: getattr(self._st, name), lambda self, v: setattr(self._st, name, v))
+
+
+class _LazyRecords:
+    """Parses row r's log record (the document and metadata of a row opened from the snapshot)
+    on first access, by its byte offset in rows.log.jsonl."""
+
+    def __init__(self, path: Path, st: "_State"):
+        self.path, self.st, self.fh = path, st, None
+
+    def parse(self, r: int):
+        if self.fh is None:
+            self.fh = open(self.path, "rb")
+        self.fh.seek(int(self.st.line_off[r]))
+        rec = json.loads(self.fh.readline())
+        live = rec.get("id") is not None
+        return (rec.get("document") if live else None), (rec.get("metadata") if live else None)
+
+
+_PENDING = object()
+_SNAPSHOT_MIN_TAIL = 1 << 15   # log records appended since the snapshot before a refresh is considered
+_SNAPSHOT_TAIL_FRAC = 0.5      # ... and their fraction of the rows
+
+
+class _LazyList(list):
+    """A row-aligned list whose first n0 entries are parsed from the log on first read (field 0:
+    document, 1: metadata); writes and appends behave as a plain list's."""
+
+    def __init__(self, n0: int, rec: _LazyRecords, field: int):
+        super().__init__([_PENDING] * n0)
+        self.rec, self.field = rec, field
+
+    def __getitem__(self, r):
+        v = list.__getitem__(self, r)
+        if v is _PENDING:
+            v = self.rec.parse(r)[self.field]
+            list.__setitem__(self, r, v)
+        return v
+
+
+def _read_snapshot(d: Path, n: int):
+    """(info, arrays, ids) of d/snapshot when it covers a prefix of the current log (same inode,
+    the log at least as long) and of the rows, else None."""
+    sd = d / "snapshot"
+    try:
+        info = json.loads((sd / "info.json").read_text(encoding="utf-8"))
+        st = os.stat(d / "rows.log.jsonl")
+        if (info.get("version") != 1 or info.get("log_ino") != st.st_ino or int(info["log_size"]) > st.st_size
+                or int(info["ids_rows"]) > n):
+            return None
+        ids = json.loads((sd / "ids.json").read_text(encoding="utf-8"))
+        arrays = {p.stem: np.load(p) for p in sd.glob("*.npy")}
+    except (OSError, ValueError, KeyError):
+        return None
+    if len(ids) != int(info["ids_rows"]) or arrays["line_off"].shape[0] != len(ids):
+        return None
+    # rows past the metadata columns' prefix (never given metadata): pad the columns' view
+    info["rows"] = len(ids) if int(info["rows"]) <= len(ids) else None
+    if info["rows"] is None:
+        return None
+    for k in [k for k in arrays if k.endswith("_py") or k.endswith("_ty")]:
+        a = arrays[k]
+        if a.shape[0] < len(ids):
+            arrays[k] = np.concatenate([a, np.full(len(ids) - a.shape[0], -1, np.int32)])
+    if arrays["live"].shape[0] < len(ids):
+        arrays["live"] = np.concatenate([arrays["live"], np.zeros(len(ids) - arrays["live"].shape[0], bool)])
+    return info, arrays, ids
 
 
 @dataclass
@@ -161,36 +240,75 @@ class GpuVectorStore:
             self._load_from(d)
 
     def _load_from(self, d: Path):
+        """Open the directory: from the snapshot + the log records appended after it when the
+        snapshot matches the log (seconds at 10M rows: no per-row JSON parse or metadata insert --
+        documents and metadata dicts are parsed when a result needs them), else by replaying the
+        whole log.  Then the live rows' vectors stream to HBM."""
         meta = json.loads((d / "meta.json").read_text(encoding="utf-8"))
         if meta.get("format") != _FORMAT:
             raise ValueError(f"{d}: unsupported vector store format {meta.get('format')!r}")
         dim, n = int(meta["dim"]), int(meta["rows"])
-        recs: Dict[int, Mapping[str, Any]] = {}
-        with (d / "rows.log.jsonl").open("r", encoding="utf-8") as f:
+        st = self._st
+        log = d / "rows.log.jsonl"
+        snap = _read_snapshot(d, n)
+        if snap is not None:
+            info, arrays, ids = snap
+            n0 = int(info["rows"])
+            st.line_off = np.full(max(n, 1), -1, np.int64)
+            st.line_off[:n0] = arrays["line_off"][:n0]
+            rec = _LazyRecords(log, st)
+            st.ids = ids
+            st.docs = _LazyList(n0, rec, 0)
+            st.meta = MetaIndex.from_snapshot(info, arrays, _LazyList(n0, rec, 1))
+            st.row = {i: r for r, i in enumerate(ids) if i is not None}
+            start = int(info["log_size"])
+        else:
+            st.line_off = np.full(max(n, 1), -1, np.int64)
+            start = 0
+        # the log from `start`: every record after the snapshot (all of them without one)
+        recs: Dict[int, tuple] = {}
+        with open(log, "rb") as f:
+            f.seek(start)
+            off = start
             for line in f:
                 if line.strip():
                     rec = json.loads(line)
                     if rec["row"] < n:   # records past meta.rows belong to an interrupted append
-                        recs[rec["row"]] = rec
-        vecs = np.memmap(d / "vectors.f32", dtype=np.float32, mode="r", shape=(n, dim)) if n else None
+                        recs[rec["row"]] = (rec, off)
+                off += len(line)
+        ids_, row_, docs_, meta_ = st.ids, st.row, st.docs, st.meta
+        while len(ids_) < n:
+            ids_.append(None)
+            docs_.append(None)
+        for r in sorted(recs):
+            rec, off = recs[r]
+            _id = rec.get("id")
+            old = ids_[r]
+            if old is not None and row_.get(old) == r:
+                del row_[old]
+            ids_[r] = _id
+            docs_[r] = rec.get("document") if _id is not None else None
+            st.line_off[r] = off
+            if _id is not None:
+                row_[_id] = r
+                meta_.set(r, rec.get("metadata"))
+            else:
+                meta_.remove(r)
         self._index = engine.DenseIndex(dim, device=self.device, capacity=max(n, 1))
         self._version += 1
-        live = []
-        for r in range(n):
-            rec = recs.get(r)
-            _id = rec.get("id") if rec else None
-            self._ids.append(_id)
-            self._docs.append(rec.get("document") if _id is not None else None)
-            if _id is not None:
-                self._row[_id] = r
-                self._meta.set(r, rec.get("metadata"))
-                live.append(r)
-        if live:
-            idx = np.asarray(live, np.int64)
-            for s in range(0, idx.shape[0], 1 << 16):
-                part = idx[s: s + (1 << 16)]
-                self._index.upsert(np.asarray(vecs[part], np.float32), part)
-        del vecs
+        live = np.fromiter((i is not None for i in ids_), bool, count=n) if n else np.zeros(0, bool)
+        if live.any():
+            vecs = np.memmap(d / "vectors.f32", dtype=np.float32, mode="r", shape=(n, dim))
+            slab = 1 << 16
+            for s0 in range(0, n, slab):
+                s1 = min(n, s0 + slab)
+                lv = live[s0:s1]
+                if lv.all():                 # contiguous: no gather copy
+                    self._index.upsert(np.asarray(vecs[s0:s1], np.float32), np.arange(s0, s1, dtype=np.int64))
+                elif lv.any():
+                    part = np.nonzero(lv)[0] + s0
+                    self._index.upsert(np.asarray(vecs[part], np.float32), part)
+            del vecs
 
     def _record(self, r: int) -> str:
         _id = self._ids[r]
@@ -204,16 +322,28 @@ class GpuVectorStore:
                        encoding="utf-8")
         os.replace(tmp, d / "meta.json")
 
+    def _line_off(self, n: int) -> np.ndarray:
+        lo = self._st.line_off
+        if lo is None or lo.shape[0] < n:
+            new = np.full(max(n, 2 * (0 if lo is None else lo.shape[0]), 1024), -1, np.int64)
+            if lo is not None:
+                new[: lo.shape[0]] = lo
+            self._st.line_off = lo = new
+        return lo
+
     def _append(self, rows: np.ndarray, emb: Optional[np.ndarray]):
-        """Autosave of one upsert (emb given) or delete: its rows' vectors and log records only."""
+        """Autosave of one upsert (emb given) or delete: its rows' vectors and log records only.
+        The snapshot is refreshed (no log rewrite) once the records appended since it outnumber
+        half the rows, so a cold open replays at most that much of the log."""
         d = self._dir
         if d is None or self._index is None:
             return
         if not (d / "meta.json").exists():   # first write of this collection: the full layout
             self.save()
             return
+        n = len(self._ids)
         if emb is not None:
-            n, dim = len(self._ids), self._index.dim
+            dim = self._index.dim
             with open(d / "vectors.f32", "r+b") as f:
                 if f.seek(0, 2) < n * dim * 4:
                     f.truncate(n * dim * 4)
@@ -221,12 +351,47 @@ class GpuVectorStore:
             mm[rows] = emb
             mm.flush()
             del mm
-        with (d / "rows.log.jsonl").open("a", encoding="utf-8") as f:
-            f.write("".join(self._record(int(r)) for r in rows))
+        lo = self._line_off(n)
+        blobs = [self._record(int(r)).encode("utf-8") for r in rows]
+        with (d / "rows.log.jsonl").open("ab") as f:
+            off = f.seek(0, 2)
+            for r, b in zip(rows, blobs):
+                lo[int(r)] = off
+                off += len(b)
+            f.write(b"".join(blobs))
         self._write_meta(d)
+        self._st.tail += len(blobs)
+        if self._st.tail > max(n * _SNAPSHOT_TAIL_FRAC, _SNAPSHOT_MIN_TAIL):
+            self._write_snapshot(d)
+
+    def _write_snapshot(self, d: Path):
+        """snapshot/: ids, each row's latest log record offset and the metadata columns, valid for
+        the log's first ``log_size`` bytes (same file: inode).  Skipped (and any old one removed)
+        when the metadata cannot round-trip through JSON."""
+        shutil.rmtree(d / "snapshot", ignore_errors=True)
+        n = len(self._ids)
+        ms = self._meta.snapshot()
+        lo = self._line_off(n)
+        if ms is None or (n and (lo[:n] < 0).any() and any(self._ids[r] is not None for r in np.nonzero(lo[:n] < 0)[0])):
+            return
+        info, arrays = ms
+        if info["rows"] > n:   # (fewer: trailing rows never given metadata -- the load pads them)
+            return
+        st = os.stat(d / "rows.log.jsonl")
+        info.update(version=1, log_size=st.st_size, log_ino=st.st_ino, ids_rows=n)
+        arrays["line_off"] = lo[:n].copy()
+        tmp = d / "snapshot.tmp"
+        shutil.rmtree(tmp, ignore_errors=True)
+        tmp.mkdir()
+        for k, a in arrays.items():
+            np.save(tmp / f"{k}.npy", a)
+        (tmp / "ids.json").write_text(json.dumps(self._ids, ensure_ascii=False), encoding="utf-8")
+        (tmp / "info.json").write_text(json.dumps(info, ensure_ascii=False), encoding="utf-8")
+        os.replace(tmp, d / "snapshot")
+        self._st.tail = 0
 
     def save(self):
-        """Full write from the device copy + a compacted log (one record per row)."""
+        """Full write from the device copy + a compacted log (one record per row) + the snapshot."""
         d = self._dir
         if d is None or self._index is None:
             return
@@ -241,12 +406,20 @@ class GpuVectorStore:
             # are tombstones were never re-uploaded): pad so the file always holds meta.rows rows
             if vecs.shape[0] < n:
                 f.truncate(n * dim * 4)
+        del vecs
         os.replace(d / "vectors.tmp.f32", d / "vectors.f32")
-        with (d / "rows.tmp.jsonl").open("w", encoding="utf-8") as f:
-            for r in range(len(self._ids)):
-                f.write(self._record(r))
+        lo = self._line_off(n)
+        off = 0
+        with (d / "rows.tmp.jsonl").open("wb") as f:
+            for r in range(n):
+                b = self._record(r).encode("utf-8")
+                lo[r] = off
+                off += len(b)
+                f.write(b)
+        shutil.rmtree(d / "snapshot", ignore_errors=True)    # offsets of the old log
         os.replace(d / "rows.tmp.jsonl", d / "rows.log.jsonl")
         self._write_meta(d)
+        self._write_snapshot(d)
         self._changed(True)
 
     # ---- upsert (vector_chroma.py:168-200) ---------------------------------

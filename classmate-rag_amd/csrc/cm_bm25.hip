@@ -1296,7 +1296,10 @@ int bm25_launch_core(cm_bm25 *h, const int32_t *q_terms_dev, const int32_t *q_of
                        q_off_dev, nq, h->vocab, w.q_idf, w.bounds, nr, rpw_a, h->post_doc.as<int32_t>(),
                        h->post_tf.as<uint16_t>(), head_id, h->headtf.as<uint8_t>(), h->npad, h->dl.as<int32_t>(),
                        h->live.as<uint32_t>(), allow_dev, avgdl, k, w.cand_key, w.cand_row, w.thr, w.need, w.qd_code,
-                       w.qd_term, w.qd_idf, w.qd_tb, w.qd_len, bm25_debug_flags());
+                       w.qd_term, w.qd_idf, w.qd_tb, w.qd_len,
+                       (h->nhead && h->maxr_avgdl > 0.0) ? h->blk_maxr.as<uint8_t>() : (const uint8_t *)nullptr,
+                       h->nhead ? h->blk_maxtf.as<uint8_t>() : (const uint8_t *)nullptr, h->blk_mindl.as<int32_t>(),
+                       h->maxr_avgdl, (int64_t)nr * (kRange / 64), bm25_debug_flags());
     h->timer.end(st);
     CM_HIP(hipGetLastError());
     hipLaunchKernelGGL(bm25_merge_kernel, dim3(nq), dim3(kMergeThreads), 0, st, w.cand_key, w.cand_row, nr, k,

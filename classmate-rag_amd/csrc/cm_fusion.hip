@@ -378,6 +378,68 @@ struct Carver {
 
 }  // namespace
 
+// Multi-GPU exchange merge: the packed all-gather of every shard's
+// dense (distance f32, global row) top-P list and BM25 (score f64, global row) top-K list ->
+// the global lists, identical on every rank.  allp[g][b][2P + 2K] int64: P distance words (f32
+// bits in the low half), P rows, K score words (f64 bits), K rows.  One 256-thread workgroup per
+// query; every entry's rank is the count of entries before it in the merge order -- dense: (f32
+// distance asc, row asc), BM25: (score desc, row asc) with -0.0 == 0.0 -- and -1 rows (pads) after
+// every real entry in shard-then-position order; ranks < P / K are written.  The same order as
+// parallel.merge_dense_topk / merge_bm25_topk (torch sorts); no data-dependent launch, no host sync.
+constexpr int kXMax = 4096;  // shard-list entries per query per kind (ws x P, ws x K)
+__global__ void __launch_bounds__(256) shard_merge_kernel(const int64_t *__restrict__ allp, int ws, int B, int P,
+                                                          int K, float *__restrict__ d_out, int64_t *__restrict__ r_out,
+                                                          double *__restrict__ s_out, int64_t *__restrict__ br_out) {
+  __shared__ uint64_t s_key[kXMax];
+  __shared__ uint32_t s_sub[kXMax];   // tie-break (row for real entries, position for pads)
+  const int b = blockIdx.x;
+  if (b >= B) return;
+  const int W = 2 * P + 2 * K;
+  for (int kind = 0; kind < 2; ++kind) {
+    const int L = kind == 0 ? P : K, n = ws * L;
+    const int c0 = kind == 0 ? 0 : 2 * P;       // value words; rows follow at c0 + L
+    for (int e = threadIdx.x; e < n; e += blockDim.x) {
+      const int g = e / L, j = e - g * L;
+      const int64_t *rec = allp + ((int64_t)g * B + b) * W;
+      const int64_t row = rec[c0 + L + j];
+      uint64_t key;
+      if (row < 0) {
+        key = ~0ull;
+      } else if (kind == 0) {
+        const float dv = __builtin_bit_cast(float, (uint32_t)rec[c0 + j]);
+        key = ((uint64_t)f32_order(dv) << 31) | ((uint64_t)row & 0x7fffffffull);
+      } else {
+        const double sv = __builtin_bit_cast(double, rec[c0 + j]) + 0.0;   // -0.0 -> 0.0
+        key = ~f64_order(sv);                                                // score descending
+      }
+      s_key[e] = key;
+      s_sub[e] = row < 0 ? (uint32_t)e : (uint32_t)row;
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < n; e += blockDim.x) {
+      const uint64_t k0 = s_key[e];
+      const uint32_t t0 = s_sub[e];
+      int rank = 0;
+      for (int x = 0; x < n; ++x) {
+        const uint64_t kx = s_key[x];
+        rank += (kx < k0 || (kx == k0 && s_sub[x] < t0)) ? 1 : 0;
+      }
+      if (rank < L) {
+        const int g = e / L, j = e - g * L;
+        const int64_t *rec = allp + ((int64_t)g * B + b) * W;
+        if (kind == 0) {
+          d_out[(int64_t)b * P + rank] = __builtin_bit_cast(float, (uint32_t)rec[c0 + j]);
+          r_out[(int64_t)b * P + rank] = rec[c0 + L + j];
+        } else {
+          s_out[(int64_t)b * K + rank] = __builtin_bit_cast(double, rec[c0 + j]) + 0.0;
+          br_out[(int64_t)b * K + rank] = rec[c0 + L + j];
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
 extern "C" {
 
 int cm_mmr_dev(const float *q_dev, const float *cands_dev, const int32_t *n_valid_dev, int32_t nq, int32_t pool,
@@ -590,6 +652,18 @@ int cm_rrf_fuse(const int64_t *keys, const int32_t *off, int32_t nl, const doubl
     CM_HIP(hipStreamSynchronize(s.st));
   }
   *out_n = n;
+  return CM_OK;
+}
+
+int cm_shard_merge_topk_dev(const int64_t *allp_dev, int32_t ws, int32_t B, int32_t P, int32_t K, float *d_out,
+                            int64_t *r_out, double *s_out, int64_t *br_out, void *stream) {
+  if (ws <= 0 || B < 0 || P <= 0 || K <= 0) CM_FAIL(CM_EINVAL, "bad shard merge shape");
+  if ((int64_t)ws * P > kXMax || (int64_t)ws * K > kXMax) CM_FAIL(CM_EUNSUPPORTED, "shard lists too long to merge");
+  if (B == 0) return CM_OK;
+  if (!allp_dev || !d_out || !r_out || !s_out || !br_out) CM_FAIL(CM_EINVAL, "NULL argument");
+  hipLaunchKernelGGL(shard_merge_kernel, dim3((unsigned)B), dim3(256), 0, (hipStream_t)stream, allp_dev, ws, B, P, K,
+                     d_out, r_out, s_out, br_out);
+  CM_HIP(hipGetLastError());
   return CM_OK;
 }
 

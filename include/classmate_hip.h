@@ -425,6 +425,16 @@ int cm_short_attention_split_masked(const float *qkv_dev, int32_t B, int32_t S, 
 int cm_long_attention_split(const float *qkv_dev, int32_t B, int32_t S, int32_t H, int32_t head_dim, float scale,
                             float a_scale, const int32_t *key_mask_dev, void *planes_dev, void *stream);
 
+/* The N > 1 step's exchange merge (no reference interface: the reference is single
+ * process -- this is the sharded form of ChromaVectorStore.query, vector_chroma.py:204-253, and
+ * BM25Store.search's sorted(...)[:top_k], bm25.py:199).  allp_dev: the all-gathered packed shard
+ * lists, ws x B x (2P + 2K) int64 (P f32 distance words, P global rows, K f64 score words, K global
+ * rows; -1 rows pad).  Writes the global dense top-P (distance asc, row asc) and BM25 top-K
+ * (score desc, row asc, -0.0 == 0.0), pads last; device pointers, stream-ordered, no sync.
+ * ws x P and ws x K <= 4096. */
+int cm_shard_merge_topk_dev(const int64_t *allp_dev, int32_t ws, int32_t B, int32_t P, int32_t K, float *d_out,
+                            int64_t *r_out, double *s_out, int64_t *br_out, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -430,3 +430,92 @@ def test_retrieve_batch_device_bm25_only_items_take_bm25_fields(corpus, monkeypa
     bm_only = [r for res in got for r in res if r["scores"]["vector_distance"] is None]
     assert bm_only and all(r["document"].endswith(" bmside") and r["metadata"]["course"].startswith("bm25-")
                            for r in bm_only)
+
+
+@pytest.mark.parametrize("refresh", [False, True])
+def test_vector_store_snapshot_cold_open(corpus, tmp_path, monkeypatch, refresh):
+    """§8f-1 / VERDICT r4 #3: a reopened directory -- snapshot + the log records appended after it,
+    and (snapshot removed) the full log replay -- returns the same ids, documents, metadata,
+    filtered lists, distances and stored embeddings as the store that wrote it.  refresh: every
+    autosave rewrites the snapshot (the tail threshold at 0) instead of leaving a tail."""
+    import shutil
+    from classmate_hip.retrieval import GpuVectorStore, build_where_filter
+    from classmate_hip.retrieval import vector_store as VS
+    if refresh:
+        monkeypatch.setattr(VS, "_SNAPSHOT_MIN_TAIL", 0)
+        monkeypatch.setattr(VS, "_SNAPSHOT_TAIL_FRAC", 0.0)
+    _new_process()
+    n = 600
+    ids, emb, metas = corpus["ids"][:n], corpus["emb"][:n], corpus["metas"][:n]
+    vs = GpuVectorStore(persist_dir=tmp_path)
+    vs.upsert(ids=ids[:400], documents=corpus["texts"][:400], metadatas=metas[:400], embeddings=emb[:400])
+    d = tmp_path / "classmate_rag"
+    assert (d / "snapshot" / "info.json").exists()             # the first write is a full save
+    vs.upsert(ids=ids[350:n], documents=["tail"] * (n - 350), metadatas=metas[350:n], embeddings=emb[350:n])
+    vs.delete(ids[:20] + ids[390:395])
+    info = __import__("json").loads((d / "snapshot" / "info.json").read_text())
+    assert (info["ids_rows"] == n) == refresh                  # a tail past the snapshot, or none
+    for mode in ("snapshot", "replay"):
+        _new_process()
+        if mode == "replay":
+            shutil.rmtree(d / "snapshot")
+        again = GpuVectorStore(persist_dir=tmp_path)
+        assert again.count() == vs.count() == n - 25
+        for f in FILTERS.values():
+            cw = build_where_filter(f) if f else None
+            for q in corpus["qvecs"][:4]:
+                a = vs.query(query_embeddings=q, where=cw, top_k=10, include_embeddings=True)
+                b = again.query(query_embeddings=q, where=cw, top_k=10, include_embeddings=True)
+                assert [(r["id"], r["document"], r["metadata"], r["distance"]) for r in a] == \
+                    [(r["id"], r["document"], r["metadata"], r["distance"]) for r in b], (mode, f)
+                assert all(np.array_equal(x["embedding"], y["embedding"]) for x, y in zip(a, b))
+
+
+def test_construct_per_call_attaches_and_sees_upserts(corpus, tmp_path):
+    """the reference's ask_question builds its stores and embedder on every call
+    (rag/pipeline/rag.py:531-545).  Constructions on the same directories / model attach to the
+    resident state (no reload), retrieve exactly what the first instances retrieve, see upserts made
+    through them (vector store: autosave; BM25: upsert_many + save, as ingest_file does,
+    rag/pipeline/rag.py:410-413), and agree with a fresh process's reload."""
+    from classmate_hip.embeddings import E5MultilingualEmbedder
+    from classmate_hip.retrieval import BM25Store, GpuVectorStore, HybridRetriever
+    _new_process()
+    n0, n = 500, len(corpus["ids"])
+    ids, texts, metas, emb = corpus["ids"], corpus["texts"], corpus["metas"], corpus["emb"]
+    vs = GpuVectorStore(persist_dir=tmp_path / "chroma")
+    vs.upsert(ids=ids[:n0], documents=texts[:n0], metadatas=metas[:n0], embeddings=emb[:n0])
+    bm = BM25Store.load_or_create(tmp_path / "bm25")
+    bm.upsert_many(ids=ids[:n0], texts=texts[:n0], metadatas=metas[:n0])
+    bm.save()
+    pe = PresetEmbedder(corpus["qtexts"], corpus["qvecs"])
+
+    def ask(q, f):
+        v = GpuVectorStore(persist_dir=tmp_path / "chroma")
+        b = BM25Store.load_or_create(tmp_path / "bm25")
+        r = HybridRetriever(vector_store=v, bm25_store=b, embedder=pe, k_vector=8, k_bm25=8, rrf_k=60)
+        return v, b, _rows(r.retrieve(question=q, filters=f, top_k=8))
+
+    first = HybridRetriever(vector_store=vs, bm25_store=bm, embedder=pe, k_vector=8, k_bm25=8, rrf_k=60)
+    for q in corpus["qtexts"][:4]:
+        for f in (None, FILTERS["course_cs101"]):
+            v, b, got = ask(q, f)
+            assert v._st is vs._st and b._st is bm._st                 # attached, not reloaded
+            assert got == _rows(first.retrieve(question=q, filters=f, top_k=8))
+    vs.upsert(ids=ids[n0:], documents=texts[n0:], metadatas=metas[n0:], embeddings=emb[n0:])
+    bm.upsert_many(ids=ids[n0:], texts=texts[n0:], metadatas=metas[n0:])
+    bm.save()
+    v, b, _ = ask(corpus["qtexts"][0], None)
+    assert v.count() == n and len(b._id_list) == n
+    want = {}
+    for q in corpus["qtexts"][:4]:
+        want[q] = ask(q, FILTERS["course_cs101"])[2]
+    _new_process()                                                       # a fresh process's reload
+    for q in corpus["qtexts"][:4]:
+        v, b, got = ask(q, FILTERS["course_cs101"])
+        assert v._st is not vs._st and got == want[q]
+    # the embedder: a construction by name attaches to the registered (here random-init) model
+    e = E5MultilingualEmbedder.random_init(seed=0, num_layers=2).share_as("test/e5-registry")
+    e2 = E5MultilingualEmbedder(model_name="test/e5-registry", device="cuda")
+    assert e2.model is e.model
+    assert np.array_equal(e2.encode_queries(["a b c"]), e.encode_queries(["a b c"]))
+    E5MultilingualEmbedder.release_all()

@@ -171,3 +171,43 @@ def test_sharded_hip_bm25_filtered_equals_unsharded_oracle(results, k):
             S, R = r["filt_uneven_10"]
             assert np.array_equal(R, rw)
             assert np.array_equal(S, sc)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ws", [2, 3, 8])
+def test_shard_merge_kernel_equals_torch_merge(ws):
+    """the N > 1 step's merge of the packed all-gather runs as one hand-written kernel
+    (cm_shard_merge_topk_dev); it must give exactly the torch merge's lists (parallel.merge_packed on
+    host tensors, merge_dense_topk / merge_bm25_topk's rules): (distance, row) ascending; (score desc,
+    row asc) with -0.0 == 0.0; -1 pads after every real entry -- incl. equal distances / scores
+    across shards and shards with fewer live entries than the list length."""
+    import torch
+    from classmate_hip import parallel as Pl
+    rng = np.random.default_rng(ws)
+    B, P, K = 64, 24, 10
+    packs = []
+    for g in range(ws):
+        d = np.sort(rng.choice(np.linspace(0.1, 0.9, 40), (B, P)).astype(np.float32), axis=1)   # ties
+        r = rng.permutation(1_000_000)[: B * P].reshape(B, P).astype(np.int64) * ws + g         # unique rows
+        d_key = np.lexsort((r, d), axis=1)
+        d, r = np.take_along_axis(d, d_key, 1), np.take_along_axis(r, d_key, 1)
+        s = -np.sort(-rng.choice([3.5, 2.25, 1.0, 0.0, -0.0, -0.5], (B, K)), axis=1)
+        br = rng.permutation(1_000_000)[: B * K].reshape(B, K).astype(np.int64) * ws + g
+        o = np.lexsort((br, -s), axis=1)
+        s, br = np.take_along_axis(s, o, 1), np.take_along_axis(br, o, 1)
+        npad = rng.integers(0, P // 2, B)                 # short shard lists: pads at the end
+        for i in range(B):
+            if npad[i]:
+                d[i, P - npad[i]:], r[i, P - npad[i]:] = 0.0, -1
+            m = min(npad[i], K)
+            if m:
+                s[i, K - m:], br[i, K - m:] = 0.0, -1
+        dt = torch.from_numpy(d)
+        packs.append(torch.cat([dt.view(torch.int32).to(torch.int64), torch.from_numpy(r),
+                                torch.from_numpy(s).view(torch.int64), torch.from_numpy(br)], 1))
+    allp = torch.stack(packs)                             # (ws, B, 2P + 2K)
+    want = Pl.merge_packed(allp, P, K)
+    got = Pl.merge_packed(allp.cuda(), P, K)
+    torch.cuda.synchronize()
+    for w, gt in zip(want, got):
+        assert torch.equal(w, gt.cpu()), (w[:2], gt[:2])

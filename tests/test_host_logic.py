@@ -123,6 +123,8 @@ def test_bm25store_sidecar_roundtrip_lazy_and_stale(tmp_path):
     side = tmp_path / "bm25_index.jsonl.cm"
     assert sorted(p.name for p in side.iterdir()) == ["doc_off.npy", "ids.json", "line_off.npy", "meta.json",
                                                        "term_ids.npy", "vocab.json"]
+    from classmate_hip.retrieval import bm25 as _bm25
+    _bm25.release_all()              # a new process: open through the sidecar (no attached state)
     s2 = BM25Store.load_or_create(tmp_path)
     assert s2._entries.pending and s2._csr is not None and s2._id_list == ["d0", "d2", "d3"]
     assert s2._csr[1].tolist() == [0, 3, 6, 9]
@@ -150,6 +152,7 @@ def test_bm25store_sidecar_roundtrip_lazy_and_stale(tmp_path):
     # a corrupt sidecar is ignored too
     s3.save()
     (side / "ids.json").write_text("[1, 2", encoding="utf-8")
+    _bm25.release_all()
     s5 = BM25Store.load_or_create(tmp_path)
     assert not s5._entries.pending and len(s5._id_list) == 4
 

@@ -134,3 +134,33 @@ def test_filter_cache_keys_are_typed_and_never_reused():
     assert DB._filter_key(m2, {"$and": [{"a": 1}, {"b": None}]}, "chroma") == \
         DB._filter_key(m2, {"$and": [{"a": 1}, {"b": None}]}, "chroma")
     assert DB._filter_key(m2, {"a": object()}, "chroma") is None
+
+
+def test_meta_index_snapshot_round_trip():
+    """The vector store's cold-open snapshot keeps the filter columns exact: typed maps (True, 1,
+    1.0 stay distinct under Chroma semantics, merge under Python equality), tag row sets,
+    unhashable-value rows (evaluated row by row from the metadata) and deleted rows."""
+    m = F.MetaIndex()
+    metas = [{"course": f"C{i % 3}", "week": [1, 1.0, True, "1"][i % 4], "flag": (i % 2 == 0),
+              "tags": ["a", "b"] if i % 4 == 0 else ["c"]} for i in range(64)]
+    for i, mm in enumerate(metas):
+        m.set(i, mm)
+    m.remove(7)
+    m.set(9, None)
+    snap = m.snapshot()
+    assert snap is not None
+    info, arrays = snap
+    info = json.loads(json.dumps(info))                  # what the file round trip sees
+    m2 = F.MetaIndex.from_snapshot(info, arrays, list(m.metas))
+    assert m2.tags == m.tags and (m2.live[:64] == m.live[:64]).all()
+    clauses = [{"course": "C1"}, {"week": 1}, {"week": True}, {"week": "1"}, {"week": 1.0}, {"flag": True},
+               {"tags": {"$contains": "a"}}, {"course": None, "week": 1}, {"$and": [{"course": "C2"}, {"flag": False}]}]
+    for w in clauses:
+        for a, b in ((m2.chroma_mask, m.chroma_mask), (m2.bm25_mask, m.bm25_mask)):
+            try:
+                want = b(w)
+            except ValueError:                               # e.g. $contains under Chroma semantics
+                with pytest.raises(ValueError):
+                    a(w)
+                continue
+            assert (a(w) == want).all(), w
