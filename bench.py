@@ -524,6 +524,10 @@ def main():
     else:
         out["cpu_baseline"] = None
         out["recall_at_10"] = None
+    if args.mode == "hybrid" and args.dense_legs and ws == 1:
+        # last: it plants rows into the shard (after the recall check has read it)
+        out["c4_dup_cluster_b256"] = dup_cluster_leg(args, dense, N, D, dev, q_main, P,
+                                                     legs.get("c4_dense_10m_b256", {}).get("ms_per_step"))
     out["setup_s"] = time.perf_counter() - t_setup
     if rank == 0:
         line = json.dumps(out)
@@ -666,6 +670,57 @@ def dense_legs(args, dense, N, D, dev, ws, q_step=None, pool=None):
     del d1
     torch.cuda.empty_cache()
     return legs
+
+
+def dup_cluster_leg(args, dense, N, D, dev, q_step, P, normal_ms):
+    """the certificate's cliff, priced.  Real corpora hold near-duplicate chunks (the
+    same file ingested under two courses: distinct ids, identical embeddings); a query that sits on
+    a cluster wider than the int8 band's 8192 rows fails its certificate and is re-searched by the
+    exact fp32 pass.  12 000 rows within 5e-4 (cosine distance) of one row are planted into the
+    shard, and 8 of the step's 256 queries are put on that row: the whole dense search (pool 24,
+    K1q + re-rank + the exact pass for the failing queries) timed like the c4 leg, with the number of
+    exact re-runs.  Runs last (it changes the shard)."""
+    import numpy as np
+    import torch
+    rng = np.random.default_rng(args.seed + 4242)
+    n_c = 12_000
+    base_row = 7
+    base = dense.export(base_row, 1)[0].astype(np.float64)
+    base /= np.linalg.norm(base)
+    at = rng.choice(np.arange(base_row + 1, N), n_c, replace=False).astype(np.int64)
+    d_c = rng.permutation(np.linspace(1e-5, 5e-4, n_c))
+    u = rng.standard_normal((n_c, D))
+    u -= np.outer(u @ base, base)
+    u /= np.linalg.norm(u, axis=1, keepdims=True)
+    t = np.sqrt(2.0 * d_c - d_c ** 2)
+    x = (np.sqrt(1.0 - t ** 2)[:, None] * base + t[:, None] * u).astype(np.float32)
+    dense.upsert(x, at)
+    q = q_step.clone()
+    near = torch.from_numpy((base + 1e-4 * rng.standard_normal((8, D)) / np.sqrt(D)).astype(np.float32)).to(dev)
+    q[:8] = near
+    B = q.shape[0]
+    ws_buf = torch.empty(dense.workspace_bytes(B, P), dtype=torch.uint8, device=dev)
+    o = (torch.empty((B, P), dtype=torch.float32, device=dev), torch.empty((B, P), dtype=torch.int64, device=dev))
+    for _ in range(max(1, args.warmup)):
+        dense.search_dev(q, P, out=o, workspace=ws_buf)
+    torch.cuda.synchronize()
+    steps = max(args.steps, 10)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        dense.search_dev(q, P, out=o, workspace=ws_buf)
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) / steps * 1e3
+    fb = dense.workspace_fallbacks(B, P, ws_buf)
+    rows = o[1][:8].cpu().numpy()
+    on_cluster = float(np.isin(rows, np.concatenate([at, [base_row]])).mean())
+    r = {"ms_per_step": ms, "queries/s": B / ms * 1e3, "exact_reruns": fb, "cluster_rows": n_c,
+         "cluster_queries": 8, "normal_batch_ms": normal_ms, "ratio_to_normal": (ms / normal_ms) if normal_ms else None,
+         "cluster_queries_top24_on_cluster": on_cluster,
+         "note": "dense search (pool 24) of the step's 256 queries with 8 moved onto a planted cluster of 12k rows "
+                 "within 5e-4 of one row; the exact fp32 pass re-searches the failing queries"}
+    log(f"c4_dup_cluster_b256: {ms:.3f} ms per search ({fb} exact re-runs; normal batch "
+        f"{normal_ms if normal_ms is None else round(normal_ms, 3)} ms)")
+    return r
 
 
 def ingest_leg(args, emb, dev, ws, rank):
@@ -1111,8 +1166,13 @@ def construct_leg(args, vs, bm, embedder, qs, K, dev, none_keys, lat):
             r = HybridRetriever(vector_store=v, bm25_store=b, embedder=emb, k_vector=8, k_bm25=8, rrf_k=60,
                                 weight_vector=1.0, weight_bm25=1.0)
             return r.retrieve(question=q, filters=dict(none_keys), top_k=K)
-        for i in range(3):
-            ask(qs[-10 - i])
+        t0 = time.perf_counter()
+        ask(qs[-10])                                   # the first question after the open: key map, filter columns
+        torch.cuda.synchronize()
+        out["first_retrieve_after_open_s"] = time.perf_counter() - t0
+        log(f"first construct-then-retrieve after the cold open: {out['first_retrieve_after_open_s']:.2f}s")
+        for i in range(2):
+            ask(qs[-11 - i])
         torch.cuda.synchronize()
         ts = []
         for i in range(args.e2e_latency_queries):

@@ -121,8 +121,10 @@ def test_bm25store_sidecar_roundtrip_lazy_and_stale(tmp_path):
     s.delete_many(["d1"])
     s.save()
     side = tmp_path / "bm25_index.jsonl.cm"
-    assert sorted(p.name for p in side.iterdir()) == ["doc_off.npy", "ids.json", "line_off.npy", "meta.json",
-                                                       "term_ids.npy", "vocab.json"]
+    names = sorted(p.name for p in side.iterdir())
+    assert [x for x in names if not x.startswith("meta_")] == ["doc_off.npy", "ids.json", "line_off.npy", "meta.json",
+                                                               "term_ids.npy", "vocab.json"]
+    assert "meta_info.json" in names and "meta_live.npy" in names    # the where-filter columns
     from classmate_hip.retrieval import bm25 as _bm25
     _bm25.release_all()              # a new process: open through the sidecar (no attached state)
     s2 = BM25Store.load_or_create(tmp_path)
@@ -132,6 +134,11 @@ def test_bm25store_sidecar_roundtrip_lazy_and_stale(tmp_path):
     assert (e.id, e.text, e.tokens, e.metadata) == ("d2", texts[2], ["epsilon", "alpha", "alpha"], metas[2])
     assert [s2._vocab.get(t) for t in e.tokens] == e.term_ids.tolist()
     assert dict.__getitem__(s2._entries, "d3") == 2           # still a line number: nothing else parsed
+    # where-filters from the persisted columns, without parsing the records (quirk Q4 included)
+    assert not s2._meta_dirty
+    for w in ({"course": "c1"}, {"course": None, "unit": None}, {"tags": {"$contains": "x"}}, {"course": "c2"}):
+        assert s2._meta.bm25_mask(w).tolist() == s._meta.bm25_mask(w).tolist(), w
+    assert dict.__getitem__(s2._entries, "d3") == 2
     ref = {i: (x.text, x.tokens, x.metadata) for i, x in s._entries.items()}
     assert {i: (x.text, x.tokens, x.metadata) for i, x in s2._entries.items()} == ref   # materializes
     assert not s2._entries.pending
