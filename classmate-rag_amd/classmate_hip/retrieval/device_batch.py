@@ -256,8 +256,18 @@ def retrieve_batch(retr, questions: Sequence[str], top_k: int,
     ok, of, ov, ob, ofl, on = engine.rrf_merge_dev(vk, vd, vn, bkeys.contiguous(), bs.contiguous(), bn,
                                                    w_vec=retr.weight_vector, w_bm25=retr.weight_bm25,
                                                    rrf_k=retr.rrf_k, top_k=k_dev)
-    # Python lists once (per-element numpy indexing + float() costs ~40 % of the dict loop)
-    ok, of, ov, ob, ofl, on = (t.cpu().tolist() for t in (ok, of, ov, ob, ofl, on))
+    # one device-to-host copy of all six outputs (byte views concatenated; six .cpu() calls were six
+    # synchronising copies), then Python lists once (per-element numpy indexing + float() costs ~40 %
+    # of the dict loop)
+    outs = (ok, of, ov, ob, ofl, on)
+    blob = torch.cat([t.contiguous().view(-1).view(torch.uint8) for t in outs]).cpu().numpy()
+    parts, o = [], 0
+    for t in outs:
+        nb = t.numel() * t.element_size()
+        arr = blob[o:o + nb].view(np.dtype(str(t.dtype).replace("torch.", ""))).reshape(tuple(t.shape))
+        parts.append(arr.tolist())
+        o += nb
+    ok, of, ov, ob, ofl, on = parts
     flush = getattr(retr.embedder, "flush_pending", None)     # CachingEmbedder: the misses' .npy files
     if flush is not None:
         flush()

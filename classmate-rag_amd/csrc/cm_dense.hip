@@ -1723,10 +1723,13 @@ bool k1q_seed_q8() {
   return v;
 }
 int64_t k1qs_sample_frac() {
+  // K1q-s's f16 seed sample: 1/32 of the rows (10M x 768, k = 24: B = 1 1.48 / B = 16 1.61 ms per search
+  // vs 1.54 / 1.64 at 1/16 and 1.47 / 1.76 at 1/64 -- a thinner sample's looser seed costs the 16-query
+  // batch more candidates than its pass saves, profiles/r05_q8s_sample_sweep.txt)
   static const int64_t v = [] {   // $CM_K1QS_SAMPLE = 1/fraction of the rows in K1q-s's seed sample (A/B knob)
     const char *e = getenv("CM_K1QS_SAMPLE");
     const int64_t f = e ? atoll(e) : 0;
-    return f >= 2 && f <= 256 ? f : (int64_t)16;
+    return f >= 2 && f <= 256 ? f : (int64_t)32;
   }();
   return v;
 }
