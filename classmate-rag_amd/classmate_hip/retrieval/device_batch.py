@@ -74,7 +74,8 @@ def applicable(retr, filters, hybrid: bool) -> bool:
     if not (0 < retr.k_vector <= pool <= limit and 0 < retr.k_bm25 <= limit):
         return False
     # the host path clamps k to the candidates; the device path needs full lists
-    return vs._index.live_count() >= pool and len(bm._id_list) >= retr.k_bm25
+    # live rows = the store's id -> row map (a device popcount + sync per call before)
+    return len(vs._row) >= pool and len(bm._id_list) >= retr.k_bm25
 
 
 def _query_vectors(embedder, questions: Sequence[str], dev):

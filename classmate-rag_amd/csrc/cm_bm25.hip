@@ -776,6 +776,136 @@ __global__ void __launch_bounds__(kMergeThreads) bm25_merge_kernel(const uint64_
   }
 }
 
+// The same merge for k <= kMergeSmallK with a 256-thread workgroup (one wave per SIMD, <= 128 VGPRs,
+// 48 B of LDS): it fits beside a K1q workgroup (384 registers per SIMD, <= 131 KiB of LDS), so the
+// BM25 chain after K2a runs while the dense scan still streams instead of queueing behind it -- the
+// 1024-thread bm25_merge_kernel needs a whole empty CU (4 waves of 128 VGPRs per SIMD) and waited
+// for K1q's last workgroup (profiles/r05_headline_timeline.txt).
+// Phase 1: each thread reads the heads of its lists l = tid + 256 s (coalesced, merge_batch<K>()
+// independent loads in flight) and keeps the K smallest in a sorted register array of (key, row,
+// list<<5 | depth).  A list whose head misses its thread's K smallest heads cannot place an entry in
+// the top k <= K (K smaller distinct heads precede all its entries), so it is dropped for good.
+// Phase 2: k rounds of a block tournament over the threads' array fronts; the owner pops its front
+// and re-inserts that list's next entry, which it prefetched the round before (the load latency
+// hides behind the reduction).  Same output as bm25_merge_kernel: the k smallest (key, row), 0.0 /
+// -1 padding.
+constexpr int kMergeSmallK = 12;   // K = 16 needs > 128 VGPRs
+constexpr int kMergeSmallThreads = 256;
+template <int K>
+constexpr int merge_batch() { return K > 8 ? 4 : 8; }   // <= 128 VGPRs
+template <int K>
+__device__ inline void merge_insert(uint64_t (&lk)[K], uint32_t (&lr)[K], uint32_t (&ll)[K], uint64_t ck,
+                                    uint32_t cr, uint32_t cl) {
+#pragma unroll
+  for (int i = 0; i < K; ++i) {  // sorted insertion, static indices (the last entry falls off)
+    if (pk_less(ck, cr, lk[i], lr[i])) {
+      const uint64_t tk = lk[i];
+      const uint32_t tr = lr[i], tl = ll[i];
+      lk[i] = ck;
+      lr[i] = cr;
+      ll[i] = cl;
+      ck = tk;
+      cr = tr;
+      cl = tl;
+    }
+  }
+}
+template <int K>
+__global__ void __launch_bounds__(kMergeSmallThreads) bm25_merge_small_kernel(const uint64_t *__restrict__ cand_key,
+                                                                               const uint32_t *__restrict__ cand_row,
+                                                                               int nr, int k, double *__restrict__ out_score,
+                                                                               int64_t *__restrict__ out_row) {
+  const int qi = blockIdx.x;
+  __shared__ uint64_t sk[kMergeSmallThreads / 64];
+  __shared__ uint32_t sr[kMergeSmallThreads / 64];
+  uint64_t lk[K];
+  uint32_t lr[K], ll[K];
+#pragma unroll
+  for (int i = 0; i < K; ++i) {
+    lk[i] = kEmptyKey;
+    lr[i] = 0xffffffffu;
+    ll[i] = 0;
+  }
+  const int64_t nl = lheads_total((int)gridDim.x, nr);
+  constexpr int kMergeBatch = merge_batch<K>();
+  for (int l0 = threadIdx.x; l0 < nr; l0 += kMergeSmallThreads * kMergeBatch) {
+    uint64_t bk[kMergeBatch];
+    uint32_t br[kMergeBatch];
+#pragma unroll
+    for (int u = 0; u < kMergeBatch; ++u) {
+      const int l = l0 + u * kMergeSmallThreads;
+      bk[u] = kEmptyKey;
+      br[u] = 0xffffffffu;
+      if (l < nr) {
+        bk[u] = cand_key[lhead(qi, l, nr)];
+        br[u] = cand_row[lhead(qi, l, nr)];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kMergeBatch; ++u)
+      if (br[u] != 0xffffffffu && pk_less(bk[u], br[u], lk[K - 1], lr[K - 1]))   // empty list / cannot enter
+        merge_insert<K>(lk, lr, ll, bk[u], br[u], (uint32_t)(l0 + u * kMergeSmallThreads) << 5);
+  }
+  uint64_t nk = kEmptyKey;   // prefetched next entry of the front list
+  uint32_t nrow = 0xffffffffu;
+  auto prefetch = [&]() {
+    nk = kEmptyKey;
+    nrow = 0xffffffffu;
+    const int d = (int)(ll[0] & 31u) + 1;
+    if (lr[0] != 0xffffffffu && d < k) {
+      const int64_t o = lslot(qi, ll[0] >> 5, nr, nl, k, d);
+      nk = cand_key[o];
+      nrow = cand_row[o];
+    }
+  };
+  prefetch();
+  for (int i = 0; i < k; ++i) {
+    const PairKey best = block_min_pair(lk[0], lr[0], sk, sr);
+    if (threadIdx.x == 0) {
+      const int64_t o = (int64_t)qi * k + i;
+      if (best.r == 0xffffffffu) {
+        out_score[o] = 0.0;
+        out_row[o] = -1;
+      } else {
+        out_score[o] = f64_unorder(~best.k);
+        out_row[o] = (int64_t)best.r;
+      }
+    }
+    if (best.r == 0xffffffffu) continue;
+    if (lr[0] == best.r && lk[0] == best.k) {   // the owner pops its front (entries are unique)
+      const uint32_t nxt = ll[0] + 1;
+#pragma unroll
+      for (int t = 0; t + 1 < K; ++t) {
+        lk[t] = lk[t + 1];
+        lr[t] = lr[t + 1];
+        ll[t] = ll[t + 1];
+      }
+      lk[K - 1] = kEmptyKey;
+      lr[K - 1] = 0xffffffffu;
+      if (nrow != 0xffffffffu) merge_insert<K>(lk, lr, ll, nk, nrow, nxt);   // the list's sentinel ends it
+      prefetch();
+    }
+  }
+}
+
+// bm25_merge_kernel or, for k <= kMergeSmallK, its small-workgroup form (launch helper)
+int launch_bm25_merge(const uint64_t *cand_key, const uint32_t *cand_row, int nq, int nr, int k, double *score,
+                      int64_t *row, hipStream_t st) {
+  if (k <= 8)
+    hipLaunchKernelGGL(bm25_merge_small_kernel<8>, dim3(nq), dim3(kMergeSmallThreads), 0, st, cand_key, cand_row, nr, k,
+                       score, row);
+  else if (k <= 10)
+    hipLaunchKernelGGL(bm25_merge_small_kernel<10>, dim3(nq), dim3(kMergeSmallThreads), 0, st, cand_key, cand_row, nr,
+                       k, score, row);
+  else if (k <= kMergeSmallK)
+    hipLaunchKernelGGL(bm25_merge_small_kernel<kMergeSmallK>, dim3(nq), dim3(kMergeSmallThreads), 0, st, cand_key,
+                       cand_row, nr, k, score, row);
+  else
+    hipLaunchKernelGGL(bm25_merge_kernel, dim3(nq), dim3(kMergeThreads), 0, st, cand_key, cand_row, nr, k, score, row);
+  CM_HIP(hipGetLastError());
+  return CM_OK;
+}
+
 // Filtered statistics: number of candidate docs and their total length.
 __global__ void bm25_filtered_stats_kernel(const int32_t *__restrict__ dl, const uint32_t *__restrict__ live,
                                            const uint32_t *__restrict__ allow, int64_t ndocs,
@@ -1253,6 +1383,7 @@ BmWs bm_ws_layout(const cm_bm25 *h, int nq, int total_terms, int k, void *base) 
 // Launch K2 + merge given q_idf and *avgdl already in the workspace.
 int bm25_launch_core(cm_bm25 *h, const int32_t *q_terms_dev, const int32_t *q_off_dev, int nq, int total_terms, int k,
                      const uint32_t *allow_dev, const BmWs &w, double *score_dev, int64_t *row_dev, hipStream_t st) {
+  int rc;
   const double *avgdl = w.avgdl;
   const int nr = (int)std::max<int64_t>(1, ceil_div(h->ndocs, kRange));
   if (nr > kMergePer * kMergeThreads) CM_FAIL(CM_EUNSUPPORTED, "BM25 shard too large (> 16.7M docs)");
@@ -1302,9 +1433,7 @@ int bm25_launch_core(cm_bm25 *h, const int32_t *q_terms_dev, const int32_t *q_of
                        h->maxr_avgdl, (int64_t)nr * (kRange / 64), bm25_debug_flags());
     h->timer.end(st);
     CM_HIP(hipGetLastError());
-    hipLaunchKernelGGL(bm25_merge_kernel, dim3(nq), dim3(kMergeThreads), 0, st, w.cand_key, w.cand_row, nr, k,
-                       score_dev, row_dev);
-    CM_HIP(hipGetLastError());
+    if ((rc = launch_bm25_merge(w.cand_key, w.cand_row, nq, nr, k, score_dev, row_dev, st))) return rc;
     CM_HIP(hipMemsetAsync(w.item_count, 0, 4, st));
     hipLaunchKernelGGL(bm25_plan_kernel, dim3((unsigned)ceil_div(nqg * nr, 256)), dim3(256), 0, st, w.qd_code,
                        w.qd_idf, w.qd_len, nq, (int)(head_id != nullptr), h->head_maxtf.as<uint8_t>(),
@@ -1328,10 +1457,7 @@ int bm25_launch_core(cm_bm25 *h, const int32_t *q_terms_dev, const int32_t *q_of
                      bm25_debug_flags());
   if (!prune) h->timer.end(st);
   CM_HIP(hipGetLastError());
-  hipLaunchKernelGGL(bm25_merge_kernel, dim3(nq), dim3(kMergeThreads), 0, st, w.cand_key, w.cand_row, nr, k,
-                     score_dev, row_dev);
-  CM_HIP(hipGetLastError());
-  return CM_OK;
+  return launch_bm25_merge(w.cand_key, w.cand_row, nq, nr, k, score_dev, row_dev, st);
 }
 
 // (query, range) pairs re-scored after the tail pass by the pruned search that last used this

@@ -1840,6 +1840,7 @@ int set_coarse_attrs() {
         {reinterpret_cast<const void *>(&dense_rerank_kernel), kGatherCap * 12},
         {reinterpret_cast<const void *>(&dense_q8_scan_kernel<false>), kQLds},
         {reinterpret_cast<const void *>(&dense_q8_scan_kernel<true>), kQLds},
+        {reinterpret_cast<const void *>(&dense_q8_scan_kernel<false, K1Q_LDS_SHARED>), kQLdsShared},
         {reinterpret_cast<const void *>(&dense_rerank_q8_kernel), kQRerankLds}};
     for (const auto &f : fs) {
       const hipError_t e = hipFuncSetAttribute(f.first, hipFuncAttributeMaxDynamicSharedMemorySize, f.second);
@@ -1922,9 +1923,15 @@ int launch_coarse(cm_dense *h, const float *q_dev, int nq, int k, int kind, cons
                        h->rnorm, h->dim, w.seed, k1q_seed_q8() ? 0 : 1);
     CM_HIP(hipGetLastError());
     h->timer.begin(st);
-    hipLaunchKernelGGL(dense_q8_scan_kernel<false>, dim3(c.n_pass * c.n_wg), dim3(256), kQLds, st, h->Xq,
-                       h->rmeta, h->live, allow, n_words, w.qq, w.qsc, nq, (const float *)w.seed, c.rows_per_wg,
-                       c.rows_end, c.n_wg, w.keys, w.ups, w.cnt, (float *)nullptr);
+    // deferred search (!run_exact): the caller runs other work beside it -> the shared LDS footprint
+    if (run_exact)
+      hipLaunchKernelGGL(dense_q8_scan_kernel<false>, dim3(c.n_pass * c.n_wg), dim3(256), kQLds, st, h->Xq,
+                         h->rmeta, h->live, allow, n_words, w.qq, w.qsc, nq, (const float *)w.seed, c.rows_per_wg,
+                         c.rows_end, c.n_wg, w.keys, w.ups, w.cnt, (float *)nullptr);
+    else
+      hipLaunchKernelGGL((dense_q8_scan_kernel<false, K1Q_LDS_SHARED>), dim3(c.n_pass * c.n_wg), dim3(256), kQLdsShared,
+                         st, h->Xq, h->rmeta, h->live, allow, n_words, w.qq, w.qsc, nq, (const float *)w.seed,
+                         c.rows_per_wg, c.rows_end, c.n_wg, w.keys, w.ups, w.cnt, (float *)nullptr);
     h->timer.end(st);
     CM_HIP(hipGetLastError());
     }

@@ -150,7 +150,9 @@ int cm_dense_search_dev(cm_dense *h, const float *q_dev, int32_t nq, int32_t k, 
  * HybridRetriever.retrieve, fusion.py:124-125): the exact pass's workgroups ask
  * for ~150 KiB of LDS each and would otherwise wait behind the other stream's
  * kernels.  For CM_DENSE_F32 the first part is the whole search and the second
- * does nothing.                                                            */
+ * does nothing.  The deferred form also runs K1q with its shared LDS footprint
+ * (131 KiB instead of 160: room for one BM25 block beside each scan workgroup);
+ * results are identical either way.                                        */
 int cm_dense_search_dev_deferred(cm_dense *h, const float *q_dev, int32_t nq, int32_t k, const uint32_t *allow_dev,
                                  float *dist_dev, int64_t *row_dev, void *workspace_dev, int64_t workspace_bytes,
                                  void *stream);

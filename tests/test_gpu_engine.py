@@ -431,7 +431,7 @@ def test_bm25_many_ranges_vs_c_oracle(eng, policy, path):
     rare = int(np.nonzero(csr["df"] == csr["df"][csr["df"] > 0].min())[0][0])
     queries = [rng.integers(0, vocab, 6).tolist() for _ in range(20)]
     queries += [[0, 1, 2], [3, 3, 7], [rare], [rare, vocab - 1], [int(x) for x in rng.integers(0, 50, 40)]]
-    for k in (1, 10, 256):
+    for k in (1, 8, 9, 10, 12, 13, 256):     # every merge form: 256-thread K = 8 / 10 / 12, 1024-thread
         scores, rows, nvalid = b.search(queries, k)
         o_sc, o_rw = corc.bm25_topk(csr, idf, avgdl, queries, k)
         for i in range(len(queries)):
