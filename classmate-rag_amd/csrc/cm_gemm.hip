@@ -65,6 +65,9 @@ __device__ __forceinline__ h16x8 as_h8(i32x4 v) { return __builtin_bit_cast(h16x
 #ifndef K10_SMALL_S
 #define K10_SMALL_S 6          // ring stages of the 64 x 32 tile (M <= 32): 6 vs 4 = 1.03 vs 1.08 ms batch-1 encode
 #endif
+#ifndef K10S_DEPTH
+#define K10S_DEPTH 8           // k-steps in flight per wave of the skinny (M <= 32) kernel
+#endif
 #ifndef K10_W6
 #define K10_W6 12              // waves per workgroup at the 96 x 192 tile (2 x 6: three per SIMD)
 #endif
@@ -378,6 +381,84 @@ __global__ void __launch_bounds__(64 * NW)
 #undef K10_STEP
 }
 
+// K10s: the skinny form for M <= 32 rows (one short query: a retrieve() call).  The GEMM is then a
+// weight stream, and the tiled kernel's N / 32 workgroups (24 at N = 768) are too few to keep it
+// in flight (FFN-down 21 us for 9.4 MB at batch 1, profiles/r05_e5_b1_kernels.txt).  Here one
+// wave per 16 output columns (N / 16 workgroups of one wave, each on its own CU) streams its
+// column block's split blocks -- one contiguous run of K / 32 x 2 KiB -- and the RB row blocks of A
+// (L2-resident: every wave reads the same <= 2 x 2 KiB per k-step) straight into registers, D
+// k-steps in flight.  Per k-step the same three MFMAs in the same order as linear_f16x3_kernel
+// (lo.hi, hi.lo, hi.hi into the fp32 accumulator, k ascending), so every output bit equals the
+// tiled kernel's: a query embeds the same alone or batched (tests/test_gpu_gemm.py).
+template <int RB, int D, int EPI>
+__global__ void __launch_bounds__(64)
+    linear_f16x3_skinny_kernel(const _Float16 *__restrict__ Ap, int64_t M, int K, const _Float16 *__restrict__ Wp,
+                               const float *__restrict__ bias, float out_scale, int N, float *__restrict__ Cout,
+                               float next_scale, _Float16 *__restrict__ Cp) {
+  const int lane = threadIdx.x, cb = blockIdx.x;
+  const int nk = K >> 5;                               // k-steps (a multiple of D: checked by the launcher)
+  const int64_t rstride = (int64_t)nk * 2048;          // bytes per row block of a split buffer
+  const unsigned char *wp = reinterpret_cast<const unsigned char *>(Wp) + (int64_t)cb * rstride + lane * 16;
+  const unsigned char *ap = reinterpret_cast<const unsigned char *>(Ap) + lane * 16;
+  i32x4 wh[D], wl[D], ah[D][RB], al[D][RB];
+#define K10S_LOAD(slot, step)                                                                       \
+  do {                                                                                              \
+    const int64_t o_ = (int64_t)(step) * 2048;                                                      \
+    wh[slot] = *reinterpret_cast<const i32x4 *>(wp + o_);                                           \
+    wl[slot] = *reinterpret_cast<const i32x4 *>(wp + o_ + 1024);                                    \
+    _Pragma("unroll") for (int r = 0; r < RB; ++r) {                                                \
+      ah[slot][r] = *reinterpret_cast<const i32x4 *>(ap + r * rstride + o_);                        \
+      al[slot][r] = *reinterpret_cast<const i32x4 *>(ap + r * rstride + o_ + 1024);                 \
+    }                                                                                               \
+  } while (0)
+#define K10S_MFMA(slot)                                                                                       \
+  _Pragma("unroll") for (int r = 0; r < RB; ++r) {                                                            \
+    acc[r][0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_h8(al[slot][r]), as_h8(wh[slot]), acc[r][0], 0, 0, 0); \
+    acc[r][0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_h8(ah[slot][r]), as_h8(wl[slot]), acc[r][0], 0, 0, 0); \
+    acc[r][0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_h8(ah[slot][r]), as_h8(wh[slot]), acc[r][0], 0, 0, 0); \
+  }
+  g32x4 acc[RB][1];
+#pragma unroll
+  for (int r = 0; r < RB; ++r) acc[r][0] = g32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int d = 0; d < D; ++d) K10S_LOAD(d, d);
+  for (int s0 = 0; s0 + D < nk; s0 += D) {             // steady state: consume step s0 + d, refill its slot
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      K10S_MFMA(d)
+      K10S_LOAD(d, s0 + D + d);
+    }
+  }
+#pragma unroll
+  for (int d = 0; d < D; ++d) K10S_MFMA(d)             // the last D steps
+#undef K10S_LOAD
+#undef K10S_MFMA
+  k10_epilogue<2 * RB, 1, 2, EPI>(acc, 0, cb, 0, 0, lane, bias, out_scale, next_scale, M, N, Cout, Cp);
+}
+
+template <int RB, int D>
+static int launch_skinny(const _Float16 *A, int64_t M, int K, const _Float16 *W, const float *bias, float out_scale,
+                         int N, int epi, float *C, float next_scale, _Float16 *Cp, hipStream_t st) {
+  const dim3 grid((unsigned)(N / 16)), block(64);
+  switch (epi) {
+    case kEpiF32:
+      hipLaunchKernelGGL((linear_f16x3_skinny_kernel<RB, D, kEpiF32>), grid, block, 0, st, A, M, K, W, bias, out_scale,
+                         N, C, next_scale, Cp);
+      break;
+    case kEpiF32Gelu:
+      hipLaunchKernelGGL((linear_f16x3_skinny_kernel<RB, D, kEpiF32Gelu>), grid, block, 0, st, A, M, K, W, bias,
+                         out_scale, N, C, next_scale, Cp);
+      break;
+    case kEpiPlanesGelu:
+      hipLaunchKernelGGL((linear_f16x3_skinny_kernel<RB, D, kEpiPlanesGelu>), grid, block, 0, st, A, M, K, W, bias,
+                         out_scale, N, C, next_scale, Cp);
+      break;
+    default: CM_FAIL(CM_EINVAL, "unknown epilogue");
+  }
+  CM_HIP(hipGetLastError());
+  return CM_OK;
+}
+
 // fp32 rows [N][K] (weights or activations) -> split blocks of rows * scale
 __global__ void split_rows_kernel(const float *__restrict__ W, int64_t N, int K, float scale, _Float16 *__restrict__ P) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // one 8-element segment
@@ -506,10 +587,20 @@ extern "C" int cm_linear_f16x3(const void *a_planes, int64_t M, int32_t K, const
     CM_HIP(hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev));
     g_n_cu = n > 0 ? n : 256;
   }
-  const TileCfg t = pick_tile(M, N, g_n_cu);
   const _Float16 *A = (const _Float16 *)a_planes, *W = (const _Float16 *)w_planes;
   _Float16 *Cp = (_Float16 *)c_planes;
   hipStream_t st = (hipStream_t)stream;
+  // K10s for M <= 32 with a bias (every XLM-R projection has one); CM_K10_SKINNY=0 forces the tiled kernel
+  static const bool skinny_on = [] {
+    const char *e = getenv("CM_K10_SKINNY");
+    return !(e && e[0] == '0');
+  }();
+  if (skinny_on && M <= 32 && bias_dev && (K / 32) % K10S_DEPTH == 0) {
+    if (M <= 16)
+      return launch_skinny<1, K10S_DEPTH>(A, M, K, W, bias_dev, out_scale, N, epilogue, c_dev, next_scale, Cp, st);
+    return launch_skinny<2, K10S_DEPTH>(A, M, K, W, bias_dev, out_scale, N, epilogue, c_dev, next_scale, Cp, st);
+  }
+  const TileCfg t = pick_tile(M, N, g_n_cu);
   // waves per workgroup: two or three per SIMD, so one wave's MFMAs cover another's waits
   if (t.bmb == 12 && t.bnb == 12)  // 192 x 192: half the operand bytes per MFMA of 96 x 192 (L2 -> LDS bound)
     return launch_tile<12, 12, 3, 8>(A, M, K, W, bias_dev, out_scale, N, epilogue, c_dev, next_scale, Cp, g_n_cu, st);

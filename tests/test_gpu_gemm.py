@@ -60,9 +60,10 @@ def test_linear_f16x3_gelu_epilogue_and_scales():
 
 
 def test_linear_f16x3_tile_independent_bits():
-    """A single short query's rows (M <= 32: the 64 x 32 tile) are bit-identical to the same rows
-    inside a batch (M = 6144: the 96 x 192 / 192 x 192 tiles) -- the per-element k order does not
-    depend on the tile, so a query embeds the same alone or batched; with and without GELU."""
+    """A single short query's rows (M <= 32: the skinny K10s kernel, one or two row blocks) are
+    bit-identical to the same rows inside a batch (M = 6144: the 96 x 192 / 192 x 192 tiles) -- the
+    per-element k order does not depend on the kernel, so a query embeds the same alone or batched;
+    with and without GELU."""
     import torch
     from classmate_hip import engine
     for K, N in ((768, 2304), (768, 768), (3072, 768), (768, 3072)):
@@ -70,9 +71,15 @@ def test_linear_f16x3_tile_independent_bits():
         W = engine.F16x3Weight(w, b)
         for gelu in (False, True):
             big = engine.linear_f16x3(x, W, gelu=gelu)
-            for m in (1, 13, 32):
+            for m in (1, 13, 16, 17, 32, 33):
                 small = engine.linear_f16x3(x[:m].contiguous(), W, gelu=gelu)
                 assert torch.equal(small, big[:m]), (K, N, gelu, m)
+        # the fused FFN-up epilogue (GELU -> split planes for the next projection), same bits
+        bigp = engine.linear_f16x3(x, W, gelu=True, planes_out=2.0 ** -3)
+        for m in (1, 17, 32):
+            smallp = engine.linear_f16x3(x[:m].contiguous(), W, gelu=True, planes_out=2.0 ** -3)
+            for a, b in zip(smallp.halves(), bigp.halves()):
+                assert torch.equal(a, b[:m]), (K, N, m)
 
 
 def test_linear_f16x3_rejects_bad_shapes():
