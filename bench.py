@@ -101,6 +101,9 @@ def parse_args():
                                                   "fresh directory under $TMPDIR)")
     ap.add_argument("--e2e-ab-same-stream", type=int, default=0,
                     help="e2e mode: also time retrieve() with BM25 on the main stream (the pre-side-stream schedule)")
+    ap.add_argument("--e2e-ab-env", default="",
+                    help="e2e mode: ';'-separated env settings (NAME=V[,NAME=V]) under which retrieve_batch is "
+                         "timed again right after the main measurement, alternating with the default (A/B)")
     ap.add_argument("--cpu-baseline", type=int, default=1)
     ap.add_argument("--cpu-queries", type=int, default=128)
     ap.add_argument("--seed", type=int, default=1)
@@ -1008,6 +1011,35 @@ def run_e2e(args, rank, ws, dev):
         import pstats
         prof.disable()
         pstats.Stats(prof, stream=sys.stderr).sort_stats("cumulative").print_stats(40)
+    ab_env = {}
+    if args.e2e_ab_env:                  # A/B knobs read at launch time (engine env_knob), alternating
+        def timed_batches(tag):
+            for w in range(2):
+                retr.retrieve_batch(questions=qs[w * B:(w + 1) * B], top_k=K)
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            for st in range(args.steps):
+                o = (args.warmup + 1 + st) * B
+                retr.retrieve_batch(questions=qs[o:o + B], top_k=K)
+            torch.cuda.synchronize()
+            v = B * args.steps / (time.perf_counter() - t1)
+            ab_env.setdefault(tag, []).append(round(v, 1))
+            log(f"A/B retrieve_batch [{tag}]: {v:.1f} q/s")
+        sets = [x for x in args.e2e_ab_env.split(";") if x]
+        for _ in range(2):
+            timed_batches("default")
+            for spec in sets:
+                kv = dict(item.split("=", 1) for item in spec.split(","))
+                old_env = {k: os.environ.get(k) for k in kv}
+                os.environ.update(kv)
+                try:
+                    timed_batches(spec)
+                finally:
+                    for k, v in old_env.items():
+                        if v is None:
+                            os.environ.pop(k, None)
+                        else:
+                            os.environ[k] = v
     # single-query retrieve() latency: unfiltered, and with ask_question's filters
     # (rag/pipeline/rag.py:548-554: DocumentMetadata(...).to_dict(), None keys kept -- quirk Q4)
     none_keys = {"course": None, "unit": None, "author": None, "semester": None, "source_path": None,
@@ -1075,6 +1107,7 @@ def run_e2e(args, rank, ws, dev):
         "retrieve_latency_ms": lat["unfiltered"],
         "retrieve_latency_ms_by_filter": lat,
         "retrieve_latency_ms_bm25_same_stream": lat_same,
+        "retrieve_batch_env_ab_qps": ab_env or None,
         "construct_then_retrieve": construct,
         "retrieve_paths": paths,
         "results_returned": n_res, "setup_s": time.perf_counter() - t_setup,

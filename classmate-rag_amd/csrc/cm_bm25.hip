@@ -891,13 +891,14 @@ __global__ void __launch_bounds__(kMergeSmallThreads) bm25_merge_small_kernel(co
 // bm25_merge_kernel or, for k <= kMergeSmallK, its small-workgroup form (launch helper)
 int launch_bm25_merge(const uint64_t *cand_key, const uint32_t *cand_row, int nq, int nr, int k, double *score,
                       int64_t *row, hipStream_t st) {
-  if (k <= 8)
+  const bool small = env_knob("CM_BM25_MERGE_SMALL", true);   // 0: the 1024-thread kernel for every k (A/B)
+  if (small && k <= 8)
     hipLaunchKernelGGL(bm25_merge_small_kernel<8>, dim3(nq), dim3(kMergeSmallThreads), 0, st, cand_key, cand_row, nr, k,
                        score, row);
-  else if (k <= 10)
+  else if (small && k <= 10)
     hipLaunchKernelGGL(bm25_merge_small_kernel<10>, dim3(nq), dim3(kMergeSmallThreads), 0, st, cand_key, cand_row, nr,
                        k, score, row);
-  else if (k <= kMergeSmallK)
+  else if (small && k <= kMergeSmallK)
     hipLaunchKernelGGL(bm25_merge_small_kernel<kMergeSmallK>, dim3(nq), dim3(kMergeSmallThreads), 0, st, cand_key,
                        cand_row, nr, k, score, row);
   else

@@ -1,5 +1,6 @@
 // Shared host/device helpers for libclassmate_hip (gfx950 only).
 #pragma once
+#include <cstdlib>
 
 #include <hip/hip_runtime.h>
 
@@ -157,5 +158,12 @@ __device__ inline void f16x3_split1(float a, _Float16 &h, _Float16 &l) {
 
 constexpr uint64_t kEmptyKey = ~0ull;
 constexpr int kMaxTopK = 256;
+
+// A/B knob read at every launch (not cached: a benchmark flips it between measurements in one
+// process): unset -> dflt, "0" -> false, anything else -> true
+inline bool env_knob(const char *name, bool dflt) {
+  const char *e = getenv(name);
+  return e ? e[0] != '0' : dflt;
+}
 
 }  // namespace cm

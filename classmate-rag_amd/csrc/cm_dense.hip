@@ -1924,7 +1924,8 @@ int launch_coarse(cm_dense *h, const float *q_dev, int nq, int k, int kind, cons
     CM_HIP(hipGetLastError());
     h->timer.begin(st);
     // deferred search (!run_exact): the caller runs other work beside it -> the shared LDS footprint
-    if (run_exact)
+    // (CM_K1Q_SHARED_LDS=0: the full one, A/B)
+    if (run_exact || !env_knob("CM_K1Q_SHARED_LDS", true))
       hipLaunchKernelGGL(dense_q8_scan_kernel<false>, dim3(c.n_pass * c.n_wg), dim3(256), kQLds, st, h->Xq,
                          h->rmeta, h->live, allow, n_words, w.qq, w.qsc, nq, (const float *)w.seed, c.rows_per_wg,
                          c.rows_end, c.n_wg, w.keys, w.ups, w.cnt, (float *)nullptr);
