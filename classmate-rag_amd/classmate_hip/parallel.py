@@ -400,6 +400,10 @@ def fetch_pool_vectors(rows, q_lo: int, bq: int, gather_local, shard_starts, dim
     equal-split all-to-all of bq.P rows per peer delivers them; the receiver picks each entry from
     its owner's slice.  B.P.D.4 bytes per rank (G x the compacted exchange, 18.9 MB at B = 256,
     P = 24), in exchange for no data-dependent split sizes: the step stays stream-ordered on RCCL.
+    The volume grows with the global batch (B = 2048: ~150 MB each way per rank, ~1 ms of xGMI at
+    ~150 GB/s per link against the ~0.1 ms host round trip the compacted exchange's split sizes
+    cost), so the equal split pays up to B ~ 512 at P = 24; larger global batches should be issued
+    as several retrieval steps of <= 512 queries (the bench and the driver use B = 256 per rank).
     Returns (bq, P, D) fp32 (zeros for -1 pads)."""
     rank, ws = world()
     B, P = rows.shape

@@ -1763,18 +1763,25 @@ CoarseCfg coarse_config(const cm_dense *h, int nq, int kind) {
   c.qs = stream ? kSQ : kBQPass;
   c.n_pass = stream ? 1 : (int)ceil_div(nq, kBQPass);
   c.rows_end = round_up(std::max<int64_t>(h->size, 1), kStepRows);
-  int64_t groups = stream ? (int64_t)num_cus(h->dev) * 4 : std::max(1, num_cus(h->dev) / c.n_pass);
+  // row groups per pass: one pass fills the CUs; many passes (nq > 256) keep >= kMinGroups groups each
+  // (more workgroups than CUs) -- fewer, longer groups would overflow the 128-slot (group, query)
+  // buffers and send the whole batch to the exact pass
+  constexpr int64_t kMinGroups = 64;
+  int64_t groups = stream ? (int64_t)num_cus(h->dev) * 4
+                          : std::max<int64_t>(kMinGroups, std::max(1, num_cus(h->dev) / c.n_pass));
   if (c.paired) groups = std::max<int64_t>(1, groups / 2);
-  auto split = [&](int64_t rows_end, int64_t &per, int &n) {
+  auto split = [&](int64_t rows_end, int64_t g, int64_t &per, int &n) {
     const int64_t tiles = rows_end / kRRows;
-    per = ceil_div(tiles, std::min<int64_t>(groups, tiles)) * kRRows;
+    per = ceil_div(tiles, std::min<int64_t>(g, tiles)) * kRRows;
     n = (int)ceil_div(rows_end, per);
   };
-  split(c.rows_end, c.rows_per_wg, c.n_wg);
+  split(c.rows_end, groups, c.rows_per_wg, c.n_wg);
   // K1q's per-row bounds widen the candidate set: a denser seed sample keeps it near ~4k per query
   const int64_t frac = c.q8s ? k1qs_sample_frac() : c.q8 ? k1q_sample_frac() : c.rows_end >= (1 << 20) ? 64 : 16;
   c.rows_end_sample = round_up(std::max<int64_t>(c.rows_end / frac, 1), kRRows);
-  split(c.rows_end_sample, c.rows_per_wg_sample, c.n_wg_sample);
+  // the seed is the k-th smallest of the sample groups' minima: >= kMaxTopK groups whenever the sample
+  // has that many tiles, so no k <= kMaxTopK gets an infinite seed at any batch size
+  split(c.rows_end_sample, std::max<int64_t>(groups, kMaxTopK), c.rows_per_wg_sample, c.n_wg_sample);
   return c;
 }
 

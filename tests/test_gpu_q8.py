@@ -6,7 +6,7 @@ exact fp32 K1 on the same store."""
 import numpy as np
 import pytest
 
-from test_gpu_scale import check_dense, exact_topk, mixed_queries, unit_rows
+from test_gpu_scale import check_dense, exact_topk, exact_topk_dev, mixed_queries, unit_rows
 
 pytestmark = pytest.mark.gpu
 
@@ -65,6 +65,26 @@ def test_q8s_matches_exact_fp64(store, nq):
         idx.set_path(0)
     check_dense(d, r, o_d, o_r, 24)
     assert np.array_equal(r, r8) and np.array_equal(d, d8)
+
+
+def test_q8_large_batch_keeps_row_groups(store):
+    """A batch in the thousands (12 passes of 256 queries): every pass keeps >= 64 row groups and the
+    seed sample >= 256, so the certificate holds as at B = 256 (the groups shrank to
+    num_cus / n_pass, the seed went infinite below k sample groups and every (group, query) buffer
+    overflowed into the exact pass).  Same check for the f16 K1c."""
+    C, idx = store
+    nq = 3000
+    Q = mixed_queries(C, nq, seed=177)
+    o_d, o_r = exact_topk_dev(C, Q, 24 + 40, chunk=1 << 18)
+    try:
+        for kind in (Q8, COARSE):
+            idx.set_path(kind)
+            d, r = idx.search(Q, 24)
+            fb = idx.last_fallbacks()
+            check_dense(d, r, o_d, o_r, 24)
+            assert fb <= nq // 100, (kind, fb)
+    finally:
+        idx.set_path(0)
 
 
 def test_q8s_gaussian_k10_deletes_filters_and_device_entry(store):
