@@ -68,6 +68,9 @@ __device__ __forceinline__ h16x8 as_h8(i32x4 v) { return __builtin_bit_cast(h16x
 #ifndef K10S_DEPTH
 #define K10S_DEPTH 8           // k-steps in flight per wave of the skinny (M <= 32) kernel
 #endif
+#ifndef K10_S6
+#define K10_S6 0              // ring stages of the 96 x 192 tile (0: 4 at 12 waves, 3 at 8; A/B knob)
+#endif
 #ifndef K10_W6
 #define K10_W6 12              // waves per workgroup at the 96 x 192 tile (2 x 6: three per SIMD)
 #endif
@@ -607,7 +610,7 @@ extern "C" int cm_linear_f16x3(const void *a_planes, int64_t M, int32_t K, const
   if (t.bmb == 8 && t.bnb == 16)
     return launch_tile<8, 16, 3, 8>(A, M, K, W, bias_dev, out_scale, N, epilogue, c_dev, next_scale, Cp, g_n_cu, st);
   if (t.bmb == 6)
-    return launch_tile<6, 12, K10_W6 == 8 ? 3 : 4, K10_W6>(A, M, K, W, bias_dev, out_scale, N, epilogue, c_dev,
+    return launch_tile<6, 12, K10_S6 ? K10_S6 : (K10_W6 == 8 ? 3 : 4), K10_W6>(A, M, K, W, bias_dev, out_scale, N, epilogue, c_dev,
                                                            next_scale, Cp, g_n_cu, st);
   if (t.bmb == 8)
     return launch_tile<8, 8, 4, 8>(A, M, K, W, bias_dev, out_scale, N, epilogue, c_dev, next_scale, Cp, g_n_cu, st);
