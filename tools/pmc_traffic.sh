@@ -37,7 +37,7 @@ W=${ONLY:-dense_B256 dense_B16 bm25_B256}   # ONLY="bm25_B256 ..." -> a subset
 for n in $W; do
   case $n in
     dense_B256) run dense_B256 "dense_coarse_scan_kernelILi12ELi3ELb0" python3 tools/dense_probe.py --reps 3 --batch 256 --path 3 || exit 1 ;;
-    dense_q8_B256) run dense_q8_B256 "dense_q8_scan_kernel<false>" python3 tools/dense_probe.py --reps 3 --batch 256 --path 5 || exit 1 ;;
+    dense_q8_B256) run dense_q8_B256 "dense_q8_scan_kernel<false" python3 tools/dense_probe.py --reps 3 --batch 256 --path 5 || exit 1 ;;
     dense_q8s_B16) run dense_q8s_B16 "dense_q8_stream_kernel" python3 tools/dense_probe.py --reps 3 --batch 16 --k 10 || exit 1 ;;
     dense_B16) run dense_B16 "dense_stream_scan_kernelILi12ELi1ELb0" python3 tools/dense_probe.py --reps 3 --batch 16 || exit 1 ;;
     bm25_B256) run bm25_B256 "bm25_tail_kernel" python3 tools/bm25_probe.py --paths 2 --reps 3 || exit 1 ;;
