@@ -714,14 +714,17 @@ def dup_cluster_leg(args, dense, N, D, dev, q_step, P, normal_ms):
     torch.cuda.synchronize()
     ms = (time.perf_counter() - t0) / steps * 1e3
     fb = dense.workspace_fallbacks(B, P, ws_buf)
+    wide = dense.workspace_wide_reranks(B, P, ws_buf)
     rows = o[1][:8].cpu().numpy()
     on_cluster = float(np.isin(rows, np.concatenate([at, [base_row]])).mean())
-    r = {"ms_per_step": ms, "queries/s": B / ms * 1e3, "exact_reruns": fb, "cluster_rows": n_c,
+    r = {"ms_per_step": ms, "queries/s": B / ms * 1e3, "exact_reruns": fb, "wide_reranks": wide, "cluster_rows": n_c,
          "cluster_queries": 8, "normal_batch_ms": normal_ms, "ratio_to_normal": (ms / normal_ms) if normal_ms else None,
          "cluster_queries_top24_on_cluster": on_cluster,
          "note": "dense search (pool 24) of the step's 256 queries with 8 moved onto a planted cluster of 12k rows "
-                 "within 5e-4 of one row; the exact fp32 pass re-searches the failing queries"}
-    log(f"c4_dup_cluster_b256: {ms:.3f} ms per search ({fb} exact re-runs; normal batch "
+                 "within 5e-4 of one row; their int8 bands overflow the re-rank's LDS and the wide re-rank "
+                 "finishes them from the complete candidate buffers (exact fp64 distances of every band row); "
+                 "the exact fp32 pass re-searches what it cannot take"}
+    log(f"c4_dup_cluster_b256: {ms:.3f} ms per search ({wide} wide re-ranks, {fb} exact re-runs; normal batch "
         f"{normal_ms if normal_ms is None else round(normal_ms, 3)} ms)")
     return r
 

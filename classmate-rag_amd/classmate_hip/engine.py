@@ -190,6 +190,11 @@ class DenseIndex:
         """K1c/K1s queries re-run by the exact fp32 pass in the last host search()."""
         return int(L.fn["cm_dense_last_fallbacks"](self._h))
 
+    def last_wide_reranks(self) -> int:
+        """K1q/K1q-s queries whose band overflowed the re-rank's LDS and that the wide re-rank
+        finished from the complete candidate buffers (no exact scan) in the last host search()."""
+        return int(L.fn["cm_dense_last_wide_reranks"](self._h))
+
     def timing(self, enable: bool = True):
         """Record HIP events around every search's scan kernel (see timing_drain)."""
         L.check(L.fn["cm_dense_timing"](self._h, int(bool(enable))), "cm_dense_timing")
@@ -205,6 +210,10 @@ class DenseIndex:
     def workspace_fallbacks(self, nq: int, k: int, workspace) -> int:
         """K1c/K1s queries re-run by the exact fp32 pass in the last search_dev() that used `workspace`."""
         return int(L.fn["cm_dense_workspace_fallbacks"](self._h, int(nq), int(k), L.ptr(workspace)))
+
+    def workspace_wide_reranks(self, nq: int, k: int, workspace) -> int:
+        """last_wide_reranks for the device search that last used ``workspace`` (synchronous read)."""
+        return int(L.fn["cm_dense_workspace_wide_reranks"](self._h, int(nq), int(k), L.ptr(workspace)))
 
     def workspace_bytes(self, nq: int, k: int) -> int:
         n = int(L.fn["cm_dense_search_workspace"](self._h, int(nq), int(k)))

@@ -1353,6 +1353,7 @@ struct cm_dense {
   float *rnorm = nullptr;                  // device {max ||Xh_r||, max ||xn_r - Xh_r||, max ||s_r q8_r||, 0}
   int path = 0;                            // cm_dense_set_path (0 = automatic)
   int32_t last_fallbacks = -1;             // K1c queries re-run exactly by the last host search
+  int32_t last_wide = -1;                  // K1q queries finished by the wide re-rank in the last host search
   KernelTimer timer;                       // scan-kernel events (cm_dense_timing)
   uint32_t *live = nullptr;
   hipStream_t stream = nullptr;
@@ -1795,8 +1796,12 @@ struct CoarseWs {
   float *ups;         // K1q: d~ + E_r beside every candidate key [pass][group][qs][kQCap]
   float *mins;        // sample minima [pass][sample group][qs]
   float *seed;        // per-query insertion bound from the sample
-  int32_t *fb_mask;   // queries sent to the exact K1 pass
+  int32_t *fb_mask;   // queries sent to the exact K1 pass (K1q: 2 = the wide re-rank first)
   int32_t *fb_count;
+  uint32_t *fb_bound; // K1q: kth_up of a query sent to the wide re-rank
+  int32_t *wide_ctr;  // K1q wide re-rank: [0] slot allocator, [1] queries it finished
+  uint32_t *wide_rows;   // [kWideSlots][kWideCap]
+  uint64_t *wide_keys;   // [kWideSlots][kWideCap]
   DenseWs k1;         // the exact K1 pass's own workspace (used only for fb_mask queries)
   size_t total;
 };
@@ -1824,6 +1829,12 @@ CoarseWs coarse_ws_layout(const cm_dense *h, const CoarseCfg &c, int nq, int k, 
   w.seed = reinterpret_cast<float *>(take(nq_pad * 4));
   w.fb_mask = reinterpret_cast<int32_t *>(take(nq_pad * 4));
   w.fb_count = reinterpret_cast<int32_t *>(take(4));
+  if (c.q8) {
+    w.fb_bound = reinterpret_cast<uint32_t *>(take(nq_pad * 4));
+    w.wide_ctr = reinterpret_cast<int32_t *>(take(8));
+    w.wide_rows = reinterpret_cast<uint32_t *>(take((int64_t)kWideSlots * kWideCap * 4));
+    w.wide_keys = reinterpret_cast<uint64_t *>(take((int64_t)kWideSlots * kWideCap * 8));
+  }
   const DenseCfg kc = dense_config(h, nq, k, true);
   w.k1 = dense_ws_layout(h, kc, nq, k, p ? p + off : nullptr);
   off += w.k1.total;
@@ -1888,6 +1899,7 @@ int launch_coarse(cm_dense *h, const float *q_dev, int nq, int k, int kind, cons
                      w.qnorm);
   CM_HIP(hipGetLastError());
   CM_HIP(hipMemsetAsync(w.fb_count, 0, 4, st));
+  if (c.q8) CM_HIP(hipMemsetAsync(w.wide_ctr, 0, 8, st));
   if (c.q8) {
     // K1q: int8 queries -> seed from a row sample -> scan -> certified re-rank (int8 band -> f16 band
     // -> fp64)
@@ -1945,7 +1957,14 @@ int launch_coarse(cm_dense *h, const float *q_dev, int nq, int k, int kind, cons
     }
     hipLaunchKernelGGL(dense_rerank_q8_kernel, dim3(nq), dim3(256), kQRerankLds, st, w.keys, w.ups, w.cnt, c.n_wg, c.qs, k,
                        nq, h->C, h->ld, h->dim, q_dev, w.qsc, h->Xh, w.qh, w.qnorm, h->rnorm, dist_dev, row_dev,
-                       w.fb_mask, w.fb_count);
+                       w.fb_mask, w.fb_count, w.fb_bound);
+    CM_HIP(hipGetLastError());
+    // band overflow with complete candidate buffers: the wide re-rank (gated; ~5 us when none failed;
+    // CM_K1Q_WIDE=0: the exact scan takes every failing query, A/B)
+    if (env_knob("CM_K1Q_WIDE", true))
+      hipLaunchKernelGGL(dense_rerank_wide_kernel, dim3(nq), dim3(kWideThreads), 0, st, w.keys, w.cnt, c.n_wg, c.qs, k,
+                       nq, h->C, h->ld, h->dim, q_dev, w.qsc, dist_dev, row_dev, w.fb_mask, w.fb_count, w.fb_bound,
+                       w.wide_ctr, w.wide_rows, w.wide_keys);
     CM_HIP(hipGetLastError());
   } else {
   const bool d768 = h->ld == 768;
@@ -2078,6 +2097,7 @@ int dense_search_full(cm_dense *h, const float *q, int nq, int k, const uint32_t
     CM_HIP(hipStreamSynchronize(h->stream));
   }
   h->last_fallbacks = 0;
+  h->last_wide = 0;
   return CM_OK;
 }
 
@@ -2302,6 +2322,19 @@ int32_t cm_dense_workspace_fallbacks(cm_dense *h, int32_t nq, int32_t k, const v
 
 int32_t cm_dense_last_fallbacks(cm_dense *h) { return h ? h->last_fallbacks : -1; }
 
+int32_t cm_dense_workspace_wide_reranks(cm_dense *h, int32_t nq, int32_t k, const void *workspace_dev) {
+  if (!h || !workspace_dev || nq <= 0 || k <= 0 || k > kMaxTopK) return -1;
+  const int kind = dense_kind(h, nq, k);
+  if (kind != CM_DENSE_Q8 && kind != CM_DENSE_Q8S) return 0;
+  DeviceGuard dg(h->dev);
+  const CoarseWs w = coarse_ws_layout(h, coarse_config(h, nq, kind), nq, k, const_cast<void *>(workspace_dev));
+  int32_t c[2] = {-1, -1};
+  if (hipMemcpy(c, w.wide_ctr, 8, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+  return c[1];
+}
+
+int32_t cm_dense_last_wide_reranks(cm_dense *h) { return h ? h->last_wide : -1; }
+
 int cm_dense_timing(cm_dense *h, int32_t enable) {
   if (!h) CM_FAIL(CM_EINVAL, "null handle");
   DeviceGuard dg(h->dev);
@@ -2451,10 +2484,12 @@ int cm_dense_search(cm_dense *h, const float *q, int32_t nq, int32_t k, const ui
   CM_HIP(hipMemcpyAsync(out_row, d_row, (size_t)nq * k * 8, hipMemcpyDeviceToHost, h->stream));
   if (out_vec) CM_HIP(hipMemcpyAsync(out_vec, d_vec, vbytes, hipMemcpyDeviceToHost, h->stream));
   h->last_fallbacks = 0;
+  h->last_wide = 0;
   const int kind = dense_kind(h, nq, k);
   if (kind != CM_DENSE_F32) {
     const CoarseWs w = coarse_ws_layout(h, coarse_config(h, nq, kind), nq, k, h->ws.ptr);
     CM_HIP(hipMemcpyAsync(&h->last_fallbacks, w.fb_count, 4, hipMemcpyDeviceToHost, h->stream));
+    if (w.wide_ctr) CM_HIP(hipMemcpyAsync(&h->last_wide, w.wide_ctr + 1, 4, hipMemcpyDeviceToHost, h->stream));
   }
   CM_HIP(hipStreamSynchronize(h->stream));
   return CM_OK;

@@ -133,6 +133,13 @@ int cm_dense_set_path(cm_dense *h, int32_t kind);
 int32_t cm_dense_workspace_fallbacks(cm_dense *h, int32_t nq, int32_t k, const void *workspace_dev);
 /* same, for the last host-array cm_dense_search on this handle. */
 int32_t cm_dense_last_fallbacks(cm_dense *h);
+/* K1q/K1q-s: queries of that search whose band overflowed the re-rank's LDS
+ * (near-duplicate clusters) and that the wide re-rank finished exactly from
+ * the complete candidate buffers instead of the exact scan of every row
+ * (ChromaVectorStore.query's result for them is unchanged,
+ * rag/retrieval/vector_chroma.py:204-253); 0 for other paths, -1 on error. */
+int32_t cm_dense_workspace_wide_reranks(cm_dense *h, int32_t nq, int32_t k, const void *workspace_dev);
+int32_t cm_dense_last_wide_reranks(cm_dense *h);
 /* kernel timing (bench roofline): while enabled, every search records HIP
  * events on its launch stream around its scan kernel (K1 / K1c / K1s coarse
  * scan); _drain synchronises on them, writes up to cap elapsed ms values and

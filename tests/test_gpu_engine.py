@@ -140,7 +140,8 @@ def test_dense_batched_split_paths(eng, n, nq, k, dim, path):
 def test_dense_coarse_certificate(eng, path):
     """K1c / K1s / K1q / K1q-s: on well-separated data every query is certified (no exact re-run);
     on a cluster of near-duplicates wider than the coarse lists the certificate fails and the
-    exact fp32 K1 pass takes over for those queries -- results stay within tolerance."""
+    exact fp32 K1 pass takes over for those queries (K1q / K1q-s: the wide re-rank, from the
+    complete candidate buffers) -- results stay within tolerance."""
     rng = np.random.default_rng(77)
     n, dim = 30000, 768
     emb = rng.standard_normal((n, dim)).astype(np.float32)
@@ -165,7 +166,9 @@ def test_dense_coarse_certificate(eng, path):
     q2 = np.concatenate([q[:8], base + 0.01 * rng.standard_normal((8, dim)).astype(np.float32)])
     dist, rows = idx.search(q2, 24)
     _check_dense(dist, rows, emb2, q2, 24)
-    assert idx.last_fallbacks() >= 8
+    # (the duplicates are contiguous rows, so they overflow the int8 kinds' 128-slot (group, query)
+    # buffers too: an incomplete candidate set, which the wide re-rank cannot finish -> the exact pass)
+    assert idx.last_fallbacks() + max(idx.last_wide_reranks(), 0) >= 8
     assert (rows[8:] >= n).all()
 
 

@@ -195,8 +195,9 @@ def test_q8_device_search_and_workspace(store):
 def test_q8_band_overflow_takes_exact_fallback():
     """Near-duplicate chunks (real corpora hold them; the synthetic bench never does): 12 000 rows
     within 5e-4 of one base row put far more rows inside the int8 certificate than its 8192-row
-    band holds, so the re-rank hands those queries to the exact fp32 K1 pass (fb_mask) and the
-    merge writes only their rows.  Every list -- cluster and ordinary queries in one batch -- must
+    band holds, so the re-rank hands those queries to the wide re-rank (every band row's exact fp64
+    distance from the complete candidate buffers; round 5) -- or, with it off, to the exact fp32 K1
+    pass (fb_mask), whose merge writes only their rows.  Every list -- cluster and ordinary queries in one batch -- must
     still equal the exact fp64 oracle, on K1q and on K1c."""
     from classmate_hip import engine
     rng = np.random.default_rng(91)
@@ -224,15 +225,27 @@ def test_q8_band_overflow_takes_exact_fallback():
             d, r = idx.search(Q, k)
             fb = idx.last_fallbacks()
             check_dense(d, r, o_d, o_r, k)
-            if kind == Q8:
-                assert 1 <= fb <= n_near, fb             # only the cluster queries re-run exactly
+            if kind == Q8:   # only the cluster queries leave the LDS re-rank; the wide re-rank finishes them
+                wide = idx.last_wide_reranks()
+                assert 1 <= fb + wide <= n_near and wide >= 1, (fb, wide)
         # the small-batch stream on the cluster queries + 8 ordinary ones: same certificate, same fallback
         idx.set_path(0)
         assert idx.search_kind(16, k) == Q8S
         d, r = idx.search(Q[:16], k)
-        fb = idx.last_fallbacks()
+        fb, wide = idx.last_fallbacks(), idx.last_wide_reranks()
         check_dense(d, r, o_d[:16], o_r[:16], k)
-        assert 1 <= fb <= n_near, fb
+        assert 1 <= fb + wide <= n_near and wide >= 1, (fb, wide)
+        # the exact scan as the only fallback (CM_K1Q_WIDE=0) gives the same lists
+        import os
+        os.environ["CM_K1Q_WIDE"] = "0"
+        try:
+            idx.set_path(Q8)
+            d0, r0 = idx.search(Q, k)
+            assert idx.last_wide_reranks() == 0 and 1 <= idx.last_fallbacks() <= n_near
+            check_dense(d0, r0, o_d, o_r, k)
+        finally:
+            del os.environ["CM_K1Q_WIDE"]
+            idx.set_path(0)
         # the deferred device entry: scan + re-rank, then the gated exact pass (what the bench step and
         # retrieve() enqueue behind the BM25 join) == the one-call search
         import torch
