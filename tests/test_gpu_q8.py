@@ -260,3 +260,57 @@ def test_q8_band_overflow_takes_exact_fallback():
     finally:
         idx.set_path(0)
         idx.close()
+
+
+def test_q8_contiguous_cluster_rescans_overflowed_groups():
+    """A contiguous run of near-duplicates (a re-ingested document): the queries on it overflow their
+    128-slot (group, query) buffers -- an incomplete candidate set -- so the wide re-rank re-scans the
+    overflowed groups' live and allowed rows on the f16 plane (rows with d_h - Eh <= kth_up) before the
+    exact fp64 stage, instead of the exact scan of every row.  K1q and K1q-s, then deletes + an allow
+    filter; every list equal to the fp64 oracle."""
+    from classmate_hip import engine
+    rng = np.random.default_rng(193)
+    C = unit_rows(200_000, 768, seed=190)
+    base = C[5].astype(np.float64)
+    at = np.arange(100_000, 103_000)
+    n_c = at.size
+    d_c = rng.permutation(np.linspace(1e-5, 5e-4, n_c))
+    u = rng.standard_normal((n_c, 768))
+    u -= np.outer(u @ base, base)
+    u /= np.linalg.norm(u, axis=1, keepdims=True)
+    t = np.sqrt(2.0 * d_c - d_c ** 2)
+    C[at] = (np.sqrt(1.0 - t ** 2)[:, None] * base + t[:, None] * u).astype(np.float32)
+    Q = mixed_queries(C, 64, seed=194)
+    Q[:8] = (base + 1e-4 * rng.standard_normal((8, 768)) / np.sqrt(768)).astype(np.float32)
+    k = 24
+    o_d, o_r = exact_topk(C, Q, k + 600)
+    idx = engine.DenseIndex(768, capacity=C.shape[0])
+    try:
+        idx.upsert(C, np.arange(C.shape[0], dtype=np.int64))
+        idx.set_path(Q8)
+        d, r = idx.search(Q, k)
+        check_dense(d, r, o_d, o_r, k)
+        wide, fb = idx.last_wide_reranks(), idx.last_fallbacks()
+        assert wide >= 8 and fb == 0, (wide, fb)          # the 8 cluster queries (+ any mixed query near it)
+        idx.set_path(Q8S)
+        d, r = idx.search(Q[:16], k)
+        check_dense(d, r, o_d[:16], o_r[:16], k)
+        assert idx.last_wide_reranks() + idx.last_fallbacks() >= 8
+        # deletes inside the cluster + an allow bitmap: the re-scan honours both
+        drop = at[::5]
+        idx.delete(drop)
+        allow = np.ones(C.shape[0], bool)
+        allow[at[1::7]] = False
+        allow[::11] = False
+        words = np.packbits(allow, bitorder="little").view(np.uint32)
+        keep = allow.copy()
+        keep[drop] = False
+        rows = np.nonzero(keep)[0]
+        o_d2, o_r2 = exact_topk(C[rows], Q, k + 600)
+        idx.set_path(Q8)
+        d2, r2 = idx.search(Q, k, words)
+        check_dense(d2, r2, o_d2, rows[o_r2], k)
+        assert not np.isin(r2, drop).any() and allow[r2[r2 >= 0]].all()
+    finally:
+        idx.set_path(0)
+        idx.close()
