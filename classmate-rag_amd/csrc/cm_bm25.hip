@@ -1405,6 +1405,13 @@ int bm25_launch_core(cm_bm25 *h, const int32_t *q_terms_dev, const int32_t *q_of
     CM_HIP(hipGetLastError());
   }
   CM_HIP(hipMemsetAsync(w.thr, 0xff, (size_t)nq * 8, st));  // no threshold yet
+  if (prune && nq > 0 && env_knob("CM_BM25_TSEED", true)) {   // K2s: a seeded T for the tail pass
+    hipLaunchKernelGGL(bm25_tseed_kernel, dim3((unsigned)ceil_div(nq, 4)), dim3(256), 0, st, nq, k, w.qd_code,
+                       w.qd_idf, w.qd_len, w.qd_term, h->term_off.as<int64_t>(), h->post_doc.as<int32_t>(),
+                       h->post_tf.as<uint16_t>(), h->headtf.as<uint8_t>(), h->npad, h->dl.as<int32_t>(),
+                       h->live.as<uint32_t>(), allow_dev, avgdl, w.thr);
+    CM_HIP(hipGetLastError());
+  }
   hipLaunchKernelGGL(bm25_lut_kernel, dim3(kLutW * kLutTF / 256), dim3(256), 0, st, (const double *)avgdl, h->lut_dmin,
                      w.lut);
   CM_HIP(hipGetLastError());
@@ -1431,7 +1438,9 @@ int bm25_launch_core(cm_bm25 *h, const int32_t *q_terms_dev, const int32_t *q_of
                        w.qd_term, w.qd_idf, w.qd_tb, w.qd_len,
                        (h->nhead && h->maxr_avgdl > 0.0) ? h->blk_maxr.as<uint8_t>() : (const uint8_t *)nullptr,
                        h->nhead ? h->blk_maxtf.as<uint8_t>() : (const uint8_t *)nullptr, h->blk_mindl.as<int32_t>(),
-                       h->maxr_avgdl, (int64_t)nr * (kRange / 64), bm25_debug_flags());
+                       h->maxr_avgdl, (int64_t)nr * (kRange / 64),
+                       h->nhead ? h->head_maxtf.as<uint8_t>() : (const uint8_t *)nullptr, h->range_mindl.as<int32_t>(),
+                       bm25_debug_flags());
     h->timer.end(st);
     CM_HIP(hipGetLastError());
     if ((rc = launch_bm25_merge(w.cand_key, w.cand_row, nq, nr, k, score_dev, row_dev, st))) return rc;
