@@ -1964,7 +1964,7 @@ int launch_coarse(cm_dense *h, const float *q_dev, int nq, int k, int kind, cons
     if (env_knob("CM_K1Q_WIDE", true))
       hipLaunchKernelGGL(dense_rerank_wide_kernel, dim3(nq), dim3(kWideThreads), 0, st, w.keys, w.cnt, c.n_wg, c.qs, k,
                          nq, h->C, h->ld, h->dim, q_dev, w.qsc, h->Xh, w.qh, w.qnorm, h->rnorm, h->live, allow,
-                         c.rows_per_wg, c.rows_end, dist_dev, row_dev, w.fb_mask, w.fb_count, w.fb_bound, w.wide_ctr,
+                         n_words, c.rows_per_wg, c.rows_end, dist_dev, row_dev, w.fb_mask, w.fb_count, w.fb_bound, w.wide_ctr,
                          w.wide_rows, w.wide_keys);
     CM_HIP(hipGetLastError());
   } else {
