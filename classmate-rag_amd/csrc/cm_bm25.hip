@@ -1406,7 +1406,7 @@ int bm25_launch_core(cm_bm25 *h, const int32_t *q_terms_dev, const int32_t *q_of
   }
   CM_HIP(hipMemsetAsync(w.thr, 0xff, (size_t)nq * 8, st));  // no threshold yet
   if (prune && nq > 0 && env_knob("CM_BM25_TSEED", true)) {   // K2s: a seeded T for the tail pass
-    hipLaunchKernelGGL(bm25_tseed_kernel, dim3((unsigned)ceil_div(nq, 4)), dim3(256), 0, st, nq, k, w.qd_code,
+    hipLaunchKernelGGL(bm25_tseed_kernel, dim3((unsigned)nq), dim3(kSeedThreads), 0, st, nq, k, w.qd_code,
                        w.qd_idf, w.qd_len, w.qd_term, h->term_off.as<int64_t>(), h->post_doc.as<int32_t>(),
                        h->post_tf.as<uint16_t>(), h->headtf.as<uint8_t>(), h->npad, h->dl.as<int32_t>(),
                        h->live.as<uint32_t>(), allow_dev, avgdl, w.thr);
