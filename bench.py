@@ -86,6 +86,10 @@ def parse_args():
                     help="launch BM25 beside the E5 encode (the round-3 schedule); default: after the encode, "
                          "beside the dense search, whose seed / re-rank / fusion kernels leave CUs to it "
                          "(31.2k vs 30.5k q/s with K1q, profiles/r04b_sched_ab.txt)")
+    ap.add_argument("--bm25-gate", type=int, default=1,
+                    help="with BM25 after the encode: its query preparation (descriptors, postings bounds, seeded "
+                         "threshold) starts beside the encode and only the scoring kernels wait for it "
+                         "(cm_bm25_search_dev_gated); 0 = the whole search after the encode")
     ap.add_argument("--pipeline", type=int, default=0,
                     help="1 (2: on a high-priority stream) = encode batch i+1 (its own hipGraph + output buffer, its own stream) while batch i is "
                          "searched; every step still runs one whole encode and one whole search")
@@ -285,13 +289,13 @@ def main():
         side = engine.cu_masked_stream(local, list(cus))
         log(f"BM25 stream on {len(list(cus))} of {n_cu} CUs ({args.bm25_cus})")
 
-    def run_bm25(e):
+    def run_bm25(e, gate=None):
         # BM25 needs only the query term ids: it runs on its own stream, overlapping the E5
         # encode and the dense search (joined before fusion)
         with torch.cuda.stream(side):
             if e:
                 e["b0"].record()
-            out = bm25.search_dev(q_terms, q_off, K, out=bout, workspace=bws)
+            out = bm25.search_dev(q_terms, q_off, K, out=bout, workspace=bws, gate=gate)
             if e:
                 e["b1"].record()
         return out
@@ -344,14 +348,20 @@ def main():
         return parallel.all_gather_into(qfull, q_local)
 
     last_lists = {}      # the last step's merged lists (recall diagnostics)
+    gate_ev = torch.cuda.Event()
 
     def step(record=False):
         e = {n: torch.cuda.Event(enable_timing=True) for n in ("e0", "e1", "d0", "d1", "b0", "b1")} if record else None
+        gated = bm25 is not None and args.bm25_after_e5 and args.bm25_gate and side is not main
+        if bm25 is not None and (not args.bm25_after_e5 or gated):
+            side.wait_stream(main)          # previous step's fusion has read bout (not this encode)
         if bm25 is not None and not args.bm25_after_e5:
-            side.wait_stream(main)          # previous step's fusion has read bout
             bs, br = run_bm25(e)
         q = encode(e) if use_e5 else qfix
-        if bm25 is not None and args.bm25_after_e5:
+        if gated:                           # preparation beside the encode, scoring after it
+            gate_ev.record(main)
+            bs, br = run_bm25(e, gate_ev)
+        elif bm25 is not None and args.bm25_after_e5:
             side.wait_stream(main)
             bs, br = run_bm25(e)
         if record:

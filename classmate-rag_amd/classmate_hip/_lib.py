@@ -103,6 +103,7 @@ SIGNATURES = {
     "cm_bm25_search": (c_int, c_vp, c_vp, c_vp, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp),
     "cm_bm25_search_workspace": (c_i64, c_vp, c_i32, c_i32, c_i32),
     "cm_bm25_search_dev": (c_int, c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp, c_i64, c_vp),
+    "cm_bm25_search_dev_gated": (c_int, c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp),
     "cm_bm25_prepare_filtered": (c_int, c_vp, c_i64),
     "cm_bm25_filter_stats_dev": (c_int, c_vp, c_vp, c_vp, c_i32, c_vp, c_vp, c_vp),
     "cm_bm25_filter_term_stats_dev": (c_int, c_vp, c_vp, c_vp, c_vp, c_vp),

@@ -399,8 +399,10 @@ class BM25Index:
             raise ValueError("bad BM25 workspace request")
         return n
 
-    def search_dev(self, q_terms, q_off, k: int, out=None, workspace=None):
-        """Unfiltered device search: q_terms int32 (T,), q_off int32 (nq+1,) device tensors."""
+    def search_dev(self, q_terms, q_off, k: int, out=None, workspace=None, gate=None):
+        """Unfiltered device search: q_terms int32 (T,), q_off int32 (nq+1,) device tensors.  ``gate``
+        (a recorded torch.cuda.Event): the scoring kernels wait for it, the query preparation does not
+        (cm_bm25_search_dev_gated)."""
         nq = q_off.numel() - 1
         total = q_terms.numel()
         wsb = self.workspace_bytes(nq, total, k)
@@ -411,9 +413,10 @@ class BM25Index:
         if out is None:
             out = (torch.empty((nq, k), dtype=torch.float64, device=q_terms.device),
                    torch.empty((nq, k), dtype=torch.int64, device=q_terms.device))
-        L.check(L.fn["cm_bm25_search_dev"](self._h, L.ptr(q_terms), L.ptr(q_off), nq, total, int(k), L.ptr(out[0]),
-                                           L.ptr(out[1]), L.ptr(workspace), int(workspace.numel()),
-                                           _stream(self.device)), "cm_bm25_search_dev")
+        L.check(L.fn["cm_bm25_search_dev_gated"](self._h, L.ptr(q_terms), L.ptr(q_off), nq, total, int(k),
+                                                 L.ptr(out[0]), L.ptr(out[1]), L.ptr(workspace), int(workspace.numel()),
+                                                 _stream(self.device), gate.cuda_event if gate is not None else None),
+                "cm_bm25_search_dev_gated")
         return out
 
 

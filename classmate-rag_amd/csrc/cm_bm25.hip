@@ -1383,7 +1383,8 @@ BmWs bm_ws_layout(const cm_bm25 *h, int nq, int total_terms, int k, void *base) 
 #endif
 // Launch K2 + merge given q_idf and *avgdl already in the workspace.
 int bm25_launch_core(cm_bm25 *h, const int32_t *q_terms_dev, const int32_t *q_off_dev, int nq, int total_terms, int k,
-                     const uint32_t *allow_dev, const BmWs &w, double *score_dev, int64_t *row_dev, hipStream_t st) {
+                     const uint32_t *allow_dev, const BmWs &w, double *score_dev, int64_t *row_dev, hipStream_t st,
+                     hipEvent_t gate = nullptr) {
   int rc;
   const double *avgdl = w.avgdl;
   const int nr = (int)std::max<int64_t>(1, ceil_div(h->ndocs, kRange));
@@ -1426,6 +1427,9 @@ int bm25_launch_core(cm_bm25 *h, const int32_t *q_terms_dev, const int32_t *q_of
   const int64_t nblk_a = ceil_div(nqg * ceil_div(nr, rpw_a), kBmThreads / 64);
   if (nblk > INT32_MAX || nblk_a > INT32_MAX) CM_FAIL(CM_EUNSUPPORTED, "BM25 batch too large");
   const int32_t *head_id = h->nhead ? h->head_id.as<int32_t>() : (const int32_t *)nullptr;
+  // the gate: the preparation above (descriptors, postings bounds, seeded threshold) overlaps the
+  // caller's producer kernels; the scoring kernels wait for it (cm_bm25_search_dev_gated)
+  if (gate) CM_HIP(hipStreamWaitEvent(st, gate, 0));
   h->timer.begin(st);  // the search's dominant scoring kernel: K2a (pruned) or K2 (full)
   if (prune) {
     // K2a: exact scores of the tail candidates -> per-range lists; merged lists give each
@@ -1956,6 +1960,13 @@ int64_t cm_bm25_search_workspace(cm_bm25 *h, int32_t nq, int32_t total_terms, in
 int cm_bm25_search_dev(cm_bm25 *h, const int32_t *q_terms_dev, const int32_t *q_off_dev, int32_t nq,
                        int32_t total_terms, int32_t k, double *score_dev, int64_t *row_dev, void *workspace_dev,
                        int64_t workspace_bytes, void *stream) {
+  return cm_bm25_search_dev_gated(h, q_terms_dev, q_off_dev, nq, total_terms, k, score_dev, row_dev, workspace_dev,
+                                  workspace_bytes, stream, nullptr);
+}
+
+int cm_bm25_search_dev_gated(cm_bm25 *h, const int32_t *q_terms_dev, const int32_t *q_off_dev, int32_t nq,
+                             int32_t total_terms, int32_t k, double *score_dev, int64_t *row_dev, void *workspace_dev,
+                             int64_t workspace_bytes, void *stream, void *gate_event) {
   if (!h) CM_FAIL(CM_EINVAL, "null handle");
   if (nq <= 0) return CM_OK;
   if (k <= 0 || k > kMaxTopK) CM_FAIL(CM_EINVAL, "k must be in [1, " + std::to_string(kMaxTopK) + "]");
@@ -1972,7 +1983,8 @@ int cm_bm25_search_dev(cm_bm25 *h, const int32_t *q_terms_dev, const int32_t *q_
   }
   hipLaunchKernelGGL(bm25_set_f64_kernel, dim3(1), dim3(64), 0, st, h->avgdl, w.avgdl);
   CM_HIP(hipGetLastError());
-  return bm25_launch_core(h, q_terms_dev, q_off_dev, nq, total_terms, k, nullptr, w, score_dev, row_dev, st);
+  return bm25_launch_core(h, q_terms_dev, q_off_dev, nq, total_terms, k, nullptr, w, score_dev, row_dev, st,
+                          (hipEvent_t)gate_event);
 }
 
 int cm_bm25_search(cm_bm25 *h, const int32_t *q_terms, const int32_t *q_off, int32_t nq, int32_t k,

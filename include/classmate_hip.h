@@ -247,6 +247,14 @@ int64_t cm_bm25_search_workspace(cm_bm25 *h, int32_t nq, int32_t total_terms, in
 int cm_bm25_search_dev(cm_bm25 *h, const int32_t *q_terms_dev, const int32_t *q_off_dev, int32_t nq,
                        int32_t total_terms, int32_t k, double *score_dev, int64_t *row_dev,
                        void *workspace_dev, int64_t workspace_bytes, void *stream);
+/* the same search with its scoring kernels behind gate_event (a hipEvent_t, NULL = none): the
+ * query preparation (term descriptors, postings bounds, the seeded threshold) runs at once, beside
+ * the caller's producer work (HybridRetriever.retrieve encodes the query first,
+ * rag/retrieval/fusion.py:124-125), the tail pass and everything after it wait for the event.
+ * Results are identical. */
+int cm_bm25_search_dev_gated(cm_bm25 *h, const int32_t *q_terms_dev, const int32_t *q_off_dev, int32_t nq,
+                             int32_t total_terms, int32_t k, double *score_dev, int64_t *row_dev,
+                             void *workspace_dev, int64_t workspace_bytes, void *stream, void *gate_event);
 
 /* Filtered search on the device (quirk Q2: rank_bm25 statistics over the
  * candidate set, rag/retrieval/bm25.py:184-191), graph-capturable.
