@@ -342,7 +342,8 @@ class BM25Store:
     # ---------- query ----------
     def _query_ids(self, query: str) -> List[int]:
         q_lang = detect_lang_tag(query)
-        return [self._vocab.get(t, -1) for t in _tokenize(query, lang_hint=q_lang)]
+        get = self._vocab.get          # (one proxy-property read, not one per token)
+        return [get(t, -1) for t in _tokenize(query, lang_hint=q_lang)]
 
     def search(self, *, query: str, where: Optional[Mapping[str, Any]] = None, top_k: int = 8) -> List[Dict[str, Any]]:
         """bm25.py:175-212 on the GPU."""

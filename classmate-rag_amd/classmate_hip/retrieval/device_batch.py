@@ -277,6 +277,8 @@ def retrieve_batch(retr, questions: Sequence[str], top_k: int,
     nvr, vs2bm = km.nvr, km.vs2bm
     vids, vdocs, vmetas = vs._ids, vs._docs, vs._meta.metas
     bids, entries = bm._id_list, bm._entries
+    dget = dict.__getitem__            # the catalog's stored value without its Python __getitem__ frame;
+                                       # a pending (int: not yet parsed) record goes through entries[...]
     for i in range(nq):
         m = len(range(on[i])[:top_k])                    # Python slice of the full order
         res = []
@@ -287,13 +289,19 @@ def retrieve_batch(retr, questions: Sequence[str], top_k: int,
                 _id = vids[kk]
                 doc, meta = vdocs[kk], vmetas[kk] or {}
                 if fl & 2 and (not doc or not meta):
-                    e = entries[bids[int(vs2bm[kk])]]
+                    key = bids[int(vs2bm[kk])]
+                    e = dget(entries, key)
+                    if type(e) is int:
+                        e = entries[key]
                     if not doc and e.text:
                         doc = e.text
                     if not meta and e.metadata:
                         meta = e.metadata
             else:                                        # BM25-only: the BM25 entry's fields (fusion.py:146-151)
-                e = entries[bids[int(vs2bm[kk])] if kk < nvr else bids[kk - nvr]]
+                key = bids[int(vs2bm[kk])] if kk < nvr else bids[kk - nvr]
+                e = dget(entries, key)
+                if type(e) is int:
+                    e = entries[key]
                 _id, doc, meta = e.id, e.text or None, e.metadata or {}
             res.append({"id": _id, "document": doc, "metadata": meta,
                         "scores": {"vector_distance": ovi[j] if fl & 1 else None,
