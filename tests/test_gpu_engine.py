@@ -302,6 +302,20 @@ def test_bm25_device_build_matches_host_build(eng, corpus):
     s3, r3 = bd.search_dev(torch.from_numpy(qflat).cuda(), torch.from_numpy(qoff).cuda(), 10)
     torch.cuda.synchronize()
     assert np.array_equal(r3.cpu().numpy(), r1) and np.array_equal(s3.cpu().numpy(), s1)
+    # the gated form (the bench step's schedule): preparation on a side stream at once, scoring behind
+    # an event recorded after a producer on the main stream -- same lists
+    qt_d, qo_d = torch.from_numpy(qflat).cuda(), torch.from_numpy(qoff).cuda()
+    side, gate = torch.cuda.Stream(), torch.cuda.Event()
+    x = torch.randn(2048, 2048, device="cuda")
+    side.wait_stream(torch.cuda.current_stream())
+    y = x @ x                                            # the producer (the encode in the step)
+    gate.record()
+    with torch.cuda.stream(side):
+        s4, r4 = bd.search_dev(qt_d, qo_d, 10, gate=gate)
+    torch.cuda.current_stream().wait_stream(side)
+    torch.cuda.synchronize()
+    assert np.array_equal(r4.cpu().numpy(), r1) and np.array_equal(s4.cpu().numpy(), s1)
+    del y
 
 
 def test_mmr_matches_reference_goldens(eng, corpus, golden):
