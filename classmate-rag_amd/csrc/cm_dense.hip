@@ -1858,6 +1858,7 @@ int set_coarse_attrs() {
         {reinterpret_cast<const void *>(&dense_rerank_kernel), kGatherCap * 12},
         {reinterpret_cast<const void *>(&dense_q8_scan_kernel<false>), kQLds},
         {reinterpret_cast<const void *>(&dense_q8_scan_kernel<true>), kQLds},
+        {reinterpret_cast<const void *>(&dense_q8_scan_kernel<true, K1Q_LDS_SHARED>), kQLdsShared},
         {reinterpret_cast<const void *>(&dense_q8_scan_kernel<false, K1Q_LDS_SHARED>), kQLdsShared},
         {reinterpret_cast<const void *>(&dense_rerank_q8_kernel), kQRerankLds}};
     for (const auto &f : fs) {
@@ -1926,11 +1927,17 @@ int launch_coarse(cm_dense *h, const float *q_dev, int nq, int k, int kind, cons
       h->timer.end(st);
       CM_HIP(hipGetLastError());
     } else {
-    if (k1q_seed_q8()) {
-      hipLaunchKernelGGL(dense_q8_scan_kernel<true>, dim3(c.n_pass * c.n_wg_sample), dim3(256), kQLds, st, h->Xq,
-                         h->rmeta, h->live, allow, n_words, w.qq, w.qsc, nq, (const float *)nullptr,
-                         c.rows_per_wg_sample, c.rows_end_sample, c.n_wg_sample, (uint64_t *)nullptr,
-                         (float *)nullptr, (uint32_t *)nullptr, w.mins);
+    if (k1q_seed_q8()) {   // (deferred search: the shared LDS footprint, beside the BM25 blocks)
+      if (run_exact || !env_knob("CM_K1Q_SHARED_LDS", true))
+        hipLaunchKernelGGL(dense_q8_scan_kernel<true>, dim3(c.n_pass * c.n_wg_sample), dim3(256), kQLds, st, h->Xq,
+                           h->rmeta, h->live, allow, n_words, w.qq, w.qsc, nq, (const float *)nullptr,
+                           c.rows_per_wg_sample, c.rows_end_sample, c.n_wg_sample, (uint64_t *)nullptr,
+                           (float *)nullptr, (uint32_t *)nullptr, w.mins);
+      else
+        hipLaunchKernelGGL((dense_q8_scan_kernel<true, K1Q_LDS_SHARED>), dim3(c.n_pass * c.n_wg_sample), dim3(256),
+                           kQLdsShared, st, h->Xq, h->rmeta, h->live, allow, n_words, w.qq, w.qsc, nq,
+                           (const float *)nullptr, c.rows_per_wg_sample, c.rows_end_sample, c.n_wg_sample,
+                           (uint64_t *)nullptr, (float *)nullptr, (uint32_t *)nullptr, w.mins);
     } else {   // K1c MINONLY over the f16 plane's sample (dim 768: the resident-query instance)
       hipLaunchKernelGGL((dense_coarse_scan_kernel<12, kK1cNql, true, kK1cWaves>), dim3(c.grid(c.n_wg_sample)),
                          dim3(64 * kK1cWaves), K1rLds<kK1cNql>::total, st, h->Xh, h->live, allow, n_words, w.qh, nq,
