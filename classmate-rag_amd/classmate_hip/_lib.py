@@ -133,8 +133,9 @@ SIGNATURES = {
     "cm_short_attention_split": (c_int, c_vp, c_i32, c_i32, c_i32, c_i32, c_f32, c_f32, c_vp, c_vp),
     "cm_short_attention_split_masked": (c_int, c_vp, c_i32, c_i32, c_i32, c_i32, c_f32, c_f32, c_vp, c_vp, c_vp),
     "cm_long_attention_split": (c_int, c_vp, c_i32, c_i32, c_i32, c_i32, c_f32, c_f32, c_vp, c_vp, c_vp),
+    "cm_planes_attention": (c_int, c_vp, c_i32, c_i32, c_i32, c_i32, c_f32, c_f32, c_f32, c_vp, c_vp, c_vp),
 }
-CM_EPI_BIAS, CM_EPI_BIAS_GELU, CM_EPI_PLANES_GELU = 0, 1, 2
+CM_EPI_BIAS, CM_EPI_BIAS_GELU, CM_EPI_PLANES_GELU, CM_EPI_PLANES_QKV = 0, 1, 2, 3
 
 fn = {name: _fn(name, sig[0], *sig[1:]) for name, sig in SIGNATURES.items()}
 

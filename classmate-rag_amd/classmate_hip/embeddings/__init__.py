@@ -107,7 +107,9 @@ def _f16x3_layers(layers, emb_ln, D: int):
         v = x Wv^T + bv, |v_i| <= ||x||_2 ||Wv_i||_2 + |bv_i| (O-projection input);
       * GELU output: |gelu(u)| <= max(|u|, 0.17), u = x Wi^T + bi bounded the same way
         (FFN-down input).
-    Returns tuples (wqkv, a_qkv, wo, a_o, g1, b1, wi, a_i, w2, a_2, g2, b2)."""
+      * Q, K, V: |y_i| <= ||x||_2 ||W_i||_2 + |b_i| over all three thirds (the scale of the QKV planes
+        that K9P reads, CM_EPI_PLANES_QKV).
+    Returns tuples (wqkv, a_qkv, wo, a_o, g1, b1, wi, a_i, w2, a_2, g2, b2, s_qkv)."""
     import torch
     sq = math.sqrt(D)
 
@@ -126,10 +128,11 @@ def _f16x3_layers(layers, emb_ln, D: int):
             o_bound = proj_bound(x_l2, wqkv[2 * D:], bqkv[2 * D:])
             y_inf, y_l2 = ln_bounds(g1, b1)
             h_bound = max(proj_bound(y_l2, wi, bi), 0.17)
+            qkv_bound = proj_bound(x_l2, wqkv, bqkv)
             out.append((engine.F16x3Weight(wqkv, bqkv), _act_scale(x_inf),
                         engine.F16x3Weight(wo, bo), _act_scale(o_bound), g1, b1,
                         engine.F16x3Weight(wi, bi), _act_scale(y_inf),
-                        engine.F16x3Weight(w2, b2), _act_scale(h_bound), g2, bb2))
+                        engine.F16x3Weight(w2, b2), _act_scale(h_bound), g2, bb2, _act_scale(qkv_bound)))
             prev_ln = (g2, bb2)
     return out
 
@@ -405,22 +408,40 @@ class E5MultilingualEmbedder:
             o = F.scaled_dot_product_attention(qkv[0], qkv[1], qkv[2], attn_mask=keep)
             return o.transpose(1, 2).reshape(B, S, D)
 
+        # passages (32 < S <= 512): the QKV projection writes planes and K9P attends on them
+        # (CM_E5_PLANES_ATTN=0: fp32 QKV rows + K9L, the round-4 path)
+        planes_attn = fused_attn and os.environ.get("CM_E5_PLANES_ATTN", "1") != "0"
+
         def fwd_f16x3(ids, mask=None, padded=False):
             # K10 path: every GEMM operand is produced directly as split planes (K8 / attention /
             # the FFN-up epilogue write them), so the projections are pure LDS-DMA + MFMA kernels
             B, S = ids.shape
+            if planes_attn and 32 < S <= 512 and S % 64 and os.environ.get("CM_E5_LONG_ATTN", "1") != "0":
+                # K9P takes whole 64-key chunks: pad with masked pad tokens (HF position ids of the
+                # real tokens unchanged, padded keys leave every softmax exactly) and drop the rows
+                Sp = (S + 63) // 64 * 64
+                ids_p = ids.new_full((B, Sp), pad)
+                ids_p[:, :S] = ids
+                mask_p = ids.new_zeros((B, Sp))
+                mask_p[:, :S] = 1 if mask is None else mask
+                return fwd_f16x3(ids_p, mask_p, padded=True)[:, :S]
             w0, pt, keep = embed(ids, mask, padded)
             x, xp = engine.add_layernorm_split(w0, pt, emb.LayerNorm.weight, emb.LayerNorm.bias, eps, layers[0][1])
             # S <= 32: K9s (one wave per (sequence, head)); longer sequences -- passages up to 512
-            # tokens -- K9L (64-key chunks, online softmax); both key-masked on padded batches and both
-            # write the O projection's planes.  CM_E5_LONG_ATTN=0 / CM_E5_MASKED_ATTN=0 restore torch
+            # tokens -- K9P on the QKV planes (K9L on fp32 QKV rows with CM_E5_PLANES_ATTN=0; 64-key
+            # chunks, online softmax); all key-masked on padded batches and all write the O
+            # projection's planes.  CM_E5_LONG_ATTN=0 / CM_E5_MASKED_ATTN=0 restore torch
             # SDPA + a split pass for those cases.
             short = fused_attn and S <= 32 and (keep is None or os.environ.get("CM_E5_MASKED_ATTN", "1") != "0")
             long_ = fused_attn and S > 32 and os.environ.get("CM_E5_LONG_ATTN", "1") != "0"
             km = mask.to(torch.int32).contiguous() if (short or long_) and keep is not None else None
-            for li, (wqkv, a_qkv, wo, a_o, g1, b1, wi, a_i, w2, a_2, g2, bb2) in enumerate(layers):
-                qkv = engine.linear_f16x3(xp, wqkv)
-                if short:   # HIP attention reads the QKV output in place and writes the O operand planes
+            kp = long_ and planes_attn and S % 64 == 0 and S <= 512
+            for li, (wqkv, a_qkv, wo, a_o, g1, b1, wi, a_i, w2, a_2, g2, bb2, s_qkv) in enumerate(layers):
+                qkv = None if kp else engine.linear_f16x3(xp, wqkv)
+                if kp:      # QKV planes -> K9P -> the O operand planes (no fp32 QKV rows)
+                    qp = engine.linear_f16x3(xp, wqkv, qkv=True, planes_out=s_qkv)
+                    op = engine.planes_attention(qp, B, S, H, scale, a_o, key_mask=km)
+                elif short:   # HIP attention reads the QKV output in place and writes the O operand planes
                     op = engine.short_attention_split(qkv.view(B, S, 3 * D), H, scale, a_o, key_mask=km)
                 elif long_:
                     op = engine.long_attention_split(qkv.view(B, S, 3 * D), H, scale, a_o, key_mask=km)

@@ -742,12 +742,15 @@ def split_rows(x, scale: float = 1.0) -> Planes:
     return p
 
 
-def linear_f16x3(x, w: "F16x3Weight", a_scale: float = 1.0, gelu: bool = False, out=None, planes_out: float = 0.0):
+def linear_f16x3(x, w: "F16x3Weight", a_scale: float = 1.0, gelu: bool = False, out=None, planes_out: float = 0.0,
+                 qkv: bool = False):
     """y = x W^T + b (then exact-erf GELU if ``gelu``) at fp32 accuracy on the f16 MFMAs (K10).
 
     x: ``Planes`` (its own scale), or (..., K) fp32 device rows (split here with ``a_scale``, a
     power of two with |x| * a_scale <= 2^15).  Returns (M, N) fp32 -- or, with
-    ``planes_out`` = s > 0 (requires gelu), the Planes of GELU(y) * s for the next projection."""
+    ``planes_out`` = s > 0 (requires gelu), the Planes of GELU(y) * s for the next projection; or,
+    with ``qkv`` and ``planes_out`` = s (no gelu), the fused QKV projection as planes of y * s for
+    ``planes_attention`` (Q, K thirds standard, V third transposed; CM_EPI_PLANES_QKV)."""
     if not isinstance(x, Planes):
         if x.dtype != torch.float32 or x.shape[-1] != w.K:
             raise ValueError(f"x must be (..., {w.K}) fp32")
@@ -761,12 +764,14 @@ def linear_f16x3(x, w: "F16x3Weight", a_scale: float = 1.0, gelu: bool = False, 
     common = (L.ptr(x.data), x.M, w.K, L.ptr(w.planes), L.ptr(w.bias) if w.bias is not None else None,
               float(1.0 / (x.scale * w.scale)), w.N)
     if planes_out:
-        if not gelu:
-            raise ValueError("planes_out is the fused FFN-up epilogue: gelu=True")
+        if gelu == qkv:
+            raise ValueError("planes_out is the fused FFN-up epilogue (gelu=True) or the QKV planes (qkv=True)")
         p = Planes(x.M, w.N, planes_out, dev)
-        L.check(L.fn["cm_linear_f16x3"](*common, L.CM_EPI_PLANES_GELU, None, p.scale, L.ptr(p.data),
-                                        _stream(dev.index)), "cm_linear_f16x3")
+        L.check(L.fn["cm_linear_f16x3"](*common, L.CM_EPI_PLANES_QKV if qkv else L.CM_EPI_PLANES_GELU, None, p.scale,
+                                        L.ptr(p.data), _stream(dev.index)), "cm_linear_f16x3")
         return p
+    if qkv:
+        raise ValueError("qkv=True writes planes: give planes_out")
     if out is None:
         out = torch.empty((*lead, w.N), dtype=torch.float32, device=dev)
     L.check(L.fn["cm_linear_f16x3"](*common, L.CM_EPI_BIAS_GELU if gelu else L.CM_EPI_BIAS, L.ptr(out), 0.0, None,
@@ -834,6 +839,40 @@ def long_attention_split(qkv, heads: int, scale: float, a_scale: float, key_mask
                                             L.ptr(key_mask) if key_mask is not None else None, L.ptr(p.data),
                                             _stream(qkv.device.index)), "cm_long_attention_split")
     return p
+
+
+def planes_attention(qkv: "Planes", B: int, S: int, heads: int, scale: float, a_scale: float,
+                     key_mask=None) -> Planes:
+    """K9P (cm_planes_attention): K9L's attention from the QKV projection's planes
+    (``linear_f16x3(..., qkv=True, planes_out=s)``), writing the context * a_scale as K10 Planes
+    (B*S x heads*64).  S % 64 == 0, S <= 512; key_mask: optional int32 (B, S), nonzero = attend."""
+    if not isinstance(qkv, Planes) or qkv.K != 3 * heads * 64 or qkv.M != B * S:
+        raise ValueError("qkv must be the (B*S) x 3*heads*64 QKV planes")
+    if S <= 0 or S % 64 or S > 512:
+        raise ValueError("planes attention: need S % 64 == 0 and 0 < S <= 512")
+    dev = qkv.data.device
+    if key_mask is not None:
+        if tuple(key_mask.shape) != (B, S) or key_mask.dtype != torch.int32 or key_mask.device != dev:
+            raise ValueError("key_mask must be int32 (B, S) on the qkv device")
+        key_mask = key_mask.contiguous()
+    p = Planes(B * S, heads * 64, a_scale, dev)
+    L.check(L.fn["cm_planes_attention"](L.ptr(qkv.data), B, S, heads, 64, float(scale), qkv.scale, p.scale,
+                                        L.ptr(key_mask) if key_mask is not None else None, L.ptr(p.data),
+                                        _stream(dev.index)), "cm_planes_attention")
+    return p
+
+
+def qkv_planes_v(p: "Planes"):
+    """(hi, lo) f16 row-major (M, N/3) views of the V third of CM_EPI_PLANES_QKV planes (tests)."""
+    N = p.K
+    nkbv = N // 96
+    blk = p.data.view(-1, N // 32, 2, 4, 16, 8)        # [row block][kb][plane][g][c][e]
+    rows = blk.shape[0] // 2 * 2
+    v = blk[:rows, 2 * nkbv:].reshape(rows // 2, 2 * nkbv, 2, 4, 16, 8)   # [32-row unit][dblk][plane][g][c][e]
+    # e 0-3: rows 4 g + e, e 4-7: rows 16 + 4 g + e - 4 of the unit; c = column within the 16-block
+    v = v.view(rows // 2, 2 * nkbv, 2, 4, 16, 2, 4).permute(2, 0, 5, 3, 6, 1, 4)   # [plane][u][half][g][r][dblk][c]
+    v = v.reshape(2, rows * 16, N // 3)
+    return v[0, :p.M], v[1, :p.M]
 
 
 # ---------------------------------------------------------------------------

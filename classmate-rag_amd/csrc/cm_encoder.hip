@@ -825,6 +825,223 @@ __global__ void __launch_bounds__(256) long_attention_f16x3_kernel(const float *
   }
 }
 
+// K9P: K9L's math on operands that are already split.  The QKV projection writes its output as
+// planes (cm_linear_f16x3 with CM_EPI_PLANES_QKV, one exact power-of-two scale s for Q, K and V from
+// the host's rigorous bound): Q and K in the standard layout, V transposed in 32-key units whose
+// lane slots are already in the permuted key order of the P V operand (k10_epilogue).  So every
+// fragment of the attention is a 1 KiB block of HBM: no fp32 loads, no maxima, no split work.  One
+// workgroup of up to 16 waves (16 queries each) per (sequence, head, 256-query block) -- at S = 256
+// the keys and values of a head are read once -- the 64-key chunks stream through a two-slot LDS
+// ring by LDS-DMA (32 one-KiB pieces per chunk, the next chunk in flight while this one is
+// consumed, one barrier per chunk).  Per chunk and wave: the same 48 MFMAs and online softmax as
+// K9L; the context is written as planes of o * a_scale with K10's DPP pair stores.  S % 64 == 0.
+constexpr int kApSlot = 32 * 1024;  // one chunk: K 16 KiB + V 16 KiB
+#ifndef K9P_WAVES
+#define K9P_WAVES 8                 // waves (16 queries each) per workgroup: 8 or 16 (A/B)
+#endif
+
+template <bool MASKED>
+__global__ void __launch_bounds__(1024) planes_attention_kernel(const _Float16 *__restrict__ qkv, int nseq, int S, int H,
+                                                                float scale, float s_qkv, float a_scale,
+                                                                const int32_t *__restrict__ key_mask,
+                                                                _Float16 *__restrict__ planes) {
+  constexpr float kPScale = 16384.f;
+  __shared__ __attribute__((aligned(16))) unsigned char lds[2 * kApSlot];
+  __shared__ uint64_t kmask[8];                        // per 64-key chunk (S <= 512)
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), nw = blockDim.x >> 6;
+  const int g = lane >> 4, c = lane & 15;
+  // XCD-aware order: the nqb query blocks of one (sequence, head) are blockIdx w, w + 8, ... (one XCD
+  // under round-robin dispatch, so the keys and values DMA'd by the first stay in that XCD's L2 for
+  // the others); the grid is padded to whole groups of 8 (sequence, head) pairs
+  const int nqb = (S + 16 * nw - 1) / (16 * nw);
+  const int64_t grp = blockIdx.x / (8 * nqb);
+  const int qb = (int)((blockIdx.x >> 3) % nqb);
+  const int64_t pair = grp * 8 + (blockIdx.x & 7);
+  if (pair >= (int64_t)nseq * H) return;          // padding: the whole workgroup, before any barrier
+  const int h = (int)(pair % H);
+  const int64_t b = pair / H;
+  const int D = H * kAttnDh, kb3 = 3 * D / 32, kbd = D / 32;   // split blocks per row block: qkv, context
+  const int nch = S / 64;
+  const int q0 = qb * 16 * nw + wave * 16;
+  const bool qok = q0 < S;                             // wave-uniform: a partial last block's spare waves
+  const unsigned char *src = reinterpret_cast<const unsigned char *>(qkv);
+
+  // key mask bits of every chunk (all keys attend without a mask)
+  if constexpr (MASKED)
+    for (int ch = wave; ch < nch; ch += nw) {
+      const uint64_t bits = __ballot(key_mask[b * S + 64 * ch + lane] != 0);
+      if (lane == 0) kmask[ch] = bits;
+    }
+  // Q fragments (B operand of S^T = K Q^T): lane (g, c) = query q0 + c, dims 32 st + 8 g .. + 7
+  h16x8_t qh[2], ql[2];
+#pragma unroll
+  for (int st = 0; st < 2; ++st) {
+    if (qok) {
+      const int64_t o = ((((b * S + q0) >> 4) * kb3 + 2 * h + st) * 128 + lane) * 8;
+      qh[st] = *reinterpret_cast<const h16x8_t *>(qkv + o);
+      ql[st] = *reinterpret_cast<const h16x8_t *>(qkv + o + 512);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) qh[st][e] = ql[st][e] = (_Float16)0.f;
+    }
+  }
+  // chunk ch's 32 DMA pieces: p < 16 K block (kt = p / 4, st, plane), else V^T block (u, dt, plane).
+  // Piece p of chunk ch sits at (first key row / 16) x kb3 split blocks + a per-piece offset (the V^T
+  // 32-row units: 2 u_g = krow / 16 since krow is a multiple of 64); this wave's pieces p = wave +
+  // i nw and their offsets are fixed for the kernel
+  int64_t poff[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int p = wave + i * nw;
+    int64_t blk = 0;
+    if (p < 16) {
+      const int kt = p >> 2, st = (p >> 1) & 1;
+      blk = (int64_t)kt * kb3 + kbd + 2 * h + st;
+    } else if (p < 32) {
+      const int u = (p - 16) >> 3, dt = ((p - 16) >> 1) & 3;
+      const int dblk = 4 * h + dt;                       // 16-dim block of V
+      blk = (int64_t)(2 * u + dblk / kbd) * kb3 + 2 * kbd + dblk % kbd;
+    }
+    poff[i] = blk * 2048 + (p & 1) * 1024 + lane * 16;
+  }
+  const unsigned char *seq_src = src + ((b * S) >> 4) * kb3 * 2048;
+  auto issue = [&](int ch) __attribute__((always_inline)) {
+    unsigned char *slot = lds + (ch & 1) * kApSlot;
+    const unsigned char *cs = seq_src + (int64_t)(4 * ch) * kb3 * 2048;   // 64 keys = 4 row blocks
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int p = wave + i * nw;
+      if (p >= 32) break;
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)(cs + poff[i]),
+                                       (__attribute__((address_space(3))) void *)(slot + p * 1024), 16, 0, 0);
+    }
+  };
+  issue(0);
+
+  // softmax in the base-2 domain: p = 2^(s lscale2 - m) with lscale2 = scale log2(e) / s_qkv^2 (one
+  // fma + v_exp per score); masked scores are -inf (2^-inf = 0), and m_safe keeps a chunk whose keys
+  // are all masked so far from producing -inf - -inf
+  const float lscale2 = scale / (s_qkv * s_qkv) * 1.4426950408889634f;
+  const float inv_pv = 1.f / (kPScale * s_qkv);
+  float m_run = -INFINITY, l_run = 0.f;               // per query column c (same in every g), log2 domain
+  f32x4_t o_run[4];                                   // [dt]: O[query 4 g + r][dim 16 dt + c]
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) o_run[dt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  for (int ch = 0; ch < nch; ++ch) {
+    // this wave's pieces of chunk ch landed; the barrier publishes everyone's (and the mask) and
+    // retires every read of the other slot, which the next chunk's pieces then overwrite
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (ch + 1 < nch) issue(ch + 1);
+    const _Float16 *kst = reinterpret_cast<const _Float16 *>(lds + (ch & 1) * kApSlot);
+    const _Float16 *vst = kst + 16 * 512;
+    f32x4_t sc[4];
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt) {
+      f32x4_t a = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int st = 0; st < 2; ++st) {
+        const h16x8_t kh = *reinterpret_cast<const h16x8_t *>(kst + ((kt * 2 + st) * 2) * 512 + lane * 8);
+        const h16x8_t kl = *reinterpret_cast<const h16x8_t *>(kst + ((kt * 2 + st) * 2 + 1) * 512 + lane * 8);
+        a = mfma3(kh, kl, qh[st], ql[st], a);
+      }
+      sc[kt] = a;
+    }
+    if constexpr (MASKED) {                           // keys 16 kt + 4 g + r of the chunk
+      const uint64_t kb = kmask[ch];
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt) {
+        const uint32_t nib = (uint32_t)(kb >> (16 * kt + 4 * g));
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (!((nib >> r) & 1u)) sc[kt][r] = -INFINITY;
+      }
+    }
+    float mloc = fmaxf(fmaxf(sc[0][0], sc[0][1]), fmaxf(sc[0][2], sc[0][3]));
+#pragma unroll
+    for (int kt = 1; kt < 4; ++kt) mloc = fmaxf(mloc, fmaxf(fmaxf(sc[kt][0], sc[kt][1]), fmaxf(sc[kt][2], sc[kt][3])));
+    mloc = fmaxf(mloc, __shfl_xor(mloc, 16));
+    mloc = fmaxf(mloc, __shfl_xor(mloc, 32));
+    const float m_new = fmaxf(m_run, mloc * lscale2);
+    const float m_safe = m_new == -INFINITY ? 0.f : m_new;
+    const float alpha = __builtin_amdgcn_exp2f(m_run - m_safe);
+    float psum = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float p = __builtin_amdgcn_exp2f(fmaf(sc[kt][r], lscale2, -m_safe));
+        sc[kt][r] = p;
+        psum += p;
+      }
+    psum += __shfl_xor(psum, 16);
+    psum += __shfl_xor(psum, 32);
+    l_run = l_run * alpha + psum;
+    m_run = m_new;
+    h16x8_t ph[2], pl[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        _Float16 hh, ll;
+        f16x3_split1(sc[2 * u + (e >> 2)][e & 3] * kPScale, hh, ll);
+        ph[u][e] = hh;
+        pl[u][e] = ll;
+      }
+    float ar[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) ar[r] = __shfl(alpha, 4 * g + r);
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      f32x4_t oc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const h16x8_t vh = *reinterpret_cast<const h16x8_t *>(vst + ((u * 4 + dt) * 2) * 512 + lane * 8);
+        const h16x8_t vl = *reinterpret_cast<const h16x8_t *>(vst + ((u * 4 + dt) * 2 + 1) * 512 + lane * 8);
+        oc = mfma3(ph[u], pl[u], vh, vl, oc);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o_run[dt][r] = fmaf(o_run[dt][r], ar[r], oc[r] * inv_pv);
+    }
+  }
+  if (!qok) return;                                   // no barrier follows
+  // ---- O / l * a_scale -> context planes: lanes c, c ^ 1 swap halves so each stores 4-byte
+  //      column pairs (k10_epilogue's planes store)
+  float lr[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) lr[r] = __shfl(l_run, 4 * g + r);
+  const bool odd = c & 1;
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) {
+    uint32_t hh[4], ll[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      _Float16 a, b2;
+      f16x3_split1(lr[r] > 0.f ? o_run[dt][r] / lr[r] * a_scale : 0.f, a, b2);
+      hh[r] = __builtin_bit_cast(uint16_t, a);
+      ll[r] = __builtin_bit_cast(uint16_t, b2);
+    }
+    const uint32_t sh = odd ? (hh[0] | hh[1] << 16) : (hh[2] | hh[3] << 16);
+    const uint32_t sl = odd ? (ll[0] | ll[1] << 16) : (ll[2] | ll[3] << 16);
+    const uint32_t rh = (uint32_t)__builtin_amdgcn_mov_dpp((int)sh, 0xB1, 0xF, 0xF, false);
+    const uint32_t rl = (uint32_t)__builtin_amdgcn_mov_dpp((int)sl, 0xB1, 0xF, 0xF, false);
+    const int r0 = odd ? 2 : 0;
+    const int c0 = h * kAttnDh + 16 * dt + (c & ~1);
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const uint32_t mine_h = hh[r0 + q], mine_l = ll[r0 + q];
+      const uint32_t oth_h = (rh >> (16 * q)) & 0xffffu, oth_l = (rl >> (16 * q)) & 0xffffu;
+      const uint32_t wh = odd ? (oth_h | mine_h << 16) : (mine_h | oth_h << 16);
+      const uint32_t wl = odd ? (oth_l | mine_l << 16) : (mine_l | oth_l << 16);
+      const int64_t off = f16x3_plane_off(b * S + q0 + 4 * g + r0 + q, c0, kbd);
+      *reinterpret_cast<uint32_t *>(planes + off) = wh;
+      *reinterpret_cast<uint32_t *>(planes + off + 512) = wl;
+    }
+  }
+}
+
 }  // namespace cm
 
 using namespace cm;
@@ -916,6 +1133,30 @@ extern "C" int cm_short_attention_split(const float *qkv_dev, int32_t B, int32_t
   else
     hipLaunchKernelGGL((short_attention_kernel<float, true>), dim3((unsigned)((int64_t)B * H)), dim3(64), 0,
                        (hipStream_t)stream, qkv_dev, S, H, scale, nullptr, a_scale, (_Float16 *)planes_dev);
+  CM_HIP(hipGetLastError());
+  return CM_OK;
+}
+
+extern "C" int cm_planes_attention(const void *qkv_planes, int32_t B, int32_t S, int32_t H, int32_t head_dim,
+                                   float scale, float s_qkv, float a_scale, const int32_t *key_mask_dev,
+                                   void *planes_dev, void *stream) {
+  if (B <= 0) return CM_OK;
+  if (!qkv_planes || !planes_dev) CM_FAIL(CM_EINVAL, "NULL argument");
+  if (head_dim != kAttnDh) CM_FAIL(CM_EINVAL, "head_dim must be 64");
+  if (S <= 0 || S % 64 || S > 512 || H <= 0) CM_FAIL(CM_EINVAL, "need S % 64 == 0, 0 < S <= 512 and H > 0");
+  if (!(s_qkv > 0.f) || !(a_scale > 0.f)) CM_FAIL(CM_EINVAL, "scales must be > 0");
+  if (((uintptr_t)qkv_planes & 15) || ((uintptr_t)planes_dev & 15)) CM_FAIL(CM_EINVAL, "planes must be 16-byte aligned");
+  // 8 waves (128 queries) per workgroup: two resident per CU (LDS 2 x 64 KiB, 4 waves per SIMD), so one
+  // workgroup's first DMA and epilogue overlap the other's chunks (16 waves: 281 vs ... us per layer)
+  const int nw = std::min(K9P_WAVES, S / 16);
+  const int64_t blocks = ceil_div((int64_t)B * H, 8) * 8 * ((S + 16 * nw - 1) / (16 * nw));
+  if (blocks > INT32_MAX) CM_FAIL(CM_EINVAL, "too many (sequence, head, query block) workgroups");
+  if (key_mask_dev)
+    hipLaunchKernelGGL(planes_attention_kernel<true>, dim3((unsigned)blocks), dim3(64 * nw), 0,
+                       (hipStream_t)stream, (const _Float16 *)qkv_planes, B, S, H, scale, s_qkv, a_scale, key_mask_dev, (_Float16 *)planes_dev);
+  else
+    hipLaunchKernelGGL(planes_attention_kernel<false>, dim3((unsigned)blocks), dim3(64 * nw), 0,
+                       (hipStream_t)stream, (const _Float16 *)qkv_planes, B, S, H, scale, s_qkv, a_scale, key_mask_dev, (_Float16 *)planes_dev);
   CM_HIP(hipGetLastError());
   return CM_OK;
 }

@@ -113,7 +113,32 @@ __device__ __forceinline__ void k10_spread(std::integer_sequence<int, I...>) {
   (k10_slot<NM, NR, ND, EARLY, I>(), ...);
 }
 
-__device__ inline float gelu_erf(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
+// GELU(x) = x Phi(x) (torch's exact-erf F.gelu) in one branch-free form: Phi(x) = 1 - h for x >= 0, h
+// for x < 0, h = erfc(u) / 2 = 2^P(u), u = |x| / sqrt 2, P a degree-9 least-squares fit of
+// log2(erfc(u) / 2) on [0, 3.92] (beyond, erf rounds to +-1 in fp32 and h is 0, as in torch).  Against
+// an fp64 GELU on a 700k-point grid over [-7, 7] (fp32 arithmetic, fma): max abs error 3.8e-7 and
+// relative 3.2e-6 for |x| < 5.5, where 0.5 x (1 + erff(x / sqrt 2)) in fp32 has 4.5e-7 and, through
+// its cancellation at negative x, 0.57 (tools/gelu_fit.py).  19 VALU operations instead of ~37 for
+// ocml's two-branch erff + the product: the FFN-up epilogue applies it to 72 outputs per lane and tile.
+#ifndef K10_GELU_OCML
+#define K10_GELU_OCML 0   // 1: 0.5 x (1 + erff(x / sqrt 2)) (variant builds, A/B)
+#endif
+__device__ inline float gelu_erf(float x) {
+  if (K10_GELU_OCML) return 0.5f * x * (1.f + erff(x * 0.70710678118654752f));
+  const float u = fminf(fabsf(x) * 0.70710678118654752f, 3.92f);
+  float p = 1.5919721363388817e-06f;
+  p = fmaf(p, u, -2.9504877602448687e-05f);
+  p = fmaf(p, u, 0.00020694537670351565f);
+  p = fmaf(p, u, -0.0004535108746495098f);
+  p = fmaf(p, u, -0.002977503463625908f);
+  p = fmaf(p, u, 0.03079916536808014f);
+  p = fmaf(p, u, -0.1500696986913681f);
+  p = fmaf(p, u, -0.9179301261901855f);
+  p = fmaf(p, u, -1.6279653310775757f);
+  p = fmaf(p, u, -0.999998927116394f);
+  const float h = u >= 3.92f ? 0.f : __builtin_amdgcn_exp2f(p);
+  return x * (x >= 0.f ? 1.f - h : h);
+}
 
 // one 8-element segment: fp32 -> (hi, lo) f16 halves after the exact power-of-two scale
 __device__ inline void split8(const float (&x)[8], float s, h16x8 &hi, h16x8 &lo) {
@@ -126,7 +151,7 @@ __device__ inline void split8(const float (&x)[8], float s, h16x8 &hi, h16x8 &lo
   }
 }
 
-enum { kEpiF32 = 0, kEpiF32Gelu = 1, kEpiPlanesGelu = 2 };
+enum { kEpiF32 = 0, kEpiF32Gelu = 1, kEpiPlanesGelu = 2, kEpiPlanesQKV = 3 };
 
 // Tile order of the persistent schedule: 8 row tiles per column sweep ("grouped").
 __device__ __forceinline__ void k10_tile(int L, int tiles_m, int tiles_n, int &tm, int &tn) {
@@ -157,7 +182,7 @@ __device__ __forceinline__ void k10_epilogue(g32x4 (&acc)[BMB / 2][BNB / (NW / 2
     const float bv = btab[col];
 #pragma unroll
     for (int i = 0; i < WMT; ++i) {
-      if constexpr (EPI != kEpiPlanesGelu) {
+      if constexpr (EPI == kEpiF32 || EPI == kEpiF32Gelu) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int64_t row = (rb0 + i) * 16 + 4 * g4 + r;
@@ -170,9 +195,31 @@ __device__ __forceinline__ void k10_epilogue(g32x4 (&acc)[BMB / 2][BNB / (NW / 2
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           _Float16 h, l;
-          f16x3_split1(gelu_erf(acc[i][j][r] * out_scale + bv) * next_scale, h, l);
+          float y = acc[i][j][r] * out_scale + bv;
+          if constexpr (EPI == kEpiPlanesGelu) y = gelu_erf(y);
+          f16x3_split1(y * next_scale, h, l);
           hh[r] = __builtin_bit_cast(uint16_t, h);
           ll[r] = __builtin_bit_cast(uint16_t, l);
+        }
+        // QKV: the V third (columns >= 2N/3, whole 16-column blocks) goes out transposed for the
+        // P V operand of planes_attention_kernel: per 32-row unit u and 16-column block d, a 2 KiB
+        // block [hi][lo] whose lane slot (c, g) holds rows 4 g .. + 3 (e 0-3) and 16 + 4 g .. + 3
+        // (e 4-7) of column c -- the key order of the P fragment.  It occupies the 2 x (N/96)
+        // split blocks of the standard layout's V region of those 32 rows (d / (N/96) picks the row
+        // block, d % (N/96) the block within it), so the buffer keeps the standard size.
+        if constexpr (EPI == kEpiPlanesQKV) {
+          const int vcol0 = (N / 3) * 2, nkbv = N / 96;
+          if (cbase + 16 * j >= vcol0) {
+            const int64_t rb16 = rb0 + i;
+            const int dblk = (col - vcol0) >> 4;
+            const int64_t rb = 2 * (rb16 >> 1) + dblk / nkbv;
+            const int kb = 2 * nkbv + dblk % nkbv;
+            const int64_t off = ((rb * (N >> 5) + kb) * 128 + c16 + 16 * g4) * 8 + 4 * (rb16 & 1);
+            *reinterpret_cast<uint2 *>(Cp + off) = make_uint2(hh[0] | hh[1] << 16, hh[2] | hh[3] << 16);
+            *reinterpret_cast<uint2 *>(Cp + off + 512) = make_uint2(ll[0] | ll[1] << 16, ll[2] | ll[3] << 16);
+            acc[i][j] = g32x4{0.f, 0.f, 0.f, 0.f};
+            continue;
+          }
         }
         // even lane keeps rows 0-1 and sends 2-3; odd lane keeps 2-3 and sends 0-1
         const uint32_t sh = odd ? (hh[0] | hh[1] << 16) : (hh[2] | hh[3] << 16);
@@ -524,7 +571,7 @@ static int launch_tile(const _Float16 *A, int64_t M, int K, const _Float16 *W, c
   const int lds_bytes = S * ((2 * (BMB + BNB) + NW - 1) / NW) * NW * 1024 + ((N * 4 + 15) & ~15);
   if (lds_bytes > 160 * 1024) CM_FAIL(CM_EINVAL, "N too large for the LDS bias table");
   const dim3 grid((unsigned)std::min<int64_t>(tiles, n_cu)), block(64 * NW);
-  static int attr_set[3] = {0, 0, 0};  // > 64 KiB of dynamic LDS: opt in once per kernel
+  static int attr_set[4] = {0, 0, 0, 0};  // > 64 KiB of dynamic LDS: opt in once per kernel
   switch (epi) {
 #define CM_K10_CASE(E)                                                                                             \
   case E:                                                                                                          \
@@ -539,6 +586,7 @@ static int launch_tile(const _Float16 *A, int64_t M, int K, const _Float16 *W, c
     CM_K10_CASE(kEpiF32)
     CM_K10_CASE(kEpiF32Gelu)
     CM_K10_CASE(kEpiPlanesGelu)
+    CM_K10_CASE(kEpiPlanesQKV)
 #undef CM_K10_CASE
     default: CM_FAIL(CM_EINVAL, "unknown epilogue");
   }
@@ -581,9 +629,14 @@ extern "C" int cm_linear_f16x3(const void *a_planes, int64_t M, int32_t K, const
   if (!a_planes || !w_planes) CM_FAIL(CM_EINVAL, "NULL argument");
   if (K <= 0 || K % 64) CM_FAIL(CM_EINVAL, "K must be a positive multiple of 64");
   if (N <= 0 || N % 64) CM_FAIL(CM_EINVAL, "N must be a positive multiple of 64");
-  if (epilogue == CM_EPI_PLANES_GELU ? !c_planes : !c_dev) CM_FAIL(CM_EINVAL, "NULL output");
-  if (epilogue != CM_EPI_BIAS && epilogue != CM_EPI_BIAS_GELU && epilogue != CM_EPI_PLANES_GELU)
+  const bool planes_out = epilogue == CM_EPI_PLANES_GELU || epilogue == CM_EPI_PLANES_QKV;
+  if (planes_out ? !c_planes : !c_dev) CM_FAIL(CM_EINVAL, "NULL output");
+  if (epilogue != CM_EPI_BIAS && epilogue != CM_EPI_BIAS_GELU && epilogue != CM_EPI_PLANES_GELU &&
+      epilogue != CM_EPI_PLANES_QKV)
     CM_FAIL(CM_EINVAL, "unknown epilogue");
+  // the QKV planes epilogue: three equal parts of whole 16-column blocks, 32-row units of V (the
+  // tiled kernel: every tile height is a multiple of 32, and M > 32 keeps it off the skinny form)
+  if (epilogue == CM_EPI_PLANES_QKV && (N % 96 || M <= 32)) CM_FAIL(CM_EINVAL, "QKV planes: need N % 96 == 0, M > 32");
   if (!g_n_cu) {
     int dev = 0, n = 0;
     CM_HIP(hipGetDevice(&dev));

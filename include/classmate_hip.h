@@ -420,6 +420,10 @@ int cm_short_attention(const void *qkv_dev, int32_t B, int32_t S, int32_t H, int
 #define CM_EPI_BIAS 0
 #define CM_EPI_BIAS_GELU 1
 #define CM_EPI_PLANES_GELU 2
+/* CM_EPI_PLANES_QKV: the fused QKV projection (N = 3 x H x 64, N % 96 == 0, M > 32) written as planes
+ * of C * next_scale for cm_planes_attention: the Q and K thirds in the standard layout, the V third
+ * transposed per 32-row unit (the attention's P V operand; see cm_gemm.hip k10_epilogue). */
+#define CM_EPI_PLANES_QKV 3
 int64_t cm_f16x3_plane_rows(int64_t M);
 int cm_f16x3_split_rows(const float *x_dev, int64_t M, int32_t K, float scale, void *planes_dev, void *stream);
 int cm_f16x3_split_weights(const float *w_dev, int32_t N, int32_t K, float scale, void *planes_dev, void *stream);
@@ -441,6 +445,12 @@ int cm_short_attention_split_masked(const float *qkv_dev, int32_t B, int32_t S, 
  * truncation at 512 tokens). */
 int cm_long_attention_split(const float *qkv_dev, int32_t B, int32_t S, int32_t H, int32_t head_dim, float scale,
                             float a_scale, const int32_t *key_mask_dev, void *planes_dev, void *stream);
+/* cm_planes_attention: the same context planes from the CM_EPI_PLANES_QKV output of the QKV
+ * projection (qkv_planes = planes of (B*S) x 3*H*64 values times s_qkv, a power of two): K9P, every
+ * operand streamed as split blocks by LDS-DMA (the passage encode, S % 64 == 0, S <= 512; the
+ * caller pads other lengths with masked keys). */
+int cm_planes_attention(const void *qkv_planes, int32_t B, int32_t S, int32_t H, int32_t head_dim, float scale,
+                        float s_qkv, float a_scale, const int32_t *key_mask_dev, void *planes_dev, void *stream);
 
 /* The N > 1 step's exchange merge (no reference interface: the reference is single
  * process -- this is the sharded form of ChromaVectorStore.query, vector_chroma.py:204-253, and

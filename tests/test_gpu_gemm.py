@@ -235,3 +235,104 @@ def test_long_attention_split_matches_fp64(S, masked):
         ps = engine.short_attention_split(qkv, H, 0.125, 2.0 ** 8)
         hs, ls = ps.halves()
         assert float(((hs.double() + ls.double()) / 2.0 ** 8 - got).abs().max()) <= 2 * e32 + 2e-6
+
+
+@pytest.mark.parametrize("M", [6144, 1000, 96, 33])
+def test_qkv_planes_epilogue_bits(M):
+    """CM_EPI_PLANES_QKV (the fused QKV projection written for K9P) == the fp32 GEMM output split
+    with cm_f16x3_split_rows, bit for bit: Q and K thirds in the standard planes, the V third in the
+    transposed 32-row-unit layout (decoded by engine.qkv_planes_v)."""
+    import torch
+    from classmate_hip import engine
+    x, w, b = _case(M, 768, 2304, seed=M + 17)
+    W = engine.F16x3Weight(w, b)
+    s = 2.0 ** 11
+    p = engine.linear_f16x3(x, W, qkv=True, planes_out=s)
+    ref = engine.split_rows(engine.linear_f16x3(x, W), s)
+    for got, want in zip(p.halves(), ref.halves()):
+        assert torch.equal(got[:, :1536], want[:, :1536])
+    for got, want in zip(engine.qkv_planes_v(p), ref.halves()):
+        assert torch.equal(got, want[:, 1536:])
+    with pytest.raises(ValueError):
+        engine.linear_f16x3(x, W, qkv=True)                      # planes only
+
+
+def _identity_qkv_planes(qkv, s):
+    """fp32 (B, S, 3*H*64) rows -> CM_EPI_PLANES_QKV planes of (hi + lo of qkv) * s, through K10 with an
+    identity weight (every output is its input's 22-bit split, exactly)."""
+    import torch
+    from classmate_hip import engine
+    F = qkv.shape[-1]
+    I = engine.F16x3Weight(torch.eye(F, device="cuda"), torch.zeros(F, device="cuda"))
+    return engine.linear_f16x3(qkv.reshape(-1, F), I, a_scale=2.0 ** 12, qkv=True, planes_out=s)
+
+
+@pytest.mark.parametrize("S", [64, 128, 256, 320, 512])
+@pytest.mark.parametrize("masked", [False, True])
+def test_planes_attention_matches_fp64(S, masked):
+    """K9P (cm_planes_attention: every operand an LDS-DMA'd split block of the QKV planes, one
+    power-of-two scale for Q, K, V) against an fp64 softmax(q k^T / 8) v, padded keys removed when
+    masked, as accurate as torch's fp32 -- and within the same bound of K9L on the fp32 rows."""
+    import torch
+    from classmate_hip import engine
+    torch.manual_seed(11 * S + masked)
+    B, H = (12 if S <= 256 else 5), 12
+    qkv = 2 * torch.randn(B, S, 3 * H * 64, device="cuda")
+    mask = None
+    keep = torch.ones(B, 1, 1, S, dtype=torch.bool, device="cuda")
+    if masked:
+        lens = torch.randint(1, S + 1, (B,), device="cuda")
+        lens[0] = S
+        lens[1] = 1
+        mask = (torch.arange(S, device="cuda")[None, :] < lens[:, None]).to(torch.int32)
+        keep = mask.bool()[:, None, None, :]
+    q, k, v = qkv.double().view(B, S, 3, H, 64).permute(2, 0, 3, 1, 4)
+    sc = (q @ k.transpose(-1, -2) / 8.0).masked_fill(~keep, float("-inf"))
+    ref = (torch.softmax(sc, dim=-1) @ v).transpose(1, 2).reshape(B * S, H * 64)
+    q32, k32, v32 = qkv.view(B, S, 3, H, 64).permute(2, 0, 3, 1, 4)
+    s32 = (q32 @ k32.transpose(-1, -2) / 8.0).masked_fill(~keep, float("-inf"))
+    t32 = (torch.softmax(s32, dim=-1) @ v32).transpose(1, 2).reshape(B * S, H * 64)
+    qp = _identity_qkv_planes(qkv, 2.0 ** 10)
+    p = engine.planes_attention(qp, B, S, H, 0.125, 2.0 ** 8, key_mask=mask)
+    hi, lo = p.halves()
+    got = (hi.double() + lo.double()) / 2.0 ** 8
+    e, e32 = float((got - ref).abs().max()), float((t32.double() - ref).abs().max())
+    print(f"\nplanes attention S={S} masked={masked}: max err {e:.2e} (torch fp32 {e32:.2e})")
+    assert e <= 2 * e32 + 2e-6
+
+
+def test_planes_attention_rejects_bad_shapes():
+    import torch
+    from classmate_hip import engine
+    qkv = torch.randn(2, 64, 3 * 12 * 64, device="cuda")
+    qp = _identity_qkv_planes(qkv, 2.0 ** 10)
+    with pytest.raises(ValueError):
+        engine.planes_attention(qp, 2, 100, 12, 0.125, 1.0)       # S % 64
+    with pytest.raises(ValueError):
+        engine.planes_attention(qp, 4, 64, 12, 0.125, 1.0)        # M != B * S
+    with pytest.raises(ValueError):
+        engine.planes_attention(qp, 2, 64, 12, 0.125, 1.0, key_mask=torch.ones(2, 64, device="cuda"))
+
+
+@pytest.mark.parametrize("S,cut", [(256, None), (100, 37), (320, 5), (64, 1)])
+def test_e5_passage_planes_attention_matches_hf(monkeypatch, S, cut):
+    """The passage encode on K9P (QKV planes; S not a multiple of 64 padded with masked pad tokens
+    inside the forward) == the Hugging Face fp32 module within 2e-5, ragged rows included, and
+    within 2e-5 of the K9L path on fp32 QKV rows (CM_E5_PLANES_ATTN=0)."""
+    import torch
+    from classmate_hip.embeddings import E5MultilingualEmbedder
+    emb = E5MultilingualEmbedder.random_init(seed=5, device="cuda", num_layers=2, dtype="float32")
+    B = 6
+    g = torch.Generator(device="cuda").manual_seed(S)
+    ids = torch.randint(5, 250002, (B, S), device="cuda", generator=g)
+    ids[:, 0] = 0
+    mask = torch.ones_like(ids)
+    if cut is not None:
+        mask[B - 1, cut:] = 0
+        ids[B - 1, cut:] = 1
+    got = emb.encode_token_ids(ids, mask)
+    torch.testing.assert_close(got, emb._encode_hf(ids, mask), atol=2e-5, rtol=0)
+    monkeypatch.setenv("CM_E5_PLANES_ATTN", "0")
+    emb._lean = None
+    old = emb.encode_token_ids(ids, mask)
+    torch.testing.assert_close(got, old, atol=2e-5, rtol=0)
