@@ -122,9 +122,110 @@ __global__ void __launch_bounds__(64 * kLnWaves)
   }
 }
 
+// K8 with the planes written per 16-row block: a workgroup of 16 waves takes one row block (a row per
+// wave, as add_layernorm_kernel: in registers, fp32 two-pass statistics, fp32 rows stored directly),
+// stages the block's hi / lo halves in LDS in the plane order and then writes the block's D / 32
+// split blocks -- one contiguous 64 D-byte run -- with 16-byte stores across the workgroup, instead
+// of every lane storing 8-byte pieces 256 B apart.  Same values, bit for bit.  Ingest shape (65536
+// rows): 216 -> 135 us per call (5.97 TB/s); query batch (6144 rows) within noise
+// (profiles/r05_ln_ab.txt).
+template <int PER>
+__global__ void __launch_bounds__(1024)
+    add_layernorm_split_rb_kernel(const float *x, const float *__restrict__ r, int64_t r_rows,
+                                  const float *__restrict__ gamma, const float *__restrict__ beta, int64_t rows, int D,
+                                  float eps, float *out, float a_scale, _Float16 *__restrict__ ph) {
+  extern __shared__ __attribute__((aligned(16))) _Float16 stage[];   // [kb][hi/lo][slot 64][8]
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t rb = blockIdx.x;
+  const int D4 = D >> 2;
+  typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+  const int rr = wave;
+  const int64_t row = rb * 16 + rr;
+  const bool live = row < rows;                        // rows past the end: zero planes (buffer padding)
+  const float *xr = x + row * D;
+  const float *rrow = r ? r + (row % r_rows) * D : nullptr;
+  float v[PER][4];
+  float sum = 0.f;
+#pragma unroll
+  for (int u = 0; u < PER; ++u) {
+    const int c = lane + 64 * u;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[u][e] = 0.f;
+    if (live && c < D4) {
+      ln_load4(xr + 4 * c, v[u]);
+      if (rrow) {
+        float w[4];
+        ln_load4(rrow + 4 * c, w);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[u][e] = v[u][e] + w[e];
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) sum += v[u][e];
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
+  const float mean = sum / (float)D;
+  float q = 0.f;
+#pragma unroll
+  for (int u = 0; u < PER; ++u) {
+    const int c = lane + 64 * u;
+    if (c < D4) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float d = v[u][e] - mean;
+        q += d * d;
+      }
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) q += __shfl_xor(q, o);
+  const float rstd = rsqrtf(q / (float)D + eps);
+  float *orow = out + row * D;
+#pragma unroll
+  for (int u = 0; u < PER; ++u) {
+    const int c = lane + 64 * u;
+    if (c < D4) {
+      float y[4] = {0.f, 0.f, 0.f, 0.f};
+      if (live) {
+        float g[4], b[4];
+        ln_load4(gamma + 4 * c, g);
+        ln_load4(beta + 4 * c, b);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) y[e] = (v[u][e] - mean) * rstd * g[e] + b[e];
+        ln_store4(orow + 4 * c, y);
+      }
+      h4 hh, ll;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        _Float16 a, b2;
+        f16x3_split1(y[e] * a_scale, a, b2);
+        hh[e] = a;
+        ll[e] = b2;
+      }
+      const int k = 4 * c, so = (((k >> 5) * 2) * 64 + rr + 16 * ((k & 31) >> 3)) * 8 + (k & 7);
+      *reinterpret_cast<h4 *>(stage + so) = hh;
+      *reinterpret_cast<h4 *>(stage + so + 512) = ll;
+    }
+  }
+  __syncthreads();
+  const int n16 = 4 * D;                               // 16-byte pieces of the row block's planes
+  uint4 *dst = reinterpret_cast<uint4 *>(ph + rb * (int64_t)(D >> 5) * 1024);
+  const uint4 *src = reinterpret_cast<const uint4 *>(stage);
+  for (int i = threadIdx.x; i < n16; i += 1024) dst[i] = src[i];
+}
+
 template <int PER>
 int launch_add_ln_split(const float *x, const float *r, int64_t r_rows, const float *g, const float *b, int64_t rows,
                         int D, float eps, float *out, float a_scale, _Float16 *ph, hipStream_t st) {
+  if (env_knob("CM_LN_RB", true)) {   // planes per 16-row block (CM_LN_RB=0: per-lane pieces, A/B)
+    const size_t lds = (size_t)64 * D;
+    if (lds > 64 * 1024)
+      CM_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&add_layernorm_split_rb_kernel<PER>),
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    hipLaunchKernelGGL((add_layernorm_split_rb_kernel<PER>), dim3((unsigned)ceil_div(rows, 16)), dim3(1024),
+                       lds, st, x, r, r_rows, g, b, rows, D, eps, out, a_scale, ph);
+    CM_HIP(hipGetLastError());
+    return CM_OK;
+  }
   const dim3 grid((unsigned)ceil_div(rows, kLnWaves)), block(64 * kLnWaves);
   hipLaunchKernelGGL((add_layernorm_kernel<float, PER, true>), grid, block, 0, st, x, r, r_rows, g, b, rows, D, eps,
                      out, a_scale, ph);
