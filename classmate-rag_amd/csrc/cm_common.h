@@ -155,6 +155,17 @@ __device__ inline void f16x3_split1(float a, _Float16 &h, _Float16 &l) {
   h = (_Float16)a;
   l = (_Float16)(a - (float)h);
 }
+// the same split of two values, returned as packed pairs (element a in the low half): the
+// conversions run as v_cvt_pk_f16_f32 (round to nearest even, like the scalar form: equal bits)
+__device__ inline void f16x3_split2(float a, float b, uint32_t &hi, uint32_t &lo) {
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+  const f2 v = {a, b};
+  const h2 h = __builtin_convertvector(v, h2);
+  const h2 l = __builtin_convertvector(v - __builtin_convertvector(h, f2), h2);
+  hi = __builtin_bit_cast(uint32_t, h);
+  lo = __builtin_bit_cast(uint32_t, l);
+}
 
 constexpr uint64_t kEmptyKey = ~0ull;
 constexpr int kMaxTopK = 256;

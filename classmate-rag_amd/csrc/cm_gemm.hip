@@ -191,16 +191,16 @@ __device__ __forceinline__ void k10_epilogue(g32x4 (&acc)[BMB / 2][BNB / (NW / 2
           if (row < M) Cout[row * N + col] = y;
         }
       } else {
-        uint32_t hh[4], ll[4];
+        float y[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          _Float16 h, l;
-          float y = acc[i][j][r] * out_scale + bv;
-          if constexpr (EPI == kEpiPlanesGelu) y = gelu_erf(y);
-          f16x3_split1(y * next_scale, h, l);
-          hh[r] = __builtin_bit_cast(uint16_t, h);
-          ll[r] = __builtin_bit_cast(uint16_t, l);
+          y[r] = acc[i][j][r] * out_scale + bv;
+          if constexpr (EPI == kEpiPlanesGelu) y[r] = gelu_erf(y[r]);
+          y[r] *= next_scale;
         }
+        uint32_t h01, l01, h23, l23;                  // rows 0-1 / 2-3 as packed (low, high) halves
+        f16x3_split2(y[0], y[1], h01, l01);
+        f16x3_split2(y[2], y[3], h23, l23);
         // QKV: the V third (columns >= 2N/3, whole 16-column blocks) goes out transposed for the
         // P V operand of planes_attention_kernel: per 32-row unit u and 16-column block d, a 2 KiB
         // block [hi][lo] whose lane slot (c, g) holds rows 4 g .. + 3 (e 0-3) and 16 + 4 g .. + 3
@@ -215,22 +215,22 @@ __device__ __forceinline__ void k10_epilogue(g32x4 (&acc)[BMB / 2][BNB / (NW / 2
             const int64_t rb = 2 * (rb16 >> 1) + dblk / nkbv;
             const int kb = 2 * nkbv + dblk % nkbv;
             const int64_t off = ((rb * (N >> 5) + kb) * 128 + c16 + 16 * g4) * 8 + 4 * (rb16 & 1);
-            *reinterpret_cast<uint2 *>(Cp + off) = make_uint2(hh[0] | hh[1] << 16, hh[2] | hh[3] << 16);
-            *reinterpret_cast<uint2 *>(Cp + off + 512) = make_uint2(ll[0] | ll[1] << 16, ll[2] | ll[3] << 16);
+            *reinterpret_cast<uint2 *>(Cp + off) = make_uint2(h01, h23);
+            *reinterpret_cast<uint2 *>(Cp + off + 512) = make_uint2(l01, l23);
             acc[i][j] = g32x4{0.f, 0.f, 0.f, 0.f};
             continue;
           }
         }
         // even lane keeps rows 0-1 and sends 2-3; odd lane keeps 2-3 and sends 0-1
-        const uint32_t sh = odd ? (hh[0] | hh[1] << 16) : (hh[2] | hh[3] << 16);
-        const uint32_t sl = odd ? (ll[0] | ll[1] << 16) : (ll[2] | ll[3] << 16);
+        const uint32_t sh = odd ? h01 : h23, sl = odd ? l01 : l23;
+        const uint32_t kh = odd ? h23 : h01, kl = odd ? l23 : l01;
         const uint32_t rh = (uint32_t)__builtin_amdgcn_mov_dpp((int)sh, 0xB1, 0xF, 0xF, false);
         const uint32_t rl = (uint32_t)__builtin_amdgcn_mov_dpp((int)sl, 0xB1, 0xF, 0xF, false);
         const int r0 = odd ? 2 : 0;
         const int c0 = col & ~1;
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
-          const uint32_t mine_h = hh[r0 + q], mine_l = ll[r0 + q];
+          const uint32_t mine_h = (kh >> (16 * q)) & 0xffffu, mine_l = (kl >> (16 * q)) & 0xffffu;
           const uint32_t oth_h = (rh >> (16 * q)) & 0xffffu, oth_l = (rl >> (16 * q)) & 0xffffu;
           // column c0 (even) in the low half, c0 + 1 in the high half
           const uint32_t wh = odd ? (oth_h | mine_h << 16) : (mine_h | oth_h << 16);
