@@ -544,6 +544,11 @@ static TileCfg pick_tile(int64_t M, int N, int n_cu) {
   // FFN-up (N = 3072): 192 x 192 measured 98.3 -> 90.5 us at M = 6144 (tools/k10_tiles.sh); the
   // other E5 shapes are faster at 96 x 192 (qkv 67 vs 75 us, o 25 vs 34, down 73 vs 95)
   if (N >= 3072 && N % 192 == 0 && ceil_div(M, 192) * (N / 192) >= n_cu) return TileCfg{12, 12};
+  // large batches (the passage encode, M = 65536 at the ingest shape): 192 x 192 for every projection
+  // once each CU has >= 4 tiles -- qkv 696 -> 667, o + down 485 -> 475 us per call there, ingest
+  // 6.96k -> 7.1k chunks/s (profiles/r05_k10_ingest_tile_ab.txt); the query batch (M = 6144) keeps
+  // 96 x 192
+  if (N % 192 == 0 && ceil_div(M, 192) * (N / 192) >= 4 * (int64_t)n_cu) return TileCfg{12, 12};
   // single short queries (M <= 32 rows, e.g. one retrieve() call): the GEMM is a weight stream spread
   // over N / (tile width) workgroups, so a 64 x 32 tile puts twice the CUs of 64 x 64 on it (the
   // per-element k order, hence every output bit, does not depend on the tile)
