@@ -25,7 +25,7 @@ def _case(M, K, N, seed, xs=1.0, ws=0.02):
 @pytest.mark.parametrize("M,K,N", [(6144, 768, 2304), (6144, 768, 768), (1000, 768, 3072), (37, 3072, 768),
                                    (1, 768, 64), (129, 64, 192), (20000, 768, 3072), (8192, 3072, 768),
                                    (9216, 768, 3072), (12288, 3072, 768), (8, 768, 2304), (24, 3072, 768),
-                                   (32, 768, 3072)])
+                                   (32, 768, 3072), (65536, 768, 768), (30000, 768, 2304)])
 def test_linear_f16x3_fp32_accuracy(M, K, N):
     import torch
     from classmate_hip import engine
@@ -237,7 +237,7 @@ def test_long_attention_split_matches_fp64(S, masked):
         assert float(((hs.double() + ls.double()) / 2.0 ** 8 - got).abs().max()) <= 2 * e32 + 2e-6
 
 
-@pytest.mark.parametrize("M", [6144, 1000, 96, 33])
+@pytest.mark.parametrize("M", [6144, 1000, 96, 33, 30000])
 def test_qkv_planes_epilogue_bits(M):
     """CM_EPI_PLANES_QKV (the fused QKV projection written for K9P) == the fp32 GEMM output split
     with cm_f16x3_split_rows, bit for bit: Q and K thirds in the standard planes, the V third in the
