@@ -562,6 +562,14 @@ __global__ void __launch_bounds__(64) short_attention_f16x3_kernel(const float *
       load_frag8(base + r * tok + d0, r < S, qx[t][st]);
       load_frag8(kb + r * tok + d0, r < S, kx[t][st]);
     }
+  // this lane's 8 keys (kk = 16 kt + 4 g + r): attended or not (the mask loads issued with the others,
+  // not between the two MFMA stages)
+  uint32_t kmask = 0;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int kk = 16 * (j >> 2) + 4 * g + (j & 3);
+    if (kk < S && (!key_mask || key_mask[b * S + kk] != 0)) kmask |= 1u << j;
+  }
   float mq = 0.f, mk = 0.f, mv = 0.f;
 #pragma unroll
   for (int t = 0; t < 2; ++t)
@@ -608,13 +616,6 @@ __global__ void __launch_bounds__(64) short_attention_f16x3_kernel(const float *
       sc[kt][it] = a;
     }
   const float lscale = scale / (sq * sk);  // exact: sq sk is a power of two
-  // this lane's 8 keys (kk = 16 kt + 4 g + r): attended or not
-  uint32_t kmask = 0;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int kk = 16 * (j >> 2) + 4 * g + (j & 3);
-    if (kk < S && (!key_mask || key_mask[b * S + kk] != 0)) kmask |= 1u << j;
-  }
   h16x8_t ph[2], pl[2];
 #pragma unroll
   for (int it = 0; it < 2; ++it) {
