@@ -75,6 +75,7 @@ SIGNATURES = {
     "cm_dense_workspace_wide_reranks": (c_i32, c_vp, c_i32, c_i32, c_vp),
     "cm_dense_last_wide_reranks": (c_i32, c_vp),
     "cm_dense_timing": (c_int, c_vp, c_i32),
+    "cm_dense_set_seed_event": (c_int, c_vp, c_vp),
     "cm_dense_timing_drain": (c_i32, c_vp, c_vp, c_i32),
     "cm_bm25_timing": (c_int, c_vp, c_i32),
     "cm_bm25_timing_drain": (c_i32, c_vp, c_vp, c_i32),

@@ -199,6 +199,13 @@ class DenseIndex:
         """Record HIP events around every search's scan kernel (see timing_drain)."""
         L.check(L.fn["cm_dense_timing"](self._h, int(bool(enable))), "cm_dense_timing")
 
+    def set_seed_event(self, event=None):
+        """Record ``event`` (a torch.cuda.Event, kept alive here; None clears) on the search stream right
+        after K1q's seed pass of every later batched search (cm_dense_set_seed_event)."""
+        self._seed_event = event
+        L.check(L.fn["cm_dense_set_seed_event"](self._h, event.cuda_event if event is not None else None),
+                "cm_dense_set_seed_event")
+
     def timing_drain(self, cap: int = 4096) -> list:
         """Synchronise on the recorded events -> per-launch scan-kernel times (ms)."""
         buf = np.zeros(cap, np.float32)

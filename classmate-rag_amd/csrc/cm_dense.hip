@@ -1355,6 +1355,7 @@ struct cm_dense {
   int32_t last_fallbacks = -1;             // K1c queries re-run exactly by the last host search
   int32_t last_wide = -1;                  // K1q queries finished by the wide re-rank in the last host search
   KernelTimer timer;                       // scan-kernel events (cm_dense_timing)
+  hipEvent_t seed_event = nullptr;         // cm_dense_set_seed_event: recorded after K1q's seed pass
   uint32_t *live = nullptr;
   hipStream_t stream = nullptr;
   int64_t mem_cur = 0, mem_peak = 0;       // device bytes of the four row arrays (cm_dense_mem_stats)
@@ -1948,6 +1949,7 @@ int launch_coarse(cm_dense *h, const float *q_dev, int nq, int k, int kind, cons
     hipLaunchKernelGGL(dense_seed_kernel, dim3(nq), dim3(256), 0, st, w.mins, c.n_wg_sample, c.qs, k, nq, w.qnorm,
                        h->rnorm, h->dim, w.seed, k1q_seed_q8() ? 0 : 1);
     CM_HIP(hipGetLastError());
+    if (h->seed_event) CM_HIP(hipEventRecord(h->seed_event, st));
     h->timer.begin(st);
     // deferred search (!run_exact): the caller runs other work beside it -> the shared LDS footprint
     // (CM_K1Q_SHARED_LDS=0: the full one, A/B)
@@ -2342,6 +2344,12 @@ int32_t cm_dense_workspace_wide_reranks(cm_dense *h, int32_t nq, int32_t k, cons
 }
 
 int32_t cm_dense_last_wide_reranks(cm_dense *h) { return h ? h->last_wide : -1; }
+
+int cm_dense_set_seed_event(cm_dense *h, void *event) {
+  if (!h) CM_FAIL(CM_EINVAL, "null handle");
+  h->seed_event = (hipEvent_t)event;
+  return CM_OK;
+}
 
 int cm_dense_timing(cm_dense *h, int32_t enable) {
   if (!h) CM_FAIL(CM_EINVAL, "null handle");

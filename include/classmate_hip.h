@@ -145,6 +145,10 @@ int32_t cm_dense_last_wide_reranks(cm_dense *h);
  * scan); _drain synchronises on them, writes up to cap elapsed ms values and
  * returns how many were recorded (< 0 on error).                         */
 int cm_dense_timing(cm_dense *h, int32_t enable);
+/* cm_dense_set_seed_event: a hipEvent_t (NULL clears) recorded on the search stream right after K1q's
+ * seed pass of every later batched search -- another stream can start work that should not compete
+ * with the seed pass for CUs (bench.py --bm25-gate 2).  The caller keeps the event alive. */
+int cm_dense_set_seed_event(cm_dense *h, void *event);
 int32_t cm_dense_timing_drain(cm_dense *h, float *ms_out, int32_t cap);
 int cm_dense_search_dev(cm_dense *h, const float *q_dev, int32_t nq, int32_t k, const uint32_t *allow_dev,
                         float *dist_dev, int64_t *row_dev, void *workspace_dev, int64_t workspace_bytes,
