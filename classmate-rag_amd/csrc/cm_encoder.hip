@@ -932,11 +932,13 @@ __global__ void __launch_bounds__(256) long_attention_f16x3_kernel(const float *
 // the host's rigorous bound): Q and K in the standard layout, V transposed in 32-key units whose
 // lane slots are already in the permuted key order of the P V operand (k10_epilogue).  So every
 // fragment of the attention is a 1 KiB block of HBM: no fp32 loads, no maxima, no split work.  One
-// workgroup of up to 16 waves (16 queries each) per (sequence, head, 256-query block) -- at S = 256
-// the keys and values of a head are read once -- the 64-key chunks stream through a two-slot LDS
-// ring by LDS-DMA (32 one-KiB pieces per chunk, the next chunk in flight while this one is
-// consumed, one barrier per chunk).  Per chunk and wave: the same 48 MFMAs and online softmax as
-// K9L; the context is written as planes of o * a_scale with K10's DPP pair stores.  S % 64 == 0.
+// workgroup of K9P_WAVES = 8 waves (16 queries each) per (sequence, head, 128-query block), two per
+// CU, the query blocks of a (sequence, head) on one XCD (its keys and values come from that L2 for
+// the second); the 64-key chunks stream through a two-slot LDS ring by LDS-DMA (32 one-KiB pieces
+// per chunk, the next chunk in flight while this one is consumed, one barrier per chunk).  Per chunk
+// and wave: K9L's 48 MFMAs, the online softmax in the log2 domain; the context is written as planes
+// of o * a_scale with K10's DPP pair stores.  S % 64 == 0.  Ingest shape: 247 us per layer (K9L 496;
+// 16 waves per workgroup: 281), profiles/r05_k9p_ab.txt.
 constexpr int kApSlot = 32 * 1024;  // one chunk: K 16 KiB + V 16 KiB
 #ifndef K9P_WAVES
 #define K9P_WAVES 8                 // waves (16 queries each) per workgroup: 8 or 16 (A/B)
@@ -1249,7 +1251,7 @@ extern "C" int cm_planes_attention(const void *qkv_planes, int32_t B, int32_t S,
   if (!(s_qkv > 0.f) || !(a_scale > 0.f)) CM_FAIL(CM_EINVAL, "scales must be > 0");
   if (((uintptr_t)qkv_planes & 15) || ((uintptr_t)planes_dev & 15)) CM_FAIL(CM_EINVAL, "planes must be 16-byte aligned");
   // 8 waves (128 queries) per workgroup: two resident per CU (LDS 2 x 64 KiB, 4 waves per SIMD), so one
-  // workgroup's first DMA and epilogue overlap the other's chunks (16 waves: 281 vs ... us per layer)
+  // workgroup's first DMA and epilogue overlap the other's chunks (247 vs 281 us per layer at 16 waves)
   const int nw = std::min(K9P_WAVES, S / 16);
   const int64_t blocks = ceil_div((int64_t)B * H, 8) * 8 * ((S + 16 * nw - 1) / (16 * nw));
   if (blocks > INT32_MAX) CM_FAIL(CM_EINVAL, "too many (sequence, head, query block) workgroups");
