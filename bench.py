@@ -204,6 +204,7 @@ def main():
     log(f"dense shard {N}x{D} fp32 ready ({time.perf_counter() - t_setup:.1f}s)")
 
     bm25 = None
+    tokens_host = None
     if args.mode == "hybrid":
         tokens, doc_off = gen_tokens(N, args.vocab, args.zipf, args.avg_len, seed=args.seed * 1000 + 500 + rank)
         bm25 = engine.BM25Index(device=local)
@@ -220,6 +221,8 @@ def main():
             torch.distributed.broadcast(qt, src=0)
         q_terms = qt.reshape(-1).contiguous()
         q_off = (torch.arange(B + 1, device=dev, dtype=torch.int32) * args.q_terms).contiguous()
+        if args.cpu_baseline:    # the recall leg's oracle builds its own CSR from these
+            tokens_host = (tokens.cpu().numpy(), doc_off.cpu().numpy())
         del tokens, doc_off
         torch.cuda.empty_cache()
         log(f"bm25 shard: {bm25.num_postings} postings, V={args.vocab} ({time.perf_counter() - t_setup:.1f}s)")
@@ -549,7 +552,8 @@ def main():
     }
     if args.cpu_baseline and args.mode == "hybrid":
         cpu, recall = cpu_baseline_and_recall(args, dense, bm25, res, q_terms, q_main, rank, ws, row0, N,
-                                              lists_main)
+                                              lists_main, tokens_host)
+        tokens_host = None
         out["cpu_baseline"] = cpu
         out["recall_at_10"] = recall
     else:
@@ -818,7 +822,8 @@ def _pmc_traffic(args, which, batch=None):
 
 
 # ---------------------------------------------------------------------------
-def cpu_baseline_and_recall(args, dense, bm25, res, q_terms, q_dev, rank, ws, row0, N, gpu_lists=None):
+def cpu_baseline_and_recall(args, dense, bm25, res, q_terms, q_dev, rank, ws, row0, N, gpu_lists=None,
+                            tokens_host=None):
     """Time the CPU oracle on a bounded sample of the step's queries (its query embeddings) over
     every rank's shard (each rank scans its own, in parallel), merge the per-shard exact lists
     (a merge of exact per-shard top lists is the exact global list), run MMR + RRF on the merged
@@ -836,19 +841,39 @@ def cpu_baseline_and_recall(args, dense, bm25, res, q_terms, q_dev, rank, ws, ro
     qt = q_terms.view(args.batch, -1)[:Qc].cpu().numpy()
     gpu_keys = res[0][:Qc].cpu().numpy()
     threads = max(corc.num_threads(), torch.get_num_threads())
-    # BM25 statistics: global (build-time, not timed)
+    # BM25 statistics: global (build-time, not timed).  The oracle scores its OWN CSR, built on the
+    # host from the shard's tokens (oracle/cm_oracle.c orc_build_csr), not the device index K7 built;
+    # the device index is compared with it array for array first
     t = time.perf_counter()
     csr = bm25.export()
-    term_off = csr["term_off"]
-    df = np.diff(term_off)
-    first = np.full(df.shape[0], np.uint64(0xFFFFFFFFFFFFFFFF))
-    nz = df > 0
-    fp = term_off[:-1][nz]
-    first[nz] = (csr["post_doc"][fp].astype(np.uint64) << np.uint64(32)) | csr["post_pos"][fp].astype(np.uint64)
-    ccsr = dict(term_off=term_off, post_doc=csr["post_doc"], post_tf=csr["post_tf"], dl=csr["dl"],
-                vocab=int(df.shape[0]), ndocs=int(csr["dl"].shape[0]))
+    if tokens_host is not None:
+        ocsr = corc.build_csr(tokens_host[0], tokens_host[1], bm25.vocab)
+        same = all(np.array_equal(csr[k], ocsr[k]) for k in ("term_off", "post_doc", "post_tf", "dl"))
+        odf = np.diff(ocsr["term_off"])
+        nz = odf > 0
+        fp0 = ocsr["term_off"][:-1][nz]
+        if same:
+            same = np.array_equal(ocsr["first_key"][nz], (csr["post_doc"][fp0].astype(np.uint64) << np.uint64(32))
+                                  | csr["post_pos"][fp0].astype(np.uint64))
+        csr_source = ("oracle CSR built on the host from the shard's tokens; device index (K7) "
+                      + ("== it, array for array" if same else "DIFFERS from it"))
+        term_off, df, first = ocsr["term_off"], ocsr["df"], ocsr["first_key"]
+        ccsr = dict(term_off=term_off, post_doc=ocsr["post_doc"], post_tf=ocsr["post_tf"], dl=ocsr["dl"],
+                    vocab=int(df.shape[0]), ndocs=int(ocsr["dl"].shape[0]))
+        del ocsr
+    else:
+        csr_source = "device index export (K7 build)"
+        term_off = csr["term_off"]
+        df = np.diff(term_off)
+        first = np.full(df.shape[0], np.uint64(0xFFFFFFFFFFFFFFFF))
+        nz = df > 0
+        fp = term_off[:-1][nz]
+        first[nz] = (csr["post_doc"][fp].astype(np.uint64) << np.uint64(32)) | csr["post_pos"][fp].astype(np.uint64)
+        ccsr = dict(term_off=term_off, post_doc=csr["post_doc"], post_tf=csr["post_tf"], dl=csr["dl"],
+                    vocab=int(df.shape[0]), ndocs=int(csr["dl"].shape[0]))
+    del csr
     n_docs = ccsr["ndocs"]
-    sum_len = int(csr["dl"].astype(np.int64).sum())
+    sum_len = int(ccsr["dl"].astype(np.int64).sum())
     if ws == 1:
         idf, _ = corc.bm25_idf(df, first, n_docs)
         gn, gsum = n_docs, sum_len
@@ -856,7 +881,7 @@ def cpu_baseline_and_recall(args, dense, bm25, res, q_terms, q_dev, rank, ws, ro
         gdf, gfk, gn, gsum = parallel.allreduce_bm25_stats(df, first, row0, n_docs, sum_len)
         idf, _ = parallel.bm25_idf_table(gdf, gfk, gn)
     avgdl = float(gsum) / gn
-    log(f"cpu baseline: shard CSR exported, global statistics ({time.perf_counter() - t:.1f}s)")
+    log(f"cpu baseline: {csr_source}; global statistics ({time.perf_counter() - t:.1f}s)")
 
     # dense: exact fp64 top-P over this shard, chunk by chunk (fp32 BLAS scan for candidates, fp64
     # re-rank of 4P per chunk; export of each chunk not timed)
@@ -941,7 +966,7 @@ def cpu_baseline_and_recall(args, dense, bm25, res, q_terms, q_dev, rank, ws, ro
                       f"fp32 BLAS scan + fp64 re-rank per 1M-row chunk; BM25: oracle/cm_oracle.c OpenMP with the "
                       f"global statistics; MMR/RRF: oracle/ref_semantics.py; E5 encode excluded); value = one host "
                       f"doing every shard's scan in turn",
-               seconds=total, per_shard_s=shard_s,
+               seconds=total, per_shard_s=shard_s, bm25_csr=csr_source,
                breakdown_s=dict(dense=sum(x["t_dense"] for x in allv), bm25=sum(x["t_bm25"] for x in allv),
                                 mmr_rrf=t_fuse))
     log(f"cpu baseline {cpu['value']:.2f} q/s ({threads} threads per shard, {ws} shards); recall@10 {recall:.4f}")

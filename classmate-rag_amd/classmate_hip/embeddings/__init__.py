@@ -173,12 +173,16 @@ class E5MultilingualEmbedder:
             self.model = _model.to(self.device, self.dtype).eval()
             self.tokenizer = _tokenizer
             self._graphs = {}
+            self._enc_lock = threading.RLock()
             with _LOADED_LOCK:
                 _LOADED.setdefault(key, self)
             return
         self.model = _model.to(self.device, self.dtype).eval()
         self.tokenizer = _tokenizer
         self._graphs = {}
+        # one encode at a time per model (instances attached by name share it): the lean forward,
+        # the small-batch graphs and their input / output buffers are built once and shared
+        self._enc_lock = threading.RLock()
 
     def _key(self, model_name: str):
         return (str(model_name), str(self.device), str(self.dtype), self.normalize)
@@ -253,7 +257,7 @@ class E5MultilingualEmbedder:
         import torch
         if os.environ.get("CM_E5_LEAN", "1") == "0":
             return self._encode_hf(input_ids, attention_mask, out=out)
-        with torch.inference_mode():
+        with self._enc_lock, torch.inference_mode():
             fwd = self._lean_forward()
             g = self._small_batch_graph(input_ids, attention_mask)
             if g is not None:
@@ -300,7 +304,9 @@ class E5MultilingualEmbedder:
             torch.cuda.current_stream(ids.device).wait_stream(side)
             graph = torch.cuda.CUDAGraph()
             try:
-                with torch.cuda.graph(graph):
+                # thread_local: other threads' HIP calls (another store's search) do not invalidate
+                # this capture, and nothing of theirs is captured (the capture stream is private)
+                with torch.cuda.graph(graph, capture_error_mode="thread_local"):
                     run()
             except RuntimeError as e:   # capture refused: the eager forward from now on, said once
                 self._small_graph_failed = True
@@ -567,6 +573,10 @@ class E5MultilingualEmbedder:
         and runs them as ONE forward when the rows are provably batch-independent
         (``_rows_independent``); otherwise the group is cut back into the reference's batches
         (each trimmed to its own longest row, exactly what tokenizing that batch alone gives)."""
+        with self._enc_lock:
+            return self._encode_dev_locked(texts, batch_size, group)
+
+    def _encode_dev_locked(self, texts, batch_size, group):
         import torch
         out = torch.empty((len(texts), self.model.config.hidden_size), dtype=torch.float32, device=self.device)
         if not texts:

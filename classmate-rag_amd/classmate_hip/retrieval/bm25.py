@@ -23,6 +23,9 @@ record.  A missing or stale sidecar falls back to the reference's full parse.
 """
 from __future__ import annotations
 
+import contextlib
+import dataclasses
+import functools
 import json
 import os
 import shutil
@@ -67,6 +70,7 @@ class _Catalog(dict):
         super().__init__()
         self._src = None  # (jsonl path, line byte offsets, CSR term ids, doc offsets)
         self._fh = None
+        self._lock = threading.Lock()   # the shared file object: seek + read as a unit
 
     def attach(self, path: Path, ids: Sequence[str], line_off, term_ids, doc_off) -> None:
         self._src = (path, line_off, term_ids, doc_off)
@@ -85,10 +89,12 @@ class _Catalog(dict):
 
     def _parse(self, row: int) -> _Entry:
         path, line_off = self._src[0], self._src[1]
-        if self._fh is None:
-            self._fh = open(path, "rb")
-        self._fh.seek(int(line_off[row]))
-        return self._finish(row, json.loads(self._fh.read(int(line_off[row + 1] - line_off[row]))))
+        with self._lock:
+            if self._fh is None:
+                self._fh = open(path, "rb")
+            self._fh.seek(int(line_off[row]))
+            blob = self._fh.read(int(line_off[row + 1] - line_off[row]))
+        return self._finish(row, json.loads(blob))
 
     def __getitem__(self, key):
         v = dict.__getitem__(self, key)
@@ -117,9 +123,10 @@ class _Catalog(dict):
         self.detach()
 
     def detach(self) -> None:
-        if self._fh is not None:
-            self._fh.close()
-        self._src = self._fh = None
+        with self._lock:
+            if self._fh is not None:
+                self._fh.close()
+            self._src = self._fh = None
 
     def values(self):
         self.materialize()
@@ -152,6 +159,9 @@ class _BState:
         self.sig = None                    # the JSONL (+ sidecar) signature it was loaded from / saved to
         self.unsaved = False               # mutated since: private to its holder
         self.holders = weakref.WeakValueDictionary()   # id(store) -> store (dataclasses are unhashable)
+        # serialises the state's users (stores attached to it, threads): the device handle's search
+        # staging and workspace are per handle (SURVEY §8(b) Threading)
+        self.lock = threading.RLock()
 
     def clone(self) -> "_BState":
         """A private copy for a holder that mutates a shared state (the reference's instances are
@@ -159,7 +169,11 @@ class _BState:
         on demand."""
         st = _BState()
         cat = _Catalog()
-        dict.update(cat, dict.items(self.entries))
+        # the clone's own _Entry objects: term ids are filled in lazily against the holder's vocab
+        # (_ensure_index / save), so shared entries would carry the other state's ids (ADVICE r5);
+        # pending records (ints: not parsed yet) are parsed by each catalog on its own
+        dict.update(cat, ((k, v if type(v) is int else dataclasses.replace(v))
+                          for k, v in dict.items(self.entries)))
         cat._src = self.entries._src if isinstance(self.entries, _Catalog) else None
         st.entries = cat
         st.id_list = list(self.id_list)
@@ -235,6 +249,23 @@ def _proxy(name: str):
     return property(lambda self: getattr(self._st, name), lambda self, v: setattr(self._st, name, v))
 
 
+@contextlib.contextmanager
+def _store_lock(store):
+    """This store's lock, then its current state's: the first serialises the threads that use one
+    BM25Store object (a copy on write swaps its state), the second the stores sharing a state."""
+    with store._obj_lock:
+        with store._st.lock:
+            yield
+
+
+def _locked(fn):
+    @functools.wraps(fn)
+    def run(self, *a, **kw):
+        with _store_lock(self):
+            return fn(self, *a, **kw)
+    return run
+
+
 @dataclass
 class BM25Store:
     index_dir: Optional[Path] = Path("./indexes/bm25")
@@ -253,8 +284,13 @@ class BM25Store:
     _uid = _proxy("uid")
 
     def __post_init__(self):
+        self._obj_lock = threading.RLock()
         self._st = _BState()
         self._st.holders[id(self)] = self
+
+    def lock(self):
+        """This store's locks as one context (HybridRetriever holds it across a whole retrieve)."""
+        return _store_lock(self)
 
     def _set_state(self, st: "_BState") -> None:
         self._st.holders.pop(id(self), None)
@@ -317,6 +353,7 @@ class BM25Store:
             self._meta.set(r, self._entries[i].metadata)
         self._meta_dirty = False
 
+    @_locked
     def upsert_many(self, *, ids: Sequence[str], texts: Sequence[str], metadatas: Sequence[Mapping[str, Any]]) -> None:
         """bm25.py:147-166: language from metadata (or detected), tokenize, replace in place."""
         if not (len(ids) == len(texts) == len(metadatas)):
@@ -333,6 +370,7 @@ class BM25Store:
             self._entries[doc_id] = _Entry(id=doc_id, text=text, tokens=toks, metadata=meta)
         self._rebuild()
 
+    @_locked
     def delete_many(self, ids: Sequence[str]) -> None:
         self._mutating()
         for doc_id in ids:
@@ -349,6 +387,7 @@ class BM25Store:
         """bm25.py:175-212 on the GPU."""
         return self.search_batch(queries=[query], where=where, top_k=top_k)[0]
 
+    @_locked
     def search_batch(self, *, queries: Sequence[str], where: Optional[Mapping[str, Any]] = None,
                      top_k: int = 8) -> List[List[Dict[str, Any]]]:
         """Many queries sharing one filter: one device launch (build-side addition)."""
@@ -392,6 +431,7 @@ class BM25Store:
     def sidecar_dir(self) -> Path:
         return Path(self.index_dir) / (self.index_file + ".cm")
 
+    @_locked
     def save(self) -> None:
         """bm25.py:220-231 (same JSONL records) + the binary sidecar of the device index."""
         if self.index_dir is None:
@@ -490,6 +530,7 @@ class BM25Store:
             self._meta, self._meta_dirty = meta, False
         return True
 
+    @_locked
     def load(self) -> None:
         """bm25.py:233-248; through the sidecar when it matches the JSONL.  A state this process
         already holds for the same file -- loaded or saved by another BM25Store, unchanged since on

@@ -11,6 +11,7 @@ queries -- single or batched, filtered or not -- stay on the device end to end
 """
 from __future__ import annotations
 
+import contextlib
 import os
 from dataclasses import dataclass
 from typing import Any, Dict, List, Mapping, Optional, Sequence
@@ -54,6 +55,21 @@ def _mmr_order(q: np.ndarray, cands: np.ndarray, ids: List[str], k: int, lambd: 
     order = engine.mmr_order_batch(np.asarray(q, np.float32).reshape(1, -1), cands[None], int(k), float(lambd),
                                    n_valid=np.array([len(ids)], np.int32))
     return [int(x) for x in order[0] if x >= 0]
+
+
+@contextlib.contextmanager
+def _stores_locked(retr):
+    """The vector store's collection lock, then the BM25 store's (always in this order, so two
+    retrievers sharing a store cannot deadlock), held across one retrieve: concurrent callers --
+    each ask_question thread building its own stores on one directory -- are serialised on the
+    handles they share (SURVEY §8(b) Threading; rag/pipeline/rag.py:531-534).  Stores without a
+    ``lock()`` (the reference's own classes) are not locked."""
+    with contextlib.ExitStack() as stack:
+        for s in (retr.vector_store, retr.bm25_store):
+            lk = getattr(s, "lock", None)
+            if callable(lk):
+                stack.enter_context(lk())
+        yield
 
 
 def _vd_term(item) -> float:
@@ -162,6 +178,10 @@ class HybridRetriever:
 
     def retrieve(self, *, question: str, filters: Optional[Mapping[str, object]] = None, top_k: int = 8,
                  hybrid: bool = True) -> List[Dict[str, object]]:
+        with _stores_locked(self):
+            return self._retrieve(question, filters, top_k, hybrid)
+
+    def _retrieve(self, question, filters, top_k, hybrid):
         raw_filters = filters or {}
         if os.environ.get("CM_RETRIEVE_DEVICE", "1") != "0" and device_batch.applicable(self, raw_filters, hybrid):
             # the device chain of retrieve_batch for a batch of one (equal dicts: tests/test_gpu_dropin.py)
@@ -181,6 +201,10 @@ class HybridRetriever:
     # ---- batched: one device launch per stage for the whole batch -----------------
     def retrieve_batch(self, *, questions: Sequence[str], filters: Optional[Mapping[str, object]] = None,
                        top_k: int = 8, hybrid: bool = True) -> List[List[Dict[str, object]]]:
+        with _stores_locked(self):
+            return self._retrieve_batch(questions, filters, top_k, hybrid)
+
+    def _retrieve_batch(self, questions, filters, top_k, hybrid):
         questions = list(questions)
         if not questions:
             return []

@@ -35,6 +35,7 @@ insertion order and re-upserting an id overwrites its row in place.
 """
 from __future__ import annotations
 
+import functools
 import json
 import os
 import shutil
@@ -74,6 +75,10 @@ class _State:
         self.unsaved = False        # changed without a write (autosave=False): not attachable
         self.line_off = None        # per row: byte offset of its latest record in rows.log.jsonl
         self.tail = 0               # records appended since the last snapshot
+        # serialises every use of the collection -- its host tables and its device handle (whose
+        # search staging buffers and workspace are per handle) -- across the stores attached to it
+        # and the threads using them (SURVEY §8(b) Threading)
+        self.lock = threading.RLock()
 
 
 def _disk_sig(d: Optional[Path]):
@@ -106,18 +111,30 @@ def _proxy(name: str):
     return property(lambda self: getattr(self._st, name), lambda self, v: setattr(self._st, name, v))
 
 
+def _locked(fn):
+    """Run a GpuVectorStore method under its collection's lock (_State.lock, reentrant)."""
+    @functools.wraps(fn)
+    def run(self, *a, **kw):
+        with self._st.lock:
+            return fn(self, *a, **kw)
+    return run
+
+
 class _LazyRecords:
     """Parses row r's log record (the document and metadata of a row opened from the snapshot)
     on first access, by its byte offset in rows.log.jsonl."""
 
     def __init__(self, path: Path, st: "_State"):
         self.path, self.st, self.fh = path, st, None
+        self._lock = threading.Lock()      # one file object: seek + readline as a unit
 
     def parse(self, r: int):
-        if self.fh is None:
-            self.fh = open(self.path, "rb")
-        self.fh.seek(int(self.st.line_off[r]))
-        rec = json.loads(self.fh.readline())
+        with self._lock:
+            if self.fh is None:
+                self.fh = open(self.path, "rb")
+            self.fh.seek(int(self.st.line_off[r]))
+            line = self.fh.readline()
+        rec = json.loads(line)
         live = rec.get("id") is not None
         return (rec.get("document") if live else None), (rec.get("metadata") if live else None)
 
@@ -231,6 +248,7 @@ class GpuVectorStore:
     def _dir(self) -> Optional[Path]:
         return None if self.persist_dir is None else self.persist_dir / self.collection_name
 
+    @_locked
     def _ensure_loaded(self):
         if self._loaded:
             return
@@ -288,12 +306,15 @@ class GpuVectorStore:
                 del row_[old]
             ids_[r] = _id
             docs_[r] = rec.get("document") if _id is not None else None
-            st.line_off[r] = off
+            # the old metadata first: MetaIndex.set / remove read metas[r], which for a snapshot row
+            # is parsed lazily through line_off[r] -- it must still point at the OLD record, or the
+            # columns and tags only the old metadata had keep their codes on a live row
             if _id is not None:
                 row_[_id] = r
                 meta_.set(r, rec.get("metadata"))
             else:
                 meta_.remove(r)
+            st.line_off[r] = off
         self._index = engine.DenseIndex(dim, device=self.device, capacity=max(n, 1))
         self._version += 1
         live = np.fromiter((i is not None for i in ids_), bool, count=n) if n else np.zeros(0, bool)
@@ -390,6 +411,7 @@ class GpuVectorStore:
         os.replace(tmp, d / "snapshot")
         self._st.tail = 0
 
+    @_locked
     def save(self):
         """Full write from the device copy + a compacted log (one record per row) + the snapshot."""
         d = self._dir
@@ -423,6 +445,7 @@ class GpuVectorStore:
         self._changed(True)
 
     # ---- upsert (vector_chroma.py:168-200) ---------------------------------
+    @_locked
     def upsert(self, *, ids: Sequence[str], documents: Sequence[str], metadatas: Sequence[Mapping[str, Any]],
                embeddings: np.ndarray, batch_size: int = 512) -> None:
         if len(ids) != len(documents) or len(ids) != len(metadatas) or len(ids) != len(embeddings):
@@ -457,6 +480,7 @@ class GpuVectorStore:
             self._append(rows, emb)
         self._changed(self.autosave)
 
+    @_locked
     def delete(self, ids: Sequence[str]) -> None:
         """col.delete(ids=...) (vector_chroma.py:181-187); unknown ids are ignored."""
         self._ensure_loaded()
@@ -506,6 +530,7 @@ class GpuVectorStore:
             out.append(item)
         return out
 
+    @_locked
     def query(self, *, query_embeddings: np.ndarray, where: Optional[Dict[str, Any]] = None, top_k: int = 8,
               include_documents: bool = True, include_embeddings: bool = False) -> List[Dict[str, Any]]:
         q = np.asarray(query_embeddings).astype("float32")
@@ -518,6 +543,7 @@ class GpuVectorStore:
         vecs = res[2] if include_embeddings else None
         return self._items(dist, rows, vecs, 0, include_documents, include_embeddings, copy=True)
 
+    @_locked
     def query_batch(self, *, query_embeddings: np.ndarray, where: Optional[Dict[str, Any]] = None, top_k: int = 8,
                     include_documents: bool = True, include_embeddings: bool = False) -> List[List[Dict[str, Any]]]:
         q = np.atleast_2d(np.asarray(query_embeddings).astype("float32"))
@@ -531,6 +557,7 @@ class GpuVectorStore:
         return [self._items(dist, rows, vecs, i, include_documents, include_embeddings) for i in range(q.shape[0])]
 
     # ---- admin ------------------------------------------------------------------
+    @_locked
     def count(self) -> int:
         self._ensure_loaded()
         try:
@@ -538,6 +565,7 @@ class GpuVectorStore:
         except Exception:
             return 0
 
+    @_locked
     def reset_collection(self) -> None:
         self._ensure_loaded()
         if self._index is not None:
@@ -557,6 +585,10 @@ class GpuVectorStore:
         return cls(persist_dir=Path(os.getenv("CHROMA_PERSIST_DIRECTORY", "./indexes/chroma") or "./indexes/chroma"),
                    collection_name=os.getenv("CHROMA_COLLECTION_NAME", "classmate_rag") or "classmate_rag",
                    distance="cosine")
+
+    def lock(self):
+        """The collection's lock (reentrant): HybridRetriever holds it across a whole retrieve."""
+        return self._st.lock
 
     # rows <-> ids for the batched device pipeline
     def id_of(self, row: int) -> Optional[str]:

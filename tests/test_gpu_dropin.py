@@ -471,6 +471,46 @@ def test_vector_store_snapshot_cold_open(corpus, tmp_path, monkeypatch, refresh)
                 assert all(np.array_equal(x["embedding"], y["embedding"]) for x, y in zip(a, b))
 
 
+def test_vector_store_cold_open_replaces_old_metadata(corpus, tmp_path):
+    """rows re-upserted after the snapshot with metadata that has OTHER keys and
+    tags must lose every old column code and tag on a cold open -- the replay has to resolve the
+    old (snapshot) record before it moves the row's log offset to the new one."""
+    from classmate_hip.retrieval import GpuVectorStore
+    _new_process()
+    n = 300
+    ids, emb = corpus["ids"][:n], corpus["emb"][:n]
+    old = [{"course": "cs101", "unit": "u1", "language": "en", "tags": ["exam", "old"], "tag_exam": True}
+           for _ in range(n)]
+    vs = GpuVectorStore(persist_dir=tmp_path)
+    vs.upsert(ids=ids, documents=corpus["texts"][:n], metadatas=old, embeddings=emb)
+    d = tmp_path / "classmate_rag"
+    assert (d / "snapshot" / "info.json").exists()
+    moved = ids[:100]
+    new = [{"doc_type": "pdf", "tags": ["fresh"], "tag_fresh": True} for _ in moved]
+    vs.upsert(ids=moved, documents=["moved"] * len(moved), metadatas=new, embeddings=emb[:100])
+    info = __import__("json").loads((d / "snapshot" / "info.json").read_text())
+    assert int(info["log_size"]) < (d / "rows.log.jsonl").stat().st_size   # the re-upserts are the tail
+    wheres_chroma = [{"course": "cs101"}, {"tag_exam": True}, {"tag_fresh": True}, {"doc_type": "pdf"},
+                     {"$and": [{"unit": "u1"}, {"language": "en"}]}]
+    wheres_bm25 = [{"course": "cs101"}, {"tags": {"$contains": "exam"}}, {"tags": {"$contains": "fresh"}},
+                   {"course": None}, {"doc_type": "pdf"}]
+    _new_process()
+    again = GpuVectorStore(persist_dir=tmp_path)
+    again._ensure_loaded()
+    for w in wheres_chroma:
+        assert np.array_equal(again._meta.chroma_mask(w), vs._meta.chroma_mask(w)), w
+    for w in wheres_bm25:
+        assert np.array_equal(again._meta.bm25_mask(w), vs._meta.bm25_mask(w)), w
+    assert not again._meta.chroma_mask({"course": "cs101"})[:100].any()
+    assert sorted(again._meta.tags.get("exam", ())) == list(range(100, n))
+    for w in wheres_chroma:
+        for q in corpus["qvecs"][:3]:
+            a = vs.query(query_embeddings=q, where=w, top_k=10)
+            b = again.query(query_embeddings=q, where=w, top_k=10)
+            assert [(r["id"], r["metadata"], r["distance"]) for r in a] == \
+                [(r["id"], r["metadata"], r["distance"]) for r in b], w
+
+
 def test_construct_per_call_attaches_and_sees_upserts(corpus, tmp_path):
     """the reference's ask_question builds its stores and embedder on every call
     (rag/pipeline/rag.py:531-545).  Constructions on the same directories / model attach to the

@@ -199,6 +199,9 @@ def test_hybrid_10m_sample():
     bm.build_dev(tokens, doc_off, 1 << 20)
     torch.cuda.synchronize()
     qt = bench.sample_query_terms(tokens, doc_off, B, 8, seed=10)
+    # the oracle's own CSR from the same tokens (the BM25 check must not score the
+    # index K7 built on the GPU): compared with the device index below, then scored on its own
+    tok_h, off_h = tokens.cpu().numpy(), doc_off.cpu().numpy()
     del tokens, doc_off
     torch.cuda.empty_cache()
     C = dense.export()                                              # host copy (30.7 GB)
@@ -223,19 +226,26 @@ def test_hybrid_10m_sample():
         finally:
             dense.set_path(0)
         check_dense(d_s, r_s, o_d[:16], o_r[:16], P)
-    # BM25 bit-exact vs the C oracle
+    # BM25 bit-exact vs the C oracle, on the oracle's own CSR (built on the host from the tokens):
+    # first the device index K7 built must equal it array for array, then the oracle scores with
+    # its own CSR and statistics (bm25.py:140-145,186-200 restated; nothing taken from the GPU)
+    ocsr = corc.build_csr(tok_h, off_h, 1 << 20)
+    del tok_h, off_h
     csr = bm.export()
-    term_off = csr["term_off"]
-    df = np.diff(term_off)
-    first = np.full(df.shape[0], np.uint64(0xFFFFFFFFFFFFFFFF))
+    assert np.array_equal(csr["term_off"], ocsr["term_off"])
+    assert np.array_equal(csr["post_doc"], ocsr["post_doc"]) and np.array_equal(csr["post_tf"], ocsr["post_tf"])
+    assert np.array_equal(csr["dl"], ocsr["dl"])
+    df = np.diff(ocsr["term_off"])
     nz = df > 0
-    fp = term_off[:-1][nz]
-    first[nz] = (csr["post_doc"][fp].astype(np.uint64) << np.uint64(32)) | csr["post_pos"][fp].astype(np.uint64)
-    ccsr = dict(term_off=term_off, post_doc=csr["post_doc"], post_tf=csr["post_tf"], dl=csr["dl"],
-                vocab=int(df.shape[0]), ndocs=N)
-    idf, _ = corc.bm25_idf(df, first, N)
+    fp = ocsr["term_off"][:-1][nz]
+    dev_first = (csr["post_doc"][fp].astype(np.uint64) << np.uint64(32)) | csr["post_pos"][fp].astype(np.uint64)
+    assert np.array_equal(dev_first, ocsr["first_key"][nz]) and np.array_equal(ocsr["df"], df)
+    del csr
+    ccsr = dict(term_off=ocsr["term_off"], post_doc=ocsr["post_doc"], post_tf=ocsr["post_tf"], dl=ocsr["dl"],
+                vocab=int(ocsr["vocab"]), ndocs=N)
+    idf, _ = corc.bm25_idf(ocsr["df"], ocsr["first_key"], N)
     queries = qt[:NCHK].cpu().numpy().tolist()
-    o_sc, o_rw = corc.bm25_topk(ccsr, idf, float(csr["dl"].astype(np.int64).sum()) / N, queries, K)
+    o_sc, o_rw = corc.bm25_topk(ccsr, idf, float(ocsr["dl"].astype(np.int64).sum()) / N, queries, K)
     for nb, (_, _, bs, br, _) in runs.items():
         m = min(nb, NCHK)
         assert np.array_equal(br[:m], o_rw[:m]) and np.array_equal(bs[:m], o_sc[:m]), nb

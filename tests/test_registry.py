@@ -98,6 +98,39 @@ def test_bm25_attached_state_searches_like_a_fresh_load(tmp_path):
     assert [s2._entries[i].metadata for i in ids] == [s3._entries[i].metadata for i in ids]
 
 
+def test_bm25_clone_owns_its_entries(tmp_path):
+    """a JSONL the reference wrote (no sidecar: term ids are assigned lazily
+    against each state's vocabulary), two stores attached to it, one mutating before any search or
+    save.  The copy on write must not share _Entry objects, or the first state to assign term ids
+    writes them in its own vocabulary into the other's entries."""
+    import numpy as np
+    B.release_all()
+    d = tmp_path / "bm25"
+    d.mkdir()
+    ids, texts, metas = _docs(12, "r")
+    with open(d / "bm25_index.jsonl", "w", encoding="utf-8") as f:
+        for i, t, m in zip(ids, texts, metas):
+            f.write(json.dumps({"id": i, "text": t, "tokens": B._tokenize(t, lang_hint="en"), "metadata": m}) + "\n")
+    s1 = B.BM25Store.load_or_create(d)
+    s2 = B.BM25Store.load_or_create(d)
+    assert s1._st is s2._st
+    s1.delete_many([ids[0]])                     # s1's vocabulary now starts at the second document
+    s1.upsert_many(ids=["new"], texts=["zeta eta theta"], metadatas=[{"language": "en"}])
+    assert s1._st is not s2._st
+    assert all(s1._entries[i] is not s2._entries[i] for i in ids[1:])
+    for s, sub in ((s1, "a"), (s2, "b")):        # each state saves its own sidecar
+        s.index_dir = tmp_path / sub
+        s.save()
+    for sub, want_ids in (("a", ids[1:] + ["new"]), ("b", ids)):
+        side = tmp_path / sub / "bm25_index.jsonl.cm"
+        vocab = json.loads((side / "vocab.json").read_text())
+        tid, off = np.load(side / "term_ids.npy"), np.load(side / "doc_off.npy")
+        recs = [json.loads(l) for l in open(tmp_path / sub / "bm25_index.jsonl", encoding="utf-8")]
+        assert [r["id"] for r in recs] == want_ids
+        for r, rec in enumerate(recs):
+            assert [vocab[t] for t in tid[off[r]:off[r + 1]]] == rec["tokens"], (sub, r)
+
+
 def test_vector_store_constructions_share_the_collection(tmp_path):
     VS.release_all()
     a = VS.GpuVectorStore(persist_dir=tmp_path / "chroma", collection_name="c1")
