@@ -78,6 +78,12 @@ def parse_args():
     ap.add_argument("--ingest-leg", type=int, default=1,
                     help="hybrid mode: also time BASELINE configs[2]'s passage encode at the reference's fp32 "
                          "(256 chunks x --seq-len tokens per step; reported as ingest_fp32 + rooflines.e5_ingest)")
+    ap.add_argument("--varlen-chunks", type=int, default=4096,
+                    help="hybrid mode with --ingest-leg: passages of S ~ U[64, 512] tokens through encode_passages "
+                         "(SURVEY §8d C3's variable-length run; reported as ingest_varlen_fp32); 0 = off")
+    ap.add_argument("--ingest-e2e-chunks", type=int, default=65536,
+                    help="hybrid mode with --ingest-leg, N = 1: chunks through ingest_file's store path (encode_passages "
+                         "-> upsert -> upsert_many -> save, files of 4096; reported as ingest_e2e); 0 = off")
     ap.add_argument("--no-e5", action="store_true", help="use perturbed corpus rows as query embeddings")
     ap.add_argument("--no-graph", action="store_true", help="run the E5 query encode eagerly (no hipGraph)")
     ap.add_argument("--serial", action="store_true", help="run BM25 on the main stream (no overlap with E5 + dense)")
@@ -511,8 +517,12 @@ def main():
         if "c4_dense_10m_b256" in legs:
             roof["standalone"] = legs["c4_dense_10m_b256"]["roofline"]
     if use_e5 and args.ingest_leg:
-        legs["ingest_fp32"], roofs["e5_ingest"] = ingest_leg(args, e5["emb"] if e5["dtype"] == "float32" else None,
-                                                           dev, ws, rank)
+        e5_f32 = e5["emb"] if e5["dtype"] == "float32" else None
+        legs["ingest_fp32"], roofs["e5_ingest"] = ingest_leg(args, e5_f32, dev, ws, rank)
+        if args.varlen_chunks > 0:
+            legs["ingest_varlen_fp32"] = varlen_ingest_leg(args, e5_f32, dev, ws, rank)
+        if args.ingest_e2e_chunks > 0 and ws == 1:
+            legs["ingest_e2e"] = ingest_e2e_leg(args, e5_f32, dev)
 
     out = {
         "metric": METRIC if args.mode == "hybrid" else f"dense cosine top-{K} queries/sec, {N}x{D} fp32",
@@ -808,6 +818,147 @@ def ingest_leg(args, emb, dev, ws, rank):
                                        "layers": args.e5_layers}}
     log(f"ingest_fp32: {leg['value']:.0f} chunks/s ({ms:.2f} ms per {B} x {S} tokens, {roof['frac']:.3f} of f16 peak)")
     return leg, roof
+
+
+def _zipf_texts(rng, n, lo, hi, zipf=1.07, vocab=1 << 16):
+    """n synthetic chunks of U[lo, hi] letters-only words (Zipf draws from `vocab` words "zq" + 4
+    letters): the BM25 tokenizer keeps every word, the E5 hash tokenizer maps each to one token."""
+    import numpy as np
+    p = 1.0 / np.arange(1, vocab + 1) ** zipf
+    cdf = np.cumsum(p)
+    cdf /= cdf[-1]
+    alpha = np.frombuffer(b"abcdefghijklmnopqrstuvwxyz", np.uint8)
+    wv = np.arange(vocab)
+    vb = np.empty((vocab, 7), np.uint8)
+    vb[:, 0], vb[:, 1], vb[:, 6] = ord("z"), ord("q"), ord(" ")
+    for i in range(4):
+        vb[:, 2 + i] = alpha[(wv // 26 ** i) % 26]
+    lens = rng.integers(lo, hi + 1, n)
+    words = np.minimum(np.searchsorted(cdf, rng.random(int(lens.sum()))), vocab - 1)
+    blob = vb[words].tobytes()
+    out, o = [], 0
+    for ln in lens.tolist():
+        out.append(blob[o * 7:(o + ln) * 7 - 1].decode("ascii"))
+        o += ln
+    return out, lens
+
+
+def _e5_seq_flops(S, layers=12, d=768):
+    """fp32-equivalent forward flops of one sequence of S real tokens (padding excluded)."""
+    return float(layers) * (24.0 * S * d * d + 4.0 * S * S * d)
+
+
+def varlen_ingest_leg(args, emb, dev, ws, rank):
+    """SURVEY §8(d) C3's variable-length run: --varlen-chunks passages of S ~ U[64, 512] tokens
+    (incl. <s>, "passage", ":" and </s>) through the drop-in ``encode_passages`` (sentence-
+    transformers' length-sorted batches of 32, rag/embeddings/__init__.py:98-105), tokenization
+    included, numpy fp32 out.  chunks/s over all ranks (replicas); the roofline counts the real
+    tokens' flops only (no padding), 3x issued on K10."""
+    import numpy as np
+    import torch
+    from classmate_hip import parallel
+    from classmate_hip.embeddings import E5MultilingualEmbedder
+    if emb is None:
+        emb = E5MultilingualEmbedder.random_init(seed=0, device=str(dev), num_layers=args.e5_layers, dtype="float32")
+    rng = np.random.default_rng(args.seed * 7 + 991 + rank)
+    n = args.varlen_chunks
+    texts, words = _zipf_texts(rng, n, 60, 508)
+    S = words + 4
+    emb.encode_passages(texts[: min(n, 256)])                       # kernels / first shapes
+    torch.cuda.synchronize()
+    if ws > 1:
+        torch.distributed.barrier()
+    t0 = time.perf_counter()
+    out = emb.encode_passages(texts)
+    torch.cuda.synchronize()
+    if ws > 1:
+        torch.distributed.barrier()
+    el = parallel.max_over_ranks(time.perf_counter() - t0, device=dev)
+    assert out.shape == (n, 768) and out.dtype == np.float32
+    alg = sum(_e5_seq_flops(int(x), args.e5_layers) for x in S)
+    tf = 3.0 * alg / el / 1e12
+    leg = {"value": n * ws / el, "unit": "chunks/s", "seconds": el,
+           "tokens_per_s": float(S.sum()) * ws / el,
+           "config": {"workload": "encode_passages, S ~ U[64, 512] (BASELINE configs[2], SURVEY §8d C3 variable-length run)",
+                      "chunks": n * ws, "mean_tokens": float(S.mean()), "min_tokens": int(S.min()),
+                      "max_tokens": int(S.max()), "batching": "length-sorted batches of 32 (sentence-transformers)",
+                      "includes": "host tokenization (offline hash tokenizer) + forward + K6 pooling + copy to numpy",
+                      "e5_forward": "fp32 (K10 f16x3)", "parallelism": f"replicas x{ws}"},
+           "roofline": {"bound": "mfma", "achieved": tf, "peak": PEAK_F16_MFMA_TFLOPS, "unit": "TFLOP/s",
+                        "frac": tf / PEAK_F16_MFMA_TFLOPS, "traffic": None,
+                        "algorithmic": {"flops_fp32_equiv": alg, "flops_issued": 3.0 * alg,
+                                        "note": "real tokens only; padding to the batch maximum is wasted work"}}}
+    log(f"ingest_varlen_fp32: {leg['value']:.0f} chunks/s ({n} chunks, mean S {S.mean():.0f}, {el:.2f} s, "
+        f"{leg['roofline']['frac']:.3f} of f16 peak on real tokens)")
+    return leg
+
+
+def ingest_e2e_leg(args, emb, dev):
+    """The reference's ingest of one file (rag/pipeline/rag.py:410-413) repeated over --ingest-e2e-chunks
+    chunks in files of 4096: CachingEmbedder(E5).encode_passages -> ChromaVectorStore.upsert
+    (persisted) -> BM25Store.upsert_many -> BM25Store.save, each file through the drop-in classes,
+    then the first search's BM25 index build.  chunks/s end to end with the per-stage seconds."""
+    import shutil
+    import tempfile
+    import numpy as np
+    import torch
+    from classmate_hip.embeddings import CachingEmbedder, E5MultilingualEmbedder
+    from classmate_hip.retrieval.bm25 import BM25Store
+    from classmate_hip.retrieval.vector_store import GpuVectorStore
+    if emb is None:
+        emb = E5MultilingualEmbedder.random_init(seed=0, device=str(dev), num_layers=args.e5_layers, dtype="float32")
+    n, per_file = args.ingest_e2e_chunks, 4096
+    rng = np.random.default_rng(args.seed * 11 + 5)
+    root = Path(tempfile.mkdtemp(prefix="cm_ingest_", dir=os.environ.get("TMPDIR")))
+    try:
+        vs = GpuVectorStore(persist_dir=root / "chroma", device=dev.index)
+        bm = BM25Store.load_or_create(root / "bm25")
+        bm.device = dev.index
+        cemb = CachingEmbedder(emb, cache_dir=str(root / "emb_cache"))
+        warm, _ = _zipf_texts(rng, 64, 60, 508)
+        emb.encode_passages(warm)
+        torch.cuda.synchronize()
+        st = dict(encode=0.0, vector_upsert=0.0, bm25_upsert=0.0, bm25_save=0.0, bm25_index_build=0.0, texts=0.0)
+        tok = 0
+        t_all = time.perf_counter()
+        for f0 in range(0, n, per_file):
+            m = min(per_file, n - f0)
+            t = time.perf_counter()
+            texts, words = _zipf_texts(rng, m, 60, 508)      # the chunker's output (not the path: untimed)
+            st["texts"] += time.perf_counter() - t
+            tok += int(words.sum()) + 4 * m
+            ids = [f"f{f0 // per_file}:c{j}" for j in range(m)]
+            metas = [{"course": f"C{(f0 + j) % 16}", "language": "en", "doc_type": "pdf", "week": (f0 + j) % 12}
+                     for j in range(m)]
+            t = time.perf_counter()
+            e = cemb.encode_passages(texts)
+            st["encode"] += time.perf_counter() - t
+            t = time.perf_counter()
+            vs.upsert(ids=ids, documents=texts, metadatas=metas, embeddings=e)
+            st["vector_upsert"] += time.perf_counter() - t
+            t = time.perf_counter()
+            bm.upsert_many(ids=ids, texts=texts, metadatas=metas)
+            st["bm25_upsert"] += time.perf_counter() - t
+            t = time.perf_counter()
+            bm.save()
+            st["bm25_save"] += time.perf_counter() - t
+        t = time.perf_counter()
+        bm._ensure_index()                                  # the first search after the ingest builds it
+        torch.cuda.synchronize()
+        st["bm25_index_build"] = time.perf_counter() - t
+        total = time.perf_counter() - t_all - st["texts"]
+        assert vs.count() == n and len(bm._id_list) == n
+    finally:
+        shutil.rmtree(root, ignore_errors=True)
+    leg = {"value": n / total, "unit": "chunks/s", "seconds": total, "chunks": n, "tokens": tok,
+           "breakdown_s": {k: v for k, v in st.items() if k != "texts"},
+           "config": {"workload": "ingest_file's store path per file of 4096 chunks (rag/pipeline/rag.py:410-413): "
+                                  "CachingEmbedder(E5 fp32).encode_passages -> ChromaVectorStore.upsert (persisted) -> "
+                                  "BM25Store.upsert_many -> BM25Store.save; + the BM25 device index build",
+                      "tokens_per_chunk": "U[64, 512]", "files": (n + per_file - 1) // per_file}}
+    log(f"ingest_e2e: {leg['value']:.0f} chunks/s over {n} chunks ({total:.1f} s: "
+        + ", ".join(f"{k} {v:.1f}" for k, v in leg["breakdown_s"].items()) + ")")
+    return leg
 
 
 def _pmc_traffic(args, which, batch=None):

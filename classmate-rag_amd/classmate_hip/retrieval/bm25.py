@@ -38,7 +38,7 @@ from typing import Any, Dict, List, Mapping, Optional, Sequence
 
 import numpy as np
 
-from .. import engine
+from .. import engine, multidev
 from .filters import MetaIndex, next_uid
 from .tokenize import _tokenize, detect_lang_tag
 
@@ -299,7 +299,7 @@ class BM25Store:
 
     def _registry_key(self):
         dev = engine.default_device() if self.device is None else int(self.device)
-        return (str(Path(self.index_path).resolve()), dev)
+        return (str(Path(self.index_path).resolve()), dev, os.environ.get("CM_DEVICES", "") if self.device is None else "")
 
     def _mutating(self) -> None:
         """Before a change of the document set: a state other stores also hold is copied first."""
@@ -326,7 +326,7 @@ class BM25Store:
         if not self._dirty and self._index is not None:
             return
         if self._index is None:
-            self._index = engine.BM25Index(device=self.device)
+            self._index = multidev.new_bm25_index(device=self.device)
         if self._csr is not None:  # opened from a sidecar: the persisted CSR is the index
             term_ids, doc_off = self._csr
             self._index.build(np.ascontiguousarray(term_ids), np.ascontiguousarray(doc_off),

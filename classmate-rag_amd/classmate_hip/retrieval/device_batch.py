@@ -152,6 +152,8 @@ def _bm25_filtered(bm, q_terms, q_off, k: int, allow, where, cache: dict):
     handed to later searches with the same filter."""
     import torch
     index = bm._index
+    if getattr(index, "sharded", False):        # multidev: the candidates' statistics over every shard
+        return index.search_filtered(q_terms, q_off, k, allow)
     index.prepare_filtered()                    # the device log table (once per index)
     fk = _filter_key(bm._meta, where, "bm25")
     ekey = None if fk is None else ("eps", bm._uid, bm._version) + fk

@@ -47,7 +47,7 @@ from typing import Any, Dict, List, Mapping, Optional, Sequence
 
 import numpy as np
 
-from .. import engine
+from .. import engine, multidev
 from .filters import MetaIndex, next_uid
 
 
@@ -221,7 +221,7 @@ class GpuVectorStore:
         if d is None:
             return _State()
         dev = engine.default_device() if self.device is None else int(self.device)
-        key = (str(d.resolve()), dev)
+        key = (str(d.resolve()), dev, os.environ.get("CM_DEVICES", "") if self.device is None else "")
         sig = _disk_sig(d)
         with _REG_LOCK:
             st = _REGISTRY.get(key)
@@ -315,7 +315,7 @@ class GpuVectorStore:
             else:
                 meta_.remove(r)
             st.line_off[r] = off
-        self._index = engine.DenseIndex(dim, device=self.device, capacity=max(n, 1))
+        self._index = multidev.new_dense_index(dim, device=self.device, capacity=max(n, 1))
         self._version += 1
         live = np.fromiter((i is not None for i in ids_), bool, count=n) if n else np.zeros(0, bool)
         if live.any():
@@ -459,7 +459,7 @@ class GpuVectorStore:
         if emb.ndim != 2:
             raise ValueError("embeddings must be a 2-D array (n, dim)")
         if self._index is None:
-            self._index = engine.DenseIndex(emb.shape[1], device=self.device, capacity=len(ids))
+            self._index = multidev.new_dense_index(emb.shape[1], device=self.device, capacity=len(ids))
         elif emb.shape[1] != self._index.dim:
             raise ValueError(f"Embedding dimension {emb.shape[1]} does not match collection dimensionality "
                              f"{self._index.dim}")

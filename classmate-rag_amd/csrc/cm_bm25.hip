@@ -1987,6 +1987,10 @@ int cm_bm25_search_dev_gated(cm_bm25 *h, const int32_t *q_terms_dev, const int32
                           (hipEvent_t)gate_event);
 }
 
+static int bm25_search_scored(cm_bm25 *h, const int32_t *q_terms, const int32_t *q_off, int32_t nq, int32_t total,
+                              int32_t k, const uint32_t *allow_dev, const double *q_idf_host, double avgdl,
+                              int64_t n_cand, double *out_score, int64_t *out_row, int32_t *out_n);
+
 int cm_bm25_search(cm_bm25 *h, const int32_t *q_terms, const int32_t *q_off, int32_t nq, int32_t k,
                    const uint32_t *allow_bits, double *out_score, int64_t *out_row, int32_t *out_n) {
   if (!h) CM_FAIL(CM_EINVAL, "null handle");
@@ -2070,8 +2074,18 @@ int cm_bm25_search(cm_bm25 *h, const int32_t *q_terms, const int32_t *q_off, int
       q_idf[i] = v < 0 ? eps : v;
     }
   }
+  return bm25_search_scored(h, q_terms, q_off, nq, total, k, allow_dev, q_idf.data(), avgdl, n_cand, out_score,
+                            out_row, out_n);
+}
+
+// The scoring half of the host-array search, given every query term's idf, the candidates' avgdl
+// and count: the fused top-k lists (k <= kMaxTopK) or the full order.  allow_dev is device memory.
+static int bm25_search_scored(cm_bm25 *h, const int32_t *q_terms, const int32_t *q_off, int32_t nq, int32_t total,
+                              int32_t k, const uint32_t *allow_dev, const double *q_idf_host, double avgdl,
+                              int64_t n_cand, double *out_score, int64_t *out_row, int32_t *out_n) {
+  int rc;
   if (k > kMaxTopK) {  // beyond the fused top-k lists: full scores + one sort per query
-    rc = bm25_search_full(h, q_terms, q_off, nq, k, q_idf.data(), avgdl, allow_dev, n_cand, out_score, out_row);
+    rc = bm25_search_full(h, q_terms, q_off, nq, k, q_idf_host, avgdl, allow_dev, n_cand, out_score, out_row);
     if (rc) return rc;
     if (out_n) {
       const int32_t nv = (int32_t)std::min<int64_t>(k, n_cand);
@@ -2090,7 +2104,7 @@ int cm_bm25_search(cm_bm25 *h, const int32_t *q_terms, const int32_t *q_off, int
   int32_t *d_off = d_terms + std::max(total, 1);
   if (total > 0) CM_HIP(hipMemcpyAsync(d_terms, q_terms, (size_t)total * 4, hipMemcpyHostToDevice, h->stream));
   CM_HIP(hipMemcpyAsync(d_off, q_off, (size_t)(nq + 1) * 4, hipMemcpyHostToDevice, h->stream));
-  if (total > 0) CM_HIP(hipMemcpyAsync(w.q_idf, q_idf.data(), (size_t)total * 8, hipMemcpyHostToDevice, h->stream));
+  if (total > 0) CM_HIP(hipMemcpyAsync(w.q_idf, q_idf_host, (size_t)total * 8, hipMemcpyHostToDevice, h->stream));
   double *d_score = h->obuf.as<double>();
   int64_t *d_row = reinterpret_cast<int64_t *>(d_score + (size_t)nq * k);
   hipLaunchKernelGGL(bm25_set_f64_kernel, dim3(1), dim3(64), 0, h->stream, avgdl, w.avgdl);
@@ -2106,6 +2120,45 @@ int cm_bm25_search(cm_bm25 *h, const int32_t *q_terms, const int32_t *q_off, int
     for (int i = 0; i < nq; ++i) out_n[i] = nv;
   }
   return CM_OK;
+}
+
+int cm_bm25_search_idf(cm_bm25 *h, const int32_t *q_terms, const int32_t *q_off, int32_t nq, int32_t k,
+                       const uint32_t *allow_bits, const double *q_idf, double avgdl, int64_t n_cand,
+                       double *out_score, int64_t *out_row, int32_t *out_n) {
+  if (!h) CM_FAIL(CM_EINVAL, "null handle");
+  if (nq <= 0) return CM_OK;
+  if (!q_off || !out_score || !out_row) CM_FAIL(CM_EINVAL, "NULL argument");
+  if (k <= 0) CM_FAIL(CM_EINVAL, "k must be >= 1");
+  const int32_t total = q_off[nq];
+  if (total < 0 || (total > 0 && (!q_terms || !q_idf))) CM_FAIL(CM_EINVAL, "bad q_off / NULL q_idf");
+  for (int i = 0; i < nq; ++i)
+    if (q_off[i + 1] < q_off[i]) CM_FAIL(CM_EINVAL, "q_off must be non-decreasing");
+  if (n_cand < 0) CM_FAIL(CM_EINVAL, "n_cand must be >= 0");
+  DeviceGuard dg(h->dev);
+  if (n_cand == 0 || h->ndocs == 0) {
+    for (int i = 0; i < nq; ++i) {
+      if (out_n) out_n[i] = 0;
+      for (int j = 0; j < k; ++j) {
+        out_score[(int64_t)i * k + j] = 0.0;
+        out_row[(int64_t)i * k + j] = -1;
+      }
+    }
+    return CM_OK;
+  }
+  if (!(avgdl > 0.0)) CM_FAIL(CM_EZERODIV, "float division by zero (candidate documents have no tokens)");
+  const uint32_t *allow_dev = nullptr;
+  int rc;
+  if (allow_bits) {
+    const int64_t nw = std::max<int64_t>(1, ceil_div(h->ndocs, 32));
+    if ((rc = h->allow_buf.ensure((size_t)nw * 4))) return rc;
+    CM_HIP(hipMemcpyAsync(h->allow_buf.ptr, allow_bits, (size_t)nw * 4, hipMemcpyDefault, h->stream));  // host or device
+    allow_dev = h->allow_buf.as<uint32_t>();
+  }
+  std::vector<double> qi((size_t)std::max(total, 1), 0.0);
+  for (int32_t i = 0; i < total; ++i)
+    qi[(size_t)i] = (q_terms[i] >= 0 && q_terms[i] < h->vocab) ? q_idf[i] : 0.0;
+  return bm25_search_scored(h, q_terms, q_off, nq, total, k, allow_dev, qi.data(), avgdl, n_cand, out_score, out_row,
+                            out_n);
 }
 
 int cm_bm25_prepare_filtered(cm_bm25 *h, int64_t max_docs) {

@@ -246,6 +246,16 @@ int cm_bm25_set_stats(cm_bm25 *h, const double *idf, int32_t vocab, int64_t n_li
  * out_n[i] = number of valid entries (min(k, #candidates)).               */
 int cm_bm25_search(cm_bm25 *h, const int32_t *q_terms, const int32_t *q_off, int32_t nq, int32_t k,
                    const uint32_t *allow_bits, double *out_score, int64_t *out_row, int32_t *out_n);
+/* cm_bm25_search with the caller's statistics instead of this index's: q_idf[total] = every
+ * query term's idf (0 for terms outside the candidate vocabulary; ignored for ids outside
+ * [0, vocab)), avgdl and n_cand of the candidate set; allow_bits (host or device words,
+ * nullable) restricts the scored documents.  A corpus sharded over several devices in one process
+ * (classmate_hip/multidev.py, SURVEY §8(b) Threading / §8(e)) scores every shard with the GLOBAL
+ * statistics -- for a where-filter the statistics of the filtered candidates of all shards (quirk
+ * Q2, rag/retrieval/bm25.py:184-191) -- and merges the shards' lists by (score desc, row asc). */
+int cm_bm25_search_idf(cm_bm25 *h, const int32_t *q_terms, const int32_t *q_off, int32_t nq, int32_t k,
+                       const uint32_t *allow_bits, const double *q_idf, double avgdl, int64_t n_cand,
+                       double *out_score, int64_t *out_row, int32_t *out_n);
 /* unfiltered device variant (inputs and outputs device, graph-capturable). */
 int64_t cm_bm25_search_workspace(cm_bm25 *h, int32_t nq, int32_t total_terms, int32_t k);
 int cm_bm25_search_dev(cm_bm25 *h, const int32_t *q_terms_dev, const int32_t *q_off_dev, int32_t nq,

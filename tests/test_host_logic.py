@@ -200,3 +200,42 @@ def test_hash_tokenizer_memo_is_transparent():
         assert list(ids[i, :len(want)]) == want
         assert int(mask[i].sum()) == len(want)
     assert len(tok._memo) <= 8
+
+
+def test_multidev_row_map_round_trip_and_word_split():
+    """classmate_hip/multidev.py's block-round-robin row map (CM_DEVICES sharding, host side):
+    global <-> (shard, local) is a bijection, local rows of a shard keep global order, local_count
+    matches the map, and the allow words split into each shard's local words bit for bit."""
+    import numpy as np
+    import torch
+    from classmate_hip.multidev import RowMap, _f32_key_np
+    for G, B in ((4, 64), (3, 32), (2, 1 << 16), (8, 128)):
+        m = RowMap(G, B)
+        n = B * G * 3 + 17
+        g = np.arange(n, dtype=np.int64)
+        s, l = m.owner_local(g)
+        back = np.empty_like(g)
+        for sh in range(G):
+            sel = s == sh
+            assert np.all(np.diff(l[sel]) == 1) and (l[sel][:1] == 0).all()     # dense local rows
+            back[sel] = m.to_global(sh, l[sel])
+            assert m.local_count(sh, n) == sel.sum()
+            tl = torch.from_numpy(l[sel])
+            assert np.array_equal(m.to_global(sh, tl).numpy(), g[sel])
+        assert np.array_equal(back, g)
+        assert (m.to_global(1 % G, np.array([-1])) == -1).all()
+        mask = (np.random.default_rng(G).random(n) < 0.4)
+        words = np.packbits(mask, bitorder="little")
+        words = np.concatenate([words, np.zeros((-len(words)) % 4, np.uint8)]).view(np.uint32)
+        for kind in ("np", "torch"):
+            w = words if kind == "np" else torch.from_numpy(words.view(np.int32))
+            parts = m.split_words(w, G)
+            for sh in range(G):
+                p = parts[sh] if kind == "np" else parts[sh].numpy().view(np.uint32)
+                bits = np.unpackbits(p.view(np.uint8), bitorder="little").astype(bool)
+                loc = l[s == sh]
+                assert np.array_equal(bits[loc], mask[s == sh])
+                assert not bits[m.local_count(sh, n):].any()
+    d = np.array([[0.5, 0.25, 0.25, -0.0, 0.0]], np.float32)
+    r = np.array([[3, 9, 2, 7, -1]], np.int64)
+    assert np.argsort(_f32_key_np(d, r), axis=1).tolist() == [[3, 2, 1, 0, 4]]
