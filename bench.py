@@ -465,10 +465,12 @@ def main():
     # scan-kernel launch times: HIP events the library records on the launch stream
     kt = dense.timing_drain()
     dense_ms = sum(kt) / len(kt)
-    bm25_ms = None
+    bm25_ms = bm25b_ms = None
     if bm25 is not None:
         bt = bm25.timing_drain()
         bm25_ms = sum(bt) / len(bt)
+        btb = bm25.timing_drain_block()
+        bm25b_ms = sum(btb) / len(btb) if btb else None
     dense.timing(False)
     if bm25 is not None:
         bm25.timing(False)
@@ -486,6 +488,9 @@ def main():
                                       _pmc_traffic(args, {5: "dense_q8", 6: "dense_q8s"}.get(kind, "dense")))}
     if bm25 is not None:
         roofs["bm25"] = _bm25_roofline(bm25, q_terms, N, bm25_ms, _pmc_traffic(args, "bm25"), args.q_terms)
+        if bm25b_ms is not None:
+            roofs["bm25_block"] = _bm25_block_roofline(bm25, q_terms, bm25.workspace_items(B, q_terms.numel(), K, bws),
+                                                       bm25b_ms, _pmc_traffic(args, "bm25b"), args.q_terms)
     # the headline roofline: the kernel with the most algorithmic work per step (K1q: 7.76 GB per launch
     # against K2a's 0.25 GB).  In-step launch times are not a fair ranking: the two run side by side and
     # whichever starts second is stretched by the other (rooflines.bm25 keeps K2a's line either way)
@@ -552,7 +557,7 @@ def main():
                    "schedule": ("pipelined: batch i+1 encoded beside batch i's search" if pipe["stream"] is not None
                                 else "serial: encode, then search")},
         "breakdown_ms": {"e5_encode": e5_ms, "dense_search": search_ms, "dense_scan_kernel": dense_ms,
-                         "bm25_search": bsearch_ms, "bm25_tail_kernel": bm25_ms},
+                         "bm25_search": bsearch_ms, "bm25_tail_kernel": bm25_ms, "bm25_block_kernel": bm25b_ms},
         "dense_exact_reruns": fallbacks,
         "bm25_rescored_pairs": rescored,
         "roofline": roof,
@@ -636,6 +641,27 @@ def _bm25_roofline(bm25, q_terms, N, ms, traffic, terms_per_query):
     r = _roof(bytes_, 0.0, 1.0, ms)
     r.update(traffic=traffic, kernel="K2a bm25_tail_kernel (pruned BM25 tail pass)", avg_launch_ms=ms,
              algorithmic_per_launch=dict(bytes=bytes_, queries=int(qt.shape[0]), docs=N))
+    return r
+
+
+def _bm25_block_roofline(bm25, q_terms, items, ms, traffic, terms_per_query):
+    """K2b (bm25_block_kernel: the head-only documents of the planned 64-doc blocks) per launch,
+    algorithmic bytes: every planned block's 64 documents read once -- one tf byte per head term of
+    its query (the dense tiles) + the 4-B length -- plus 16 B of live / allow words per block and
+    the 8-B item itself.  Planned items from the last timed step's workspace."""
+    import numpy as np
+    df, _ = bm25.term_stats()
+    nh = bm25.num_head_terms
+    head_df = np.sort(df)[::-1][nh - 1] if nh > 0 else np.iinfo(np.int64).max
+    qt = q_terms.view(-1, terms_per_query).cpu().numpy()
+    nh_q = np.array([int((df[row[(row >= 0) & (row < df.shape[0])]] >= head_df).sum()) for row in qt], np.int64)
+    q = (items >> np.uint64(40)).astype(np.int64)
+    nblk = np.array([bin(int(x)).count("1") for x in (items & np.uint64(0xFFFF)).tolist()], np.int64)
+    bytes_ = float((nblk * (64 * (nh_q[q] + 4) + 16)).sum() + 8 * items.shape[0])
+    r = _roof(bytes_, 0.0, 1.0, ms)
+    r.update(traffic=traffic, kernel="K2b bm25_block_kernel (head-only documents of the planned 64-doc blocks)",
+             avg_launch_ms=ms, algorithmic_per_launch=dict(bytes=bytes_, items=int(items.shape[0]),
+                                                           blocks=int(nblk.sum()), docs=int(nblk.sum()) * 64))
     return r
 
 

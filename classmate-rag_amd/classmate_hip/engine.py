@@ -363,6 +363,24 @@ class BM25Index:
             raise RuntimeError(L.last_error())
         return buf[:min(n, cap)].tolist()
 
+    def timing_drain_block(self, cap: int = 4096) -> list:
+        """Per-launch times (ms) of K2b (bm25_block_kernel) since timing(True)."""
+        buf = np.zeros(cap, np.float32)
+        n = int(L.fn["cm_bm25_timing_drain_block"](self._h, L.ptr(buf), int(cap)))
+        if n < 0:
+            raise RuntimeError(L.last_error())
+        return buf[:min(n, cap)].tolist()
+
+    def workspace_items(self, nq: int, total_terms: int, k: int, workspace, cap: int = 1 << 22) -> np.ndarray:
+        """K2b's planned items (q << 40 | range << 16 | 64-doc block mask) of the last pruned search
+        that used ``workspace`` (synchronous read)."""
+        buf = np.zeros(cap, np.uint64)
+        n = int(L.fn["cm_bm25_workspace_items"](self._h, int(nq), int(total_terms), int(k), L.ptr(workspace),
+                                                 L.ptr(buf), int(cap)))
+        if n < 0:
+            raise RuntimeError(L.last_error() or "no planned items (full path?)")
+        return buf[:min(n, cap)]
+
     @property
     def num_head_terms(self) -> int:
         return int(L.fn["cm_bm25_num_head_terms"](self._h))

@@ -1146,7 +1146,8 @@ struct cm_bm25 {
   int64_t head_max_bytes = 8ll << 30;    // tile memory budget
   std::vector<double> idf_host;
   DevBuf ws, qbuf, obuf, allow_buf, tmp;
-  KernelTimer timer;  // K2 events (cm_bm25_timing)
+  KernelTimer timer;    // K2 events (cm_bm25_timing)
+  KernelTimer timer_b;  // K2b events (cm_bm25_timing_drain_block)
 };
 
 namespace {
@@ -1457,10 +1458,12 @@ int bm25_launch_core(cm_bm25 *h, const int32_t *q_terms_dev, const int32_t *q_of
                        w.item_count);
     CM_HIP(hipGetLastError());
     // K2b: head-only documents of the planned blocks, merged into the tail pass's lists
+    h->timer_b.begin(st);
     hipLaunchKernelGGL(bm25_block_kernel, dim3(K2B_GRID), dim3(256), 0, st, w.items, w.item_count, w.qd_code,
                        w.qd_idf, w.qd_tb, w.bounds, nr, h->post_doc.as<int32_t>(), h->headtf.as<uint8_t>(), h->npad,
                        h->dl.as<int32_t>(), h->live.as<uint32_t>(), allow_dev, h->ndocs, avgdl, k, score_dev, nq,
                        w.cand_key, w.cand_row);
+    h->timer_b.end(st);
     CM_HIP(hipGetLastError());
   }
   hipLaunchKernelGGL(bm25_range_kernel<uint16_t>, dim3((unsigned)nblk), dim3(kBmThreads), 0, st, q_terms_dev,
@@ -1605,6 +1608,7 @@ void cm_bm25_destroy(cm_bm25 *h) {
   if (h->stream) (void)hipStreamSynchronize(h->stream);
   bm25_free(h);
   h->timer.release();
+  h->timer_b.release();
   if (h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
 }
@@ -1919,11 +1923,37 @@ int32_t cm_bm25_workspace_rescored(cm_bm25 *h, int32_t nq, int32_t total_terms, 
 
 int32_t cm_bm25_last_rescored(cm_bm25 *h) { return h ? h->last_rescored : -1; }
 
+int64_t cm_bm25_workspace_items(cm_bm25 *h, int32_t nq, int32_t total_terms, int32_t k, const void *workspace_dev,
+                                uint64_t *items_out, int64_t cap) {
+  if (!h || !workspace_dev || nq <= 0 || k <= 0 || cap < 0) return -1;
+  if (h->path == 1) return -1;
+  DeviceGuard dg(h->dev);
+  const BmWs w = bm_ws_layout(h, nq, total_terms, k, const_cast<void *>(workspace_dev));
+  uint32_t n = 0;
+  if (hipMemcpyAsync(&n, w.item_count, 4, hipMemcpyDeviceToHost, h->stream) != hipSuccess ||
+      hipStreamSynchronize(h->stream) != hipSuccess)
+    return -1;
+  const int64_t m = std::min<int64_t>(n, cap);
+  if (m > 0 && items_out &&
+      (hipMemcpyAsync(items_out, w.items, (size_t)m * 8, hipMemcpyDeviceToHost, h->stream) != hipSuccess ||
+       hipStreamSynchronize(h->stream) != hipSuccess))
+    return -1;
+  return n;
+}
+
 int cm_bm25_timing(cm_bm25 *h, int32_t enable) {
   if (!h) CM_FAIL(CM_EINVAL, "null handle");
-  h->timer.on = enable != 0;
-  h->timer.used = 0;
+  h->timer.on = h->timer_b.on = enable != 0;
+  h->timer.used = h->timer_b.used = 0;
   return CM_OK;
+}
+
+int32_t cm_bm25_timing_drain_block(cm_bm25 *h, float *ms_out, int32_t cap) {
+  if (!h) CM_FAIL(CM_EINVAL, "null handle");
+  DeviceGuard dg(h->dev);
+  const int n = h->timer_b.drain(ms_out, cap);
+  if (n < 0) CM_FAIL(CM_EDEVICE, "event query failed");
+  return n;
 }
 
 int32_t cm_bm25_timing_drain(cm_bm25 *h, float *ms_out, int32_t cap) {

@@ -223,10 +223,17 @@ int cm_bm25_set_path(cm_bm25 *h, int32_t kind);
  * same for the last host-array cm_bm25_search on this handle.            */
 int32_t cm_bm25_workspace_rescored(cm_bm25 *h, int32_t nq, int32_t total_terms, int32_t k, const void *workspace_dev);
 int32_t cm_bm25_last_rescored(cm_bm25 *h);
+/* K2b's planned items of the pruned search that last used `workspace_dev` (synchronous read):
+ * returns their count (-1 on the full path or error) and copies up to cap items (q << 40 |
+ * 1024-doc range << 16 | 64-doc block mask) -- bench.py prices K2b's algorithmic bytes with them. */
+int64_t cm_bm25_workspace_items(cm_bm25 *h, int32_t nq, int32_t total_terms, int32_t k, const void *workspace_dev,
+                                uint64_t *items_out, int64_t cap);
 /* kernel timing (bench roofline): events around every search's K2 launch;
  * same contract as cm_dense_timing / cm_dense_timing_drain.              */
 int cm_bm25_timing(cm_bm25 *h, int32_t enable);
 int32_t cm_bm25_timing_drain(cm_bm25 *h, float *ms_out, int32_t cap);
+/* the same for K2b (bm25_block_kernel) launches of the pruned search. */
+int32_t cm_bm25_timing_drain_block(cm_bm25 *h, float *ms_out, int32_t cap);
 /* Sharding support: local df per term and the first posting's
  * (row << 32 | first position) key (0xff..ff when absent), so ranks can
  * all-reduce df (sum) and first keys (min, after offsetting rows) and agree
