@@ -1424,14 +1424,29 @@ def construct_leg(args, vs, bm, embedder, qs, K, dev, none_keys, lat):
             f"bm25 {out['cold_open_bm25_s']:.1f}s ({len(b0._id_list)} docs)")
         cache_dir = root / "emb_cache"
 
+        phase = {}
+
         def ask(q):
+            t_a = time.perf_counter()
             v = GpuVectorStore.from_config()
             b = BM25Store.load_or_create(root / "bm25")
             base = E5MultilingualEmbedder(model_name=model, device=str(dev))
             emb = CachingEmbedder(base, cache_dir=str(cache_dir))
             r = HybridRetriever(vector_store=v, bm25_store=b, embedder=emb, k_vector=8, k_bm25=8, rrf_k=60,
                                 weight_vector=1.0, weight_bm25=1.0)
-            return r.retrieve(question=q, filters=dict(none_keys), top_k=K)
+            t_b = time.perf_counter()
+            res = r.retrieve(question=q, filters=dict(none_keys), top_k=K)
+            phase.update(construct_ms=(t_b - t_a) * 1e3, retrieve_ms=(time.perf_counter() - t_b) * 1e3)
+            return res
+
+        import gc
+        gc_ms = []                                     # the tail's suspects: Python collections ...
+
+        def gc_cb(ev, info, _t=[0.0]):
+            if ev == "start":
+                _t[0] = time.perf_counter()
+            else:
+                gc_ms.append((info.get("generation"), (time.perf_counter() - _t[0]) * 1e3))
         t0 = time.perf_counter()
         ask(qs[-10])                                   # the first question after the open: key map, filter columns
         torch.cuda.synchronize()
@@ -1440,11 +1455,18 @@ def construct_leg(args, vs, bm, embedder, qs, K, dev, none_keys, lat):
         for i in range(2):
             ask(qs[-11 - i])
         torch.cuda.synchronize()
-        ts = []
-        for i in range(args.e2e_latency_queries):
-            t1 = time.perf_counter()
-            ask(qs[100 + i])                           # new questions: embedding-cache misses
-            ts.append((time.perf_counter() - t1) * 1e3)
+        ts, calls = [], []
+        gc.callbacks.append(gc_cb)
+        try:
+            for i in range(args.e2e_latency_queries):
+                n_gc = len(gc_ms)
+                t1 = time.perf_counter()
+                ask(qs[100 + i])                           # new questions: embedding-cache misses
+                ts.append((time.perf_counter() - t1) * 1e3)
+                calls.append(dict(ms=ts[-1], **phase, gc=[(g, round(m, 2)) for g, m in gc_ms[n_gc:]]))
+        finally:
+            gc.callbacks.remove(gc_cb)
+        out["slowest_calls"] = sorted(calls, key=lambda c: -c["ms"])[:3]     # ... or the phase that grew
         ts.sort()
         out.update(p50_ms=ts[len(ts) // 2], p99_ms=ts[min(len(ts) - 1, int(len(ts) * 0.99))], n=len(ts),
                    bare_retrieve_p50_ms=lat["to_dict_default"]["p50"], filters="DocumentMetadata.to_dict() (None keys)",
