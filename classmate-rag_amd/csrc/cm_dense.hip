@@ -1221,10 +1221,11 @@ __global__ void __launch_bounds__(256) dense_scatter_kernel(const float *__restr
                                                             int64_t row0, int64_t n, int dim, int ld,
                                                             float *__restrict__ C, float *__restrict__ invc,
                                                             uint32_t *__restrict__ live, _Float16 *__restrict__ Xh,
-                                                            uint32_t *__restrict__ rnorm) {
+                                                            int64_t xh_rows, uint32_t *__restrict__ rnorm) {
   const int64_t i = blockIdx.x;
   if (i >= n) return;
   const int64_t r = rows ? rows[i] : row0 + i;
+  const bool in_plane = r < xh_rows;   // the f16 plane holds every row, or only the seed-sample prefix
   const float *s = src + i * dim;
   float *d = C + r * ld;
   float acc = 0.f;
@@ -1249,7 +1250,7 @@ __global__ void __launch_bounds__(256) dense_scatter_kernel(const float *__restr
     const float xn = (c < dim ? s[c] : 0.f) * inv;
     const _Float16 hi = (_Float16)xn;  // subnormal halves included: the matrix cores keep them
     const float lo = xn - (float)hi;    // exact residual (||xl|| of the bound E; tools/denorm_probe.hip)
-    Xh[plane_off(r, c, ld)] = hi;
+    if (in_plane) Xh[plane_off(r, c, ld)] = hi;
     sh += (float)hi * (float)hi;
     sl += lo * lo;
   }
@@ -1348,6 +1349,7 @@ struct cm_dense {
   float *C = nullptr;
   float *invc = nullptr;
   _Float16 *Xh = nullptr;                 // normalised f16 plane, fragment-major (K1c/K1s)
+  int64_t xh_rows = 0;                     // rows Xh holds: all of rows_alloc, or the seed-sample prefix
   int8_t *Xq = nullptr;                    // normalised int8 plane, fragment-major (K1q)
   float2 *rmeta = nullptr;                 // per row {s_r, e_r} of the int8 plane (K1q bound)
   float *rnorm = nullptr;                  // device {max ||Xh_r||, max ||xn_r - Xh_r||, max ||s_r q8_r||, 0}
@@ -1472,8 +1474,33 @@ DenseWs dense_ws_layout(const cm_dense *h, const DenseCfg &c, int nq, int k, voi
   return w;
 }
 
+// The f16 plane (round 6).  Above kXhFullRows rows a dim-768 store searches with the
+// int8 plane (K1q / K1q-s) and reads its f16 plane only for the seed pass, over a prefix of 1/16 of
+// the rows: the plane then holds that prefix alone (10M x 768: 0.96 instead of 15.4 GB), the
+// re-rank's middle stage reads the band rows' fp32 data directly (dense_rerank_q8_kernel with Xh =
+// nullptr: every band row gets its exact fp64 distance), and the K1c / K1s scans, which read every
+// row of the plane, are not eligible (dense_kind).  CM_DENSE_F16=full keeps the whole plane,
+// =prefix forces the prefix at any size (tests).
+constexpr int64_t kXhFullRows = 4ll << 20;
+constexpr int64_t kXhPrefixFrac = 16;
+int xh_mode() {   // read at every allocation (a store's policy is fixed by its arrays, not re-read per search)
+  const char *e = getenv("CM_DENSE_F16");
+  if (!e) return 0;
+  const std::string v(e);
+  return v == "full" ? 1 : v == "prefix" ? 2 : 0;
+}
+int64_t xh_rows_for(const cm_dense *h, int64_t cap) {
+  const int m = xh_mode();
+  if (h->ld != 768 || m == 1 || (m == 0 && cap <= kXhFullRows)) return cap;
+  return std::min<int64_t>(cap, round_up(ceil_div(cap, kXhPrefixFrac), kStepRows));
+}
+// true when the f16 plane holds every written row (the K1c / K1s scans and the f16 band stage)
+bool xh_full(const cm_dense *h) { return round_up(std::max<int64_t>(h->size, 1), kStepRows) <= h->xh_rows; }
+
 // Bytes of the row arrays at `rows` rows (C fp32, invc, live bits, Xh f16 plane, Xq int8 plane + rmeta).
-int64_t dense_row_bytes(const cm_dense *h, int64_t rows) { return rows * h->ld * 7 + rows * 12 + rows / 8; }
+int64_t dense_row_bytes(const cm_dense *h, int64_t rows) {
+  return rows * h->ld * 5 + xh_rows_for(h, rows) * h->ld * 2 + rows * 12 + rows / 8;
+}
 
 // Growth (dense_grow).  The arrays are reallocated at max(need, 1.5 x rows_alloc) rows.  When the
 // new arrays fit in the device's free memory next to the old ones (hipMemGetInfo, with kGrowSlack to
@@ -1506,9 +1533,10 @@ int staged_copy(cm_dense *h, char *host, char *dev, size_t bytes, bool to_host, 
 }
 
 __global__ void __launch_bounds__(256) dense_replane_kernel(const float *__restrict__ C, const float *__restrict__ invc,
-                                                            int64_t n, int dim, int ld, _Float16 *__restrict__ Xh) {
-  const int64_t r = blockIdx.x;
-  if (r >= n) return;
+                                                            int64_t r0, int64_t n, int dim, int ld,
+                                                            _Float16 *__restrict__ Xh) {
+  const int64_t r = r0 + blockIdx.x;
+  if (r >= r0 + n) return;
   const float inv = invc[r];
   for (int c = threadIdx.x; c < ld; c += 256) {
     const float xn = (c < dim ? C[r * ld + c] : 0.f) * inv;  // == dense_scatter_kernel's
@@ -1520,6 +1548,7 @@ struct RowArrays {
   float *C = nullptr, *invc = nullptr;
   uint32_t *live = nullptr;
   _Float16 *Xh = nullptr;
+  int64_t xh_rows = 0;
   int8_t *Xq = nullptr;
   float2 *rmeta = nullptr;
 };
@@ -1527,8 +1556,10 @@ struct RowArrays {
 int dense_alloc_rows(cm_dense *h, int64_t cap, RowArrays &a) {
   a = RowArrays{};
   const size_t nel = (size_t)cap * h->ld;
+  a.xh_rows = xh_rows_for(h, cap);
+  const size_t nel_h = (size_t)a.xh_rows * h->ld;
   if (hipMalloc(&a.C, nel * 4) != hipSuccess || hipMalloc(&a.invc, (size_t)cap * 4) != hipSuccess ||
-      hipMalloc(&a.live, (size_t)cap / 8) != hipSuccess || hipMalloc(&a.Xh, nel * 2) != hipSuccess ||
+      hipMalloc(&a.live, (size_t)cap / 8) != hipSuccess || hipMalloc(&a.Xh, nel_h * 2) != hipSuccess ||
       hipMalloc(&a.Xq, nel) != hipSuccess || hipMalloc(&a.rmeta, (size_t)cap * 8) != hipSuccess) {
     for (void *p : {(void *)a.C, (void *)a.invc, (void *)a.live, (void *)a.Xh, (void *)a.Xq, (void *)a.rmeta})
       if (p) (void)hipFree(p);
@@ -1538,7 +1569,7 @@ int dense_alloc_rows(cm_dense *h, int64_t cap, RowArrays &a) {
   CM_HIP(hipMemsetAsync(a.C, 0, nel * 4, h->stream));
   CM_HIP(hipMemsetAsync(a.invc, 0, (size_t)cap * 4, h->stream));
   CM_HIP(hipMemsetAsync(a.live, 0, (size_t)cap / 8, h->stream));
-  CM_HIP(hipMemsetAsync(a.Xh, 0, nel * 2, h->stream));
+  CM_HIP(hipMemsetAsync(a.Xh, 0, nel_h * 2, h->stream));
   CM_HIP(hipMemsetAsync(a.Xq, 0, nel, h->stream));
   CM_HIP(hipMemsetAsync(a.rmeta, 0, (size_t)cap * 8, h->stream));
   return CM_OK;
@@ -1546,6 +1577,7 @@ int dense_alloc_rows(cm_dense *h, int64_t cap, RowArrays &a) {
 
 void dense_set_rows(cm_dense *h, const RowArrays &a) {
   h->C = a.C, h->invc = a.invc, h->live = a.live, h->Xh = a.Xh, h->Xq = a.Xq, h->rmeta = a.rmeta;
+  h->xh_rows = a.xh_rows;
 }
 
 void dense_free_rows(cm_dense *h) {
@@ -1612,8 +1644,10 @@ int dense_grow(cm_dense *h, int64_t need_rows) {
       return rc2;
     }
     // both coarse planes recomputed from the fp32 rows, bit-identical to the upserts'
-    hipLaunchKernelGGL(dense_replane_kernel, dim3((unsigned)keep), dim3(256), 0, h->stream, a.C, a.invc, keep, h->dim,
-                       h->ld, a.Xh);
+    const int64_t kh = std::min(keep, a.xh_rows);   // the plane's rows (all, or the sample prefix)
+    if (kh > 0)
+      hipLaunchKernelGGL(dense_replane_kernel, dim3((unsigned)kh), dim3(256), 0, h->stream, a.C, a.invc, (int64_t)0, kh,
+                         h->dim, h->ld, a.Xh);
     CM_HIP(hipGetLastError());
     hipLaunchKernelGGL(dense_q8_group_kernel, dim3((unsigned)(keep / 16)), dim3(256), 0, h->stream, a.C, a.invc,
                        (const int64_t *)nullptr, (int64_t)0, keep / 16, h->dim, h->ld, a.Xq, a.rmeta,
@@ -1636,7 +1670,13 @@ int dense_grow(cm_dense *h, int64_t need_rows) {
     CM_HIP(hipMemcpyAsync(a.C, h->C, old * 4, hipMemcpyDeviceToDevice, h->stream));
     CM_HIP(hipMemcpyAsync(a.invc, h->invc, (size_t)keep * 4, hipMemcpyDeviceToDevice, h->stream));
     CM_HIP(hipMemcpyAsync(a.live, h->live, (size_t)keep / 8, hipMemcpyDeviceToDevice, h->stream));
-    CM_HIP(hipMemcpyAsync(a.Xh, h->Xh, old * 2, hipMemcpyDeviceToDevice, h->stream));
+    const int64_t kh_old = std::min(keep, std::min(h->xh_rows, a.xh_rows));   // plane rows both hold
+    if (kh_old > 0)
+      CM_HIP(hipMemcpyAsync(a.Xh, h->Xh, (size_t)kh_old * h->ld * 2, hipMemcpyDeviceToDevice, h->stream));
+    const int64_t kh_new = std::min(keep, a.xh_rows);   // a longer prefix: its new rows from the fp32 data
+    if (kh_new > kh_old)
+      hipLaunchKernelGGL(dense_replane_kernel, dim3((unsigned)(kh_new - kh_old)), dim3(256), 0, h->stream, a.C,
+                         a.invc, kh_old, kh_new - kh_old, h->dim, h->ld, a.Xh);
     CM_HIP(hipMemcpyAsync(a.Xq, h->Xq, old, hipMemcpyDeviceToDevice, h->stream));
     CM_HIP(hipMemcpyAsync(a.rmeta, h->rmeta, (size_t)keep * 8, hipMemcpyDeviceToDevice, h->stream));
   }
@@ -1689,6 +1729,8 @@ int dense_kind(const cm_dense *h, int nq, int k) {
   const bool coarse_ok = k <= kBMaxK && (h->ld == 768 || h->ld == 384) && h->size >= 16384;
   const bool q8_ok = coarse_ok && h->ld == 768;  // K1q / K1q-s: the 6-chunk (ld 768) instances
   if (force == CM_DENSE_F32 || !coarse_ok) return CM_DENSE_F32;
+  if (!xh_full(h))   // the f16 plane holds only the seed-sample prefix: the int8 scans (xh_rows_for)
+    return nq <= kSQ ? CM_DENSE_Q8S : CM_DENSE_Q8;
   if (force == CM_DENSE_COARSE) return CM_DENSE_COARSE;
   if (force == CM_DENSE_STREAM && nq <= kSQ) return CM_DENSE_STREAM;
   if (force == CM_DENSE_Q8 && q8_ok) return CM_DENSE_Q8;
@@ -1781,6 +1823,8 @@ CoarseCfg coarse_config(const cm_dense *h, int nq, int kind) {
   // K1q's per-row bounds widen the candidate set: a denser seed sample keeps it near ~4k per query
   const int64_t frac = c.q8s ? k1qs_sample_frac() : c.q8 ? k1q_sample_frac() : c.rows_end >= (1 << 20) ? 64 : 16;
   c.rows_end_sample = round_up(std::max<int64_t>(c.rows_end / frac, 1), kRRows);
+  if (c.rows_end_sample > h->xh_rows)   // the sample stays inside the f16 plane's prefix (xh_rows_for)
+    c.rows_end_sample = std::max<int64_t>(kRRows, h->xh_rows / kRRows * kRRows);
   // the seed is the k-th smallest of the sample groups' minima: >= kMaxTopK groups whenever the sample
   // has that many tiles, so no k <= kMaxTopK gets an infinite seed at any batch size
   split(c.rows_end_sample, std::max<int64_t>(groups, kMaxTopK), c.rows_per_wg_sample, c.n_wg_sample);
@@ -1965,14 +2009,16 @@ int launch_coarse(cm_dense *h, const float *q_dev, int nq, int k, int kind, cons
     CM_HIP(hipGetLastError());
     }
     hipLaunchKernelGGL(dense_rerank_q8_kernel, dim3(nq), dim3(256), kQRerankLds, st, w.keys, w.ups, w.cnt, c.n_wg, c.qs, k,
-                       nq, h->C, h->ld, h->dim, q_dev, w.qsc, h->Xh, w.qh, w.qnorm, h->rnorm, dist_dev, row_dev,
+                       nq, h->C, h->ld, h->dim, q_dev, w.qsc, xh_full(h) ? h->Xh : nullptr, w.qh, w.qnorm, h->rnorm,
+                       dist_dev, row_dev,
                        w.fb_mask, w.fb_count, w.fb_bound);
     CM_HIP(hipGetLastError());
     // band overflow with complete candidate buffers: the wide re-rank (gated; ~5 us when none failed;
     // CM_K1Q_WIDE=0: the exact scan takes every failing query, A/B)
     if (env_knob("CM_K1Q_WIDE", true))
       hipLaunchKernelGGL(dense_rerank_wide_kernel, dim3(nq), dim3(kWideThreads), 0, st, w.keys, w.cnt, c.n_wg, c.qs, k,
-                         nq, h->C, h->ld, h->dim, q_dev, w.qsc, h->Xh, w.qh, w.qnorm, h->rnorm, h->live, allow,
+                         nq, h->C, h->ld, h->dim, q_dev, w.qsc, xh_full(h) ? h->Xh : nullptr, w.qh, w.qnorm, h->rnorm,
+                         h->Xq, h->rmeta, w.qq, h->live, allow,
                          n_words, c.rows_per_wg, c.rows_end, dist_dev, row_dev, w.fb_mask, w.fb_count, w.fb_bound, w.wide_ctr,
                          w.wide_rows, w.wide_keys);
     CM_HIP(hipGetLastError());
@@ -2191,7 +2237,7 @@ int cm_dense_upsert(cm_dense *h, const float *vecs, const int64_t *rows, int64_t
     CM_HIP(hipMemcpyAsync(h->rows_buf.ptr, rows + s, (size_t)m * 8, hipMemcpyHostToDevice, h->stream));
     hipLaunchKernelGGL(dense_scatter_kernel, dim3((unsigned)m), dim3(256), 0, h->stream, h->staging.as<float>(),
                        h->rows_buf.as<int64_t>(), (int64_t)0, m, h->dim, h->ld, h->C, h->invc, h->live, h->Xh,
-                       reinterpret_cast<uint32_t *>(h->rnorm));
+                       h->xh_rows, reinterpret_cast<uint32_t *>(h->rnorm));
     CM_HIP(hipGetLastError());
     // the int8 plane: every row group the batch touched, once (stream-ordered after the scatter)
     std::vector<int64_t> gs((size_t)m);
@@ -2225,7 +2271,7 @@ int cm_dense_upsert_dev(cm_dense *h, const float *vecs_dev, int64_t row0, int64_
     const int64_t m = std::min(batch, n - s);
     hipLaunchKernelGGL(dense_scatter_kernel, dim3((unsigned)m), dim3(256), 0, st, vecs_dev + s * h->dim,
                        (const int64_t *)nullptr, row0 + s, m, h->dim, h->ld, h->C, h->invc, h->live, h->Xh,
-                       reinterpret_cast<uint32_t *>(h->rnorm));
+                       h->xh_rows, reinterpret_cast<uint32_t *>(h->rnorm));
     CM_HIP(hipGetLastError());
   }
   // the int8 plane of every row group in the written tiles (rows_alloc is a multiple of 128)
@@ -2259,7 +2305,7 @@ int cm_dense_reset(cm_dense *h) {
   CM_HIP(hipMemsetAsync(h->live, 0, (size_t)h->rows_alloc / 8, h->stream));
   CM_HIP(hipMemsetAsync(h->invc, 0, (size_t)h->rows_alloc * 4, h->stream));
   CM_HIP(hipMemsetAsync(h->C, 0, (size_t)h->rows_alloc * h->ld * 4, h->stream));
-  CM_HIP(hipMemsetAsync(h->Xh, 0, (size_t)h->rows_alloc * h->ld * 2, h->stream));
+  CM_HIP(hipMemsetAsync(h->Xh, 0, (size_t)h->xh_rows * h->ld * 2, h->stream));
   CM_HIP(hipMemsetAsync(h->Xq, 0, (size_t)h->rows_alloc * h->ld, h->stream));
   CM_HIP(hipMemsetAsync(h->rmeta, 0, (size_t)h->rows_alloc * 8, h->stream));
   CM_HIP(hipMemsetAsync(h->rnorm, 0, 16, h->stream));
