@@ -84,6 +84,9 @@ def parse_args():
     ap.add_argument("--ingest-e2e-chunks", type=int, default=65536,
                     help="hybrid mode with --ingest-leg, N = 1: chunks through ingest_file's store path (encode_passages "
                          "-> upsert -> upsert_many -> save, files of 4096; reported as ingest_e2e); 0 = off")
+    ap.add_argument("--ingest-e2e-file-chunks", type=int, default=4096,
+                    help="chunks per ingested file in the ingest_e2e leg (the reference saves the whole BM25 JSONL "
+                         "after every file, rag/pipeline/rag.py:413, so the leg's cost grows with files x corpus)")
     ap.add_argument("--no-e5", action="store_true", help="use perturbed corpus rows as query embeddings")
     ap.add_argument("--no-graph", action="store_true", help="run the E5 query encode eagerly (no hipGraph)")
     ap.add_argument("--serial", action="store_true", help="run BM25 on the main stream (no overlap with E5 + dense)")
@@ -923,7 +926,8 @@ def ingest_e2e_leg(args, emb, dev):
     """The reference's ingest of one file (rag/pipeline/rag.py:410-413) repeated over --ingest-e2e-chunks
     chunks in files of 4096: CachingEmbedder(E5).encode_passages -> ChromaVectorStore.upsert
     (persisted) -> BM25Store.upsert_many -> BM25Store.save, each file through the drop-in classes,
-    then the first search's BM25 index build.  chunks/s end to end with the per-stage seconds."""
+    then the first search's BM25 index build.  chunks/s end to end with the per-stage seconds.  Files of
+    --ingest-e2e-file-chunks (4096 by default)."""
     import shutil
     import tempfile
     import numpy as np
@@ -933,7 +937,7 @@ def ingest_e2e_leg(args, emb, dev):
     from classmate_hip.retrieval.vector_store import GpuVectorStore
     if emb is None:
         emb = E5MultilingualEmbedder.random_init(seed=0, device=str(dev), num_layers=args.e5_layers, dtype="float32")
-    n, per_file = args.ingest_e2e_chunks, 4096
+    n, per_file = args.ingest_e2e_chunks, args.ingest_e2e_file_chunks
     rng = np.random.default_rng(args.seed * 11 + 5)
     root = Path(tempfile.mkdtemp(prefix="cm_ingest_", dir=os.environ.get("TMPDIR")))
     try:
@@ -978,9 +982,10 @@ def ingest_e2e_leg(args, emb, dev):
         shutil.rmtree(root, ignore_errors=True)
     leg = {"value": n / total, "unit": "chunks/s", "seconds": total, "chunks": n, "tokens": tok,
            "breakdown_s": {k: v for k, v in st.items() if k != "texts"},
-           "config": {"workload": "ingest_file's store path per file of 4096 chunks (rag/pipeline/rag.py:410-413): "
+           "config": {"workload": "ingest_file's store path per file (rag/pipeline/rag.py:410-413): "
                                   "CachingEmbedder(E5 fp32).encode_passages -> ChromaVectorStore.upsert (persisted) -> "
                                   "BM25Store.upsert_many -> BM25Store.save; + the BM25 device index build",
+                      "chunks_per_file": per_file,
                       "tokens_per_chunk": "U[64, 512]", "files": (n + per_file - 1) // per_file}}
     log(f"ingest_e2e: {leg['value']:.0f} chunks/s over {n} chunks ({total:.1f} s: "
         + ", ".join(f"{k} {v:.1f}" for k, v in leg["breakdown_s"].items()) + ")")

@@ -392,6 +392,7 @@ class ShardedBM25Index(_Shards):
                 tids, off, lv = np.zeros(0, np.int32), np.zeros(1, np.int64), None
             sh.build(tids, off, vocab, lv)
         self.vocab, self.ndocs = int(vocab), int(N)
+        self._prepared = False
         self._install_global_stats()
 
     def _install_global_stats(self):
@@ -466,8 +467,11 @@ class ShardedBM25Index(_Shards):
                     post_pos=np.concatenate(poss)[o], dl=dl)
 
     def prepare_filtered(self, max_docs: int = 0):
+        """Every shard's device log table for idf over the GLOBAL candidate count (up to ndocs)."""
         for sh in self.shards:
-            sh.prepare_filtered(max(int(max_docs), self.ndocs))
+            if sh.num_docs:
+                sh.prepare_filtered(max(int(max_docs), self.ndocs))
+        self._prepared = True
 
     # -- statistics of a where-filter's candidates over all shards (quirk Q2) -------------------
     def _filtered_q_idf(self, flat: np.ndarray, parts_dev):
@@ -621,8 +625,9 @@ class ShardedBM25Index(_Shards):
         global per-term idf (and epsilon) on the host, every shard scored through
         search_stats_dev with the summed statistics, one merge.  Synchronises (statistics)."""
         nq = q_off.numel() - 1
+        if not getattr(self, "_prepared", False):
+            self.prepare_filtered()
         parts = self._parts_dev(allow)
-        flat = q_terms.cpu().numpy().astype(np.int32)
         T = int(q_terms.numel())
         # summed candidate statistics (device tensors per shard) and, when needed, epsilon
         stats = torch.zeros(2, dtype=torch.int64, device=q_terms.device)

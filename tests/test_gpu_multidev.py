@@ -141,8 +141,8 @@ def test_sharded_dense_equals_one_index(block):
     rows = torch.from_numpy(np.concatenate([r0.reshape(-1), [-1, 0, nd - 1]])).cuda()
     assert torch.equal(sh.gather_dev(rows), full.gather_dev(rows))
     assert np.array_equal(sh.export(), full.export())
-    e1, l1 = sh.export(1000, 9000, with_live=True)
-    e0, l0 = full.export(1000, 9000, with_live=True)
+    e1, l1 = sh.export(1024, 9000, with_live=True)
+    e0, l0 = full.export(1024, 9000, with_live=True)
     assert np.array_equal(e0, e1) and np.array_equal(l0, l1)
     full.close()
     sh.close()
