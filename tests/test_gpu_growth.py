@@ -37,9 +37,11 @@ def _grow(index, batches, rows_per_batch, seed):
 
 
 def _row_bytes(rows):
-    """fp32 rows (4 B) + f16 plane (2 B) + int8 plane (1 B) per element; invc + K1q {scale, bound}
-    (12 B) and a live bit per row (cm_dense.hip dense_row_bytes)."""
-    return rows * D * 7 + rows * 12 + rows // 8
+    """fp32 rows (4 B) + int8 plane (1 B) per element, the f16 plane (2 B) over every row -- or, above
+    4M rows of dim 768, over the seed sample's prefix of 1/16 of them (round 6, cm_dense.hip
+    xh_rows_for) -- invc + K1q {scale, bound} (12 B) and a live bit per row (dense_row_bytes)."""
+    xh = rows if (D != 768 or rows <= 4 << 20) else min(rows, -(-(-(-rows // 16)) // 128) * 128)
+    return rows * D * 5 + xh * D * 2 + rows * 12 + rows // 8
 
 
 def _check_search(index, probes):
