@@ -972,6 +972,8 @@ def ingest_e2e_leg(args, emb, dev):
             t = time.perf_counter()
             bm.save()
             st["bm25_save"] += time.perf_counter() - t
+            if per_file >= 16384 or (f0 // per_file) % 4 == 3 or f0 + m >= n:   # progress (long runs)
+                log(f"ingest_e2e: {f0 + m} / {n} chunks ({time.perf_counter() - t_all:.1f} s)")
         t = time.perf_counter()
         bm._ensure_index()                                  # the first search after the ingest builds it
         torch.cuda.synchronize()

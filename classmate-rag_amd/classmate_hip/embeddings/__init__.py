@@ -239,21 +239,33 @@ class E5MultilingualEmbedder:
     def _fmt_passages(texts: Iterable[str]) -> List[str]:
         return [f"passage: {t}" for t in texts]
 
-    def _tokenize(self, texts: List[str]):
-        import torch
+    def _tokenize_host(self, texts: List[str]):
+        """(ids, mask) int64 numpy arrays, padded to the longest text (truncation at 512 tokens)."""
         if isinstance(self.tokenizer, HashTokenizer):
             ids, mask = self.tokenizer(texts)
         else:
             enc = self.tokenizer(texts, padding=True, truncation=True, max_length=MAX_SEQ_LEN, return_tensors="np")
             ids, mask = enc["input_ids"], enc["attention_mask"]
-        return (torch.from_numpy(np.ascontiguousarray(ids)).to(self.device),
-                torch.from_numpy(np.ascontiguousarray(mask)).to(self.device))
+        return np.ascontiguousarray(ids), np.ascontiguousarray(mask)
 
-    def encode_token_ids(self, input_ids, attention_mask, out=None):
+    def _to_dev(self, a: np.ndarray):
+        """A host array on the device through pinned memory, stream-ordered: the host does not wait for
+        the kernels already queued (a pageable copy would), so the next batch's tokenization overlaps
+        the previous batch's forward."""
+        import torch
+        return torch.from_numpy(np.ascontiguousarray(a)).pin_memory().to(self.device, non_blocking=True)
+
+    def _tokenize(self, texts: List[str]):
+        ids, mask = self._tokenize_host(texts)
+        return self._to_dev(ids), self._to_dev(mask)
+
+    def encode_token_ids(self, input_ids, attention_mask, out=None, all_ones: Optional[bool] = None):
         """Device path: (B,S) int ids + mask on the GPU -> (B,768) fp32 unit rows on the GPU.
         Runs the lean forward (padded batches: per-row positions + key-masked SDPA); CM_E5_LEAN=0
         runs the Hugging Face module instead (``_encode_hf``, the reference's computation, which
-        the GPU tests hold the lean forward to: 2e-5 in fp32)."""
+        the GPU tests hold the lean forward to: 2e-5 in fp32).  ``all_ones``: the caller knows whether
+        the mask has padding (True: none, False: some), which spares the forward its device-to-host
+        check of the mask."""
         import torch
         if os.environ.get("CM_E5_LEAN", "1") == "0":
             return self._encode_hf(input_ids, attention_mask, out=out)
@@ -262,7 +274,12 @@ class E5MultilingualEmbedder:
             g = self._small_batch_graph(input_ids, attention_mask)
             if g is not None:
                 return g if out is None else out.copy_(g)
-            hidden = fwd(input_ids, attention_mask)
+            if all_ones is None:
+                hidden = fwd(input_ids, attention_mask)
+            elif all_ones:
+                hidden = fwd(input_ids, None)                       # unpadded path, no mask check
+            else:
+                hidden = fwd(input_ids, attention_mask, padded=True)
             return engine.meanpool_l2norm(hidden, attention_mask, self.normalize, out=out)
 
     _SMALL_B, _SMALL_S = (8, 32)
@@ -557,14 +574,20 @@ class E5MultilingualEmbedder:
     def _rows_independent(self, seq_len: int) -> bool:
         """True when every kernel of the forward computes a row independently of the other rows of
         its batch and of the batch's pad length: the fp32 K10 path (fixed k order per output row,
-        per-row LayerNorm) with the HIP attention of S <= 32 (per-sequence, padded keys leave the
-        softmax exactly).  Torch SDPA (S > 32) and hipBLASLt (bf16, the HF module) may pick kernels
-        by batch shape, so their rows are only reproduced in sentence-transformers' own batches."""
-        if os.environ.get("CM_E5_LEAN", "1") == "0" or seq_len > 32:
+        per-row LayerNorm) with the HIP attention -- K9s for S <= 32 and, since round 6, K9P for
+        32 < S <= 512 (per sequence; padded keys leave the softmax exactly: a masked score is -inf, so
+        an all-masked 64-key chunk leaves the running max, sum and output bit-unchanged).  Torch SDPA
+        and hipBLASLt (bf16, the HF module, CM_E5_PLANES_ATTN=0) may pick kernels by batch shape, so
+        their rows are only reproduced in sentence-transformers' own batches."""
+        if os.environ.get("CM_E5_LEAN", "1") == "0" or seq_len > MAX_SEQ_LEN:
             return False
         self._lean_forward()
-        return bool(getattr(self, "f16x3", False)) and os.environ.get("CM_E5_MASKED_ATTN", "1") != "0" \
-            and os.environ.get("CM_E5_FUSED_ATTN", "1") != "0"
+        env = os.environ.get
+        short_ok = bool(getattr(self, "f16x3", False)) and env("CM_E5_MASKED_ATTN", "1") != "0" \
+            and env("CM_E5_FUSED_ATTN", "1") != "0"
+        if seq_len <= 32:
+            return short_ok
+        return short_ok and env("CM_E5_LONG_ATTN", "1") != "0" and env("CM_E5_PLANES_ATTN", "1") != "0"
 
     def _encode_dev(self, texts: List[str], batch_size: int = 32, group: Optional[int] = None):
         """(len(texts), 768) fp32 device tensor: sentence-transformers' length-sorted batches of
@@ -583,19 +606,35 @@ class E5MultilingualEmbedder:
             return out
         group = max(group or batch_size, batch_size)
         order = np.argsort([-len(t) for t in texts], kind="stable")
+
+        def run(rows: np.ndarray, ids_h, mask_h, lens):
+            """The rows (positions in the group) as one forward, trimmed to their longest; host arrays
+            in, pinned stream-ordered copies: no host wait inside the loop."""
+            w = int(lens[rows].max())
+            m = mask_h[rows, :w]
+            emb = self.encode_token_ids(self._to_dev(ids_h[rows, :w]), self._to_dev(m), all_ones=bool(m.all()))
+            out[self._to_dev(idx[rows])] = emb.float()
+
         for s in range(0, len(texts), group):
             idx = order[s: s + group]
-            ids, mask = self._tokenize([texts[i] for i in idx])
-            # the order's device copy before the launches (a pageable copy waits for the stream)
-            idx_dev = torch.from_numpy(np.ascontiguousarray(idx)).to(self.device)
-            if len(idx) <= batch_size or self._rows_independent(ids.shape[1]):
-                out[idx_dev] = self.encode_token_ids(ids, mask).float()
-                continue
-            lens = mask.sum(1).tolist()
-            for t in range(0, len(idx), batch_size):
-                w = max(lens[t:t + batch_size])
-                out[idx_dev[t:t + batch_size]] = self.encode_token_ids(
-                    ids[t:t + batch_size, :w].contiguous(), mask[t:t + batch_size, :w].contiguous()).float()
+            ids_h, mask_h = self._tokenize_host([texts[i] for i in idx])
+            lens = mask_h.sum(1)
+            allr = np.arange(len(idx))
+            if len(idx) <= batch_size:
+                run(allr, ids_h, mask_h, lens)
+            elif self._rows_independent(ids_h.shape[1]):
+                # one forward per attention path the reference's own batches would take (a 32-text
+                # batch whose longest row has <= 32 tokens runs K9s, a longer one K9P -- every row
+                # of it): per path the rows are batch- and padding-independent, so these forwards
+                # give every row the bits its 32-text batch gives it, with 8x fewer launches
+                bmax = np.repeat([int(lens[t:t + batch_size].max()) for t in range(0, len(idx), batch_size)],
+                                 batch_size)[:len(idx)]
+                for rows in (allr[bmax > 32], allr[bmax <= 32]):
+                    if rows.size:
+                        run(rows, ids_h, mask_h, lens)
+            else:
+                for t in range(0, len(idx), batch_size):
+                    run(allr[t:t + batch_size], ids_h, mask_h, lens)
         return out
 
     def _encode(self, texts: List[str], batch_size: int = 32, group: Optional[int] = None) -> np.ndarray:
@@ -616,8 +655,13 @@ class E5MultilingualEmbedder:
         """encode_queries, left on the device (the batched retrieval path consumes it there)."""
         return self._encode_dev(self._fmt_queries(queries), group=self.query_batch_size)
 
+    # Passages: the same grouping (round 6) -- 256 texts tokenized together, one forward per attention
+    # path of the reference's 32-text batches when the rows are batch-independent (_rows_independent:
+    # the fp32 K10 path with K9s / K9P), else the reference's batches.
+    passage_batch_size = 256
+
     def encode_passages(self, texts: Iterable[str]) -> np.ndarray:
-        return self._encode(self._fmt_passages(texts)).astype("float32", copy=False)
+        return self._encode(self._fmt_passages(texts), group=self.passage_batch_size).astype("float32", copy=False)
 
 
 from .cache import CachingEmbedder  # noqa: E402  (rag/embeddings/cache.py drop-in)

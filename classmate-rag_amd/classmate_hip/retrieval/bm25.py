@@ -159,6 +159,11 @@ class _BState:
         self.sig = None                    # the JSONL (+ sidecar) signature it was loaded from / saved to
         self.unsaved = False               # mutated since: private to its holder
         self.holders = weakref.WeakValueDictionary()   # id(store) -> store (dataclasses are unhashable)
+        # the JSONL + sidecar this state last wrote or read (path, JSONL size / mtime, record count, line
+        # and document offsets, term ids); while only new documents were appended since (append_only),
+        # the next save appends their records instead of rewriting the file (same bytes either way)
+        self.saved: Optional[dict] = None
+        self.append_only = False
         # serialises the state's users (stores attached to it, threads): the device handle's search
         # staging and workspace are per handle (SURVEY §8(b) Threading)
         self.lock = threading.RLock()
@@ -181,6 +186,14 @@ class _BState:
         st.csr = self.csr
         st.version = self.version
         return st
+
+
+def _jsonl_sig(path) -> Optional[tuple]:
+    try:
+        s = os.stat(path)
+        return (s.st_size, s.st_mtime_ns)
+    except OSError:
+        return None
 
 
 def _file_sig(store) -> Optional[tuple]:
@@ -359,6 +372,9 @@ class BM25Store:
         if not (len(ids) == len(texts) == len(metadatas)):
             raise ValueError("ids, texts, metadatas must have the same length")
         self._mutating()
+        st = self._st
+        n0 = len(self._entries)
+        appended = []                  # (row, metadata) of documents new to the store, in insertion order
         for i, doc_id in enumerate(ids):
             text = texts[i] or ""
             meta = dict(metadatas[i] or {})
@@ -367,12 +383,23 @@ class BM25Store:
                 lang = detect_lang_tag(text)
                 meta["language"] = lang
             toks = _tokenize(text, lang_hint=lang)
+            if doc_id in self._entries:  # replaced in place: the saved records are no longer a prefix
+                st.append_only = False
+                appended = None
+            elif appended is not None:
+                appended.append((n0 + len(appended), meta))
             self._entries[doc_id] = _Entry(id=doc_id, text=text, tokens=toks, metadata=meta)
+        meta_ok = not self._meta_dirty
         self._rebuild()
+        if meta_ok and appended is not None:   # the filter columns follow the appended rows
+            for r, meta in appended:
+                self._meta.set(r, meta)
+            self._meta_dirty = False
 
     @_locked
     def delete_many(self, ids: Sequence[str]) -> None:
         self._mutating()
+        self._st.append_only = False
         for doc_id in ids:
             self._entries.pop(doc_id, None)
         self._rebuild()
@@ -440,11 +467,21 @@ class BM25Store:
         side = self.sidecar_dir
         if (side / "meta.json").exists():
             os.remove(side / "meta.json")  # the sidecar is invalid until rewritten below
-        entries = list(self._entries.values())
+        bs = self._st
+        sv = bs.saved
+        n_all = len(self._entries)
+        append = (bs.append_only and sv is not None and sv["path"] == str(self.index_path)
+                  and sv["n"] <= n_all and _jsonl_sig(self.index_path) == sv["sig"])
+        r0 = sv["n"] if append else 0
+        ids_new = self._id_list[r0:] if append else list(self._entries.keys())
+        entries = [self._entries[i] for i in ids_new] if append else list(self._entries.values())
         line_off = np.zeros(len(entries) + 1, np.int64)
         doc_off = np.zeros(len(entries) + 1, np.int64)
         parts = []
-        with self.index_path.open("wb") as f:
+        # the reference rewrites the whole JSONL (bm25.py:220-231); while only documents were appended
+        # since this state's last save or load, the file is that file plus their records: append them
+        with self.index_path.open("ab" if append else "wb") as f:
+            base = f.tell() if append else 0
             for r, e in enumerate(entries):
                 rec = {"id": e.id, "text": e.text, "tokens": e.tokens, "metadata": e.metadata}
                 line = (json.dumps(rec, ensure_ascii=False) + "\n").encode("utf-8")
@@ -454,32 +491,47 @@ class BM25Store:
                     e.term_ids = self._term_ids(e.tokens)
                 parts.append(e.term_ids)
                 doc_off[r + 1] = doc_off[r] + e.term_ids.shape[0]
+        new_terms = np.concatenate(parts) if doc_off[-1] else np.zeros(0, np.int32)
+        if append:
+            line_off = np.concatenate([sv["line_off"], line_off[1:] + base])
+            doc_off = np.concatenate([sv["doc_off"], doc_off[1:] + sv["doc_off"][-1]])
+            terms = np.concatenate([np.asarray(sv["term_ids"], np.int32), new_terms])
+            ids_all = self._id_list
+        else:
+            terms = new_terms
+            ids_all = [e.id for e in entries]
         st = self.index_path.stat()
         tmp = Path(str(side) + ".tmp")
         shutil.rmtree(tmp, ignore_errors=True)
         tmp.mkdir(parents=True)
-        np.save(tmp / "term_ids.npy", np.concatenate(parts) if doc_off[-1] else np.zeros(0, np.int32))
+        np.save(tmp / "term_ids.npy", terms)
         np.save(tmp / "doc_off.npy", doc_off)
         np.save(tmp / "line_off.npy", line_off)
         vocab = [None] * len(self._vocab)
         for t, i in self._vocab.items():
             vocab[i] = t
         (tmp / "vocab.json").write_text(json.dumps(vocab, ensure_ascii=False), encoding="utf-8")
-        (tmp / "ids.json").write_text(json.dumps([e.id for e in entries], ensure_ascii=False), encoding="utf-8")
+        (tmp / "ids.json").write_text(json.dumps(list(ids_all), ensure_ascii=False), encoding="utf-8")
         # the where-filter columns (filters.MetaIndex), so a sidecar open can filter without parsing
         # every record's metadata (10M records: ~100 s of JSON before the first filtered search)
         self._ensure_meta()
         ms = self._meta.snapshot()
-        if ms is not None and ms[0]["rows"] <= len(entries):
+        if ms is not None and ms[0]["rows"] <= len(ids_all):
             info, arrays = ms
             for k, a in arrays.items():
                 np.save(tmp / f"meta_{k}.npy", a)
             (tmp / "meta_info.json").write_text(json.dumps(info, ensure_ascii=False), encoding="utf-8")
         (tmp / "meta.json").write_text(json.dumps({
-            "version": _SIDECAR_VERSION, "docs": len(entries), "postings": int(doc_off[-1]),
+            "version": _SIDECAR_VERSION, "docs": len(ids_all), "postings": int(doc_off[-1]),
             "jsonl_size": st.st_size, "jsonl_mtime_ns": st.st_mtime_ns}), encoding="utf-8")
         shutil.rmtree(side, ignore_errors=True)
         os.replace(tmp, side)
+        del terms    # (the saved arrays are kept memory-mapped from the new sidecar, not in RAM)
+        bs.saved = dict(path=str(self.index_path), sig=(st.st_size, st.st_mtime_ns), n=len(ids_all),
+                        line_off=np.load(side / "line_off.npy", mmap_mode="r"),
+                        doc_off=np.load(side / "doc_off.npy", mmap_mode="r"),
+                        term_ids=np.load(side / "term_ids.npy", mmap_mode="r"))
+        bs.append_only = True
         # the state matches the files again: later load()s of this index attach to it
         st = self._st
         st.sig, st.unsaved = _file_sig(self), False
@@ -525,6 +577,9 @@ class BM25Store:
         self._version += 1
         self._csr = (term_ids, doc_off)
         self._dirty = self._meta_dirty = True
+        self._st.saved = dict(path=str(self.index_path), sig=(meta["jsonl_size"], meta["jsonl_mtime_ns"]), n=n,
+                              line_off=line_off, doc_off=doc_off, term_ids=term_ids)
+        self._st.append_only = True
         meta = _load_meta_snapshot(side, n, cat, self._id_list)
         if meta is not None:   # filter columns restored; a row's metadata dict is parsed on demand
             self._meta, self._meta_dirty = meta, False

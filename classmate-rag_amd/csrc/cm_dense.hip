@@ -1729,8 +1729,10 @@ int dense_kind(const cm_dense *h, int nq, int k) {
   const bool coarse_ok = k <= kBMaxK && (h->ld == 768 || h->ld == 384) && h->size >= 16384;
   const bool q8_ok = coarse_ok && h->ld == 768;  // K1q / K1q-s: the 6-chunk (ld 768) instances
   if (force == CM_DENSE_F32 || !coarse_ok) return CM_DENSE_F32;
-  if (!xh_full(h))   // the f16 plane holds only the seed-sample prefix: the int8 scans (xh_rows_for)
+  if (!xh_full(h)) {   // the f16 plane holds only the seed-sample prefix: the int8 scans (xh_rows_for)
+    if (force == CM_DENSE_Q8) return CM_DENSE_Q8;
     return nq <= kSQ ? CM_DENSE_Q8S : CM_DENSE_Q8;
+  }
   if (force == CM_DENSE_COARSE) return CM_DENSE_COARSE;
   if (force == CM_DENSE_STREAM && nq <= kSQ) return CM_DENSE_STREAM;
   if (force == CM_DENSE_Q8 && q8_ok) return CM_DENSE_Q8;

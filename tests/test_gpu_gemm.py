@@ -336,3 +336,25 @@ def test_e5_passage_planes_attention_matches_hf(monkeypatch, S, cut):
     emb._lean = None
     old = emb.encode_token_ids(ids, mask)
     torch.testing.assert_close(got, old, atol=2e-5, rtol=0)
+
+
+def test_e5_passage_groups_equal_reference_batches_bit_for_bit():
+    """encode_passages (round 6) tokenizes 256 texts at once and runs one forward per attention path
+    of sentence-transformers' 32-text batches (rag/embeddings/__init__.py:98-105); every row must get
+    exactly the bits its own 32-text batch gives it (group=32: the reference's batches one by one) --
+    texts from 3 to ~500 words, so batches with padding on both paths (K9s at <= 32 tokens, K9P
+    above, incl. short rows inside a long batch and lengths that are not multiples of 64)."""
+    import random
+    from classmate_hip.embeddings import E5MultilingualEmbedder
+    emb = E5MultilingualEmbedder.random_init(seed=3, device="cuda", num_layers=2, dtype="float32")
+    rng = random.Random(11)
+    words = [f"w{i}" for i in range(3000)]
+    lens = [3, 4, 5, 7, 20, 25, 26, 27, 28, 29, 40, 60, 61, 62, 125, 126, 200, 317, 400, 507, 520]
+    lens += [rng.randint(3, 520) for _ in range(280)]
+    rng.shuffle(lens)
+    texts = [" ".join(rng.choice(words) for _ in range(n)) for n in lens]
+    grouped = emb.encode_passages(texts)
+    ref = emb._encode(emb._fmt_passages(texts), batch_size=32, group=32)
+    assert grouped.shape == (len(texts), 768)
+    assert np.array_equal(grouped, ref)
+    E5MultilingualEmbedder.release_all()

@@ -197,3 +197,59 @@ def test_meta_index_snapshot_round_trip():
                     a(w)
                 continue
             assert (a(w) == want).all(), w
+
+
+def test_bm25_save_appends_when_only_documents_were_added(tmp_path):
+    """ingest_file saves the whole BM25 catalog after every file (rag/pipeline/rag.py:413).  While a
+    state only gained new documents since its last save (or sidecar load), save() appends their
+    records: the JSONL and the sidecar must be byte-identical to a full rewrite of the same content
+    (a fresh store saving everything once), and a replaced or deleted document forces the rewrite."""
+    import numpy as np
+    B.release_all()
+
+    def files(d):
+        side = d / "bm25_index.jsonl.cm"
+        out = {"jsonl": (d / "bm25_index.jsonl").read_bytes()}
+        for k in ("term_ids", "doc_off", "line_off"):
+            out[k] = np.load(side / f"{k}.npy").tobytes()
+        for k in ("ids.json", "vocab.json"):
+            out[k] = (side / k).read_text()
+        out["cols"] = {p.name: np.load(p).tobytes() for p in side.glob("meta_*.npy")}
+        return out
+
+    ids, texts, metas = _docs(60, "p")
+    inc = B.BM25Store.load_or_create(tmp_path / "inc")
+    for s0 in range(0, 60, 20):                         # three "files", saved after each
+        inc.upsert_many(ids=ids[s0:s0 + 20], texts=texts[s0:s0 + 20], metadatas=metas[s0:s0 + 20])
+        size_before = (tmp_path / "inc" / "bm25_index.jsonl").stat().st_size if s0 else 0
+        inc.save()
+        assert inc._st.append_only
+    once = B.BM25Store.load_or_create(tmp_path / "once")
+    once.upsert_many(ids=ids, texts=texts, metadatas=metas)
+    once.save()
+    a, b = files(tmp_path / "inc"), files(tmp_path / "once")
+    assert a == b and size_before > 0
+    # a sidecar-opened store (another process) appending: still identical
+    B.release_all()
+    more_ids, more_texts, more_metas = _docs(15, "q")
+    again = B.BM25Store.load_or_create(tmp_path / "inc")
+    assert again._st.append_only and again._st.saved["n"] == 60
+    again.upsert_many(ids=more_ids, texts=more_texts, metadatas=more_metas)
+    again.save()
+    once.upsert_many(ids=more_ids, texts=more_texts, metadatas=more_metas)
+    once.save()
+    assert files(tmp_path / "inc") == files(tmp_path / "once")
+    # a replaced document: the full rewrite (same bytes as the fresh store's)
+    for s in (again, once):
+        s.upsert_many(ids=[ids[3]], texts=["replaced words here"], metadatas=[{"language": "en", "course": "CX"}])
+    assert not again._st.append_only
+    again.save()
+    once.save()
+    assert files(tmp_path / "inc") == files(tmp_path / "once")
+    # filters over the incrementally maintained metadata columns == a full rebuild's
+    B.release_all()
+    fresh = B.BM25Store.load_or_create(tmp_path / "inc")
+    fresh._ensure_meta()
+    again._meta_dirty = False
+    for w in ({"course": "C1"}, {"course": "CX"}, {"course": None}):
+        assert (again._meta.bm25_mask(w) == fresh._meta.bm25_mask(w)).all(), w
