@@ -8,6 +8,7 @@ epilogue against torch's F.gelu (exact erf) of the fp64 product.  The E5 forward
 held to the Hugging Face fp32 module at 2e-5 (test_gpu_scale.py C3 at B = 32, S = 256, and the
 query shape B = 256, S = 24 below).
 """
+import numpy as np
 import pytest
 
 pytestmark = pytest.mark.gpu
