@@ -1482,6 +1482,45 @@ def construct_leg(args, vs, bm, embedder, qs, K, dev, none_keys, lat):
         out["overhead_vs_bare_ms"] = out["p50_ms"] - out["bare_retrieve_p50_ms"]
         log(f"construct-then-retrieve: p50 {out['p50_ms']:.2f} ms (bare retrieve {out['bare_retrieve_p50_ms']:.2f} ms), "
             f"p99 {out['p99_ms']:.2f} ms")
+        # the tail's anatomy (a separate pass, so the introspection does not touch the timings above):
+        # every collection's generation, duration, object count of the collected generations, largest
+        # container in them and objects freed; then the same calls after gc.freeze() (the startup
+        # objects moved to the permanent generation, as a serving process would do after warm-up)
+        diag = []
+
+        def gc_diag(ev, info, _s={}):
+            if ev == "start":
+                objs = [o for g in range(info["generation"] + 1) for o in gc.get_objects(g)]
+                big = max(objs, key=lambda o: len(o) if isinstance(o, (list, dict, set, tuple)) else 0, default=None)
+                _s["n"] = len(objs)
+                _s["big"] = [type(big).__name__, len(big) if isinstance(big, (list, dict, set, tuple)) else 0]
+                del objs, big
+                _s["t"] = time.perf_counter()
+            else:
+                diag.append(dict(gen=info["generation"], ms=round((time.perf_counter() - _s["t"]) * 1e3, 2),
+                                 objects=_s["n"], largest=_s["big"], collected=info["collected"]))
+        gc.callbacks.append(gc_diag)
+        try:
+            for i in range(args.e2e_latency_queries):
+                ask(qs[200 + i])
+        finally:
+            gc.callbacks.remove(gc_diag)
+        out["gc_events"] = dict(n=len(diag), slowest=sorted(diag, key=lambda d: -d["ms"])[:4],
+                                by_gen={g: sum(1 for d in diag if d["gen"] == g) for g in range(3)})
+        gc.freeze()
+        try:
+            tf = []
+            for i in range(args.e2e_latency_queries):
+                t1 = time.perf_counter()
+                ask(qs[300 + i])
+                tf.append((time.perf_counter() - t1) * 1e3)
+        finally:
+            gc.unfreeze()
+        tf.sort()
+        out["after_gc_freeze"] = dict(p50_ms=tf[len(tf) // 2], p99_ms=tf[min(len(tf) - 1, int(len(tf) * 0.99))],
+                                      n=len(tf), frozen_note="gc.freeze() after the warm-up (serving-process practice)")
+        log(f"construct-then-retrieve gc: {out['gc_events']['n']} collections, slowest {out['gc_events']['slowest'][:2]}; "
+            f"after gc.freeze(): p50 {out['after_gc_freeze']['p50_ms']:.2f} ms, p99 {out['after_gc_freeze']['p99_ms']:.2f} ms")
         del v0, b0
     finally:
         stop.set()

@@ -39,7 +39,7 @@ from typing import Any, Dict, List, Mapping, Optional, Sequence
 import numpy as np
 
 from .. import engine, multidev
-from .filters import MetaIndex, next_uid
+from .filters import MetaIndex, next_uid, settle_loaded
 from .tokenize import _tokenize, detect_lang_tag
 
 
@@ -613,6 +613,7 @@ class BM25Store:
                     rec = json.loads(line)
                     self._entries[rec["id"]] = _entry_of(rec)
             self._rebuild()
+        settle_loaded()
         st = self._st
         st.sig, st.unsaved = sig, False
         with _REG_LOCK:

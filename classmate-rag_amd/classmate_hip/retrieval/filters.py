@@ -95,6 +95,18 @@ def next_uid() -> int:
     return next(_UIDS)
 
 
+def settle_loaded() -> None:
+    """After a cold open: move the objects it just built out of the young generations.  A 10M-row
+    open creates a few 10M-entry id lists as single container allocations, too few to trigger a
+    collection, so they sat in generation 0 until the first request's gen-0 collection traversed
+    them: a one-time ~15 ms stall inside that request (the construct-then-retrieve p99 at 10M,
+    bench.py's gc diagnostics).  One gen-1 collection here traverses them during the open instead
+    and promotes them to the oldest generation."""
+    import gc
+    if gc.isenabled():
+        gc.collect(1)
+
+
 class _Column:
     __slots__ = ("py", "ty", "py_map", "ty_map", "n_odd")
 

@@ -48,7 +48,7 @@ from typing import Any, Dict, List, Mapping, Optional, Sequence
 import numpy as np
 
 from .. import engine, multidev
-from .filters import MetaIndex, next_uid
+from .filters import MetaIndex, next_uid, settle_loaded
 
 
 _FORMAT = 2
@@ -256,6 +256,7 @@ class GpuVectorStore:
         d = self._dir
         if d is not None and (d / "meta.json").exists():
             self._load_from(d)
+            settle_loaded()
 
     def _load_from(self, d: Path):
         """Open the directory: from the snapshot + the log records appended after it when the
