@@ -2010,7 +2010,7 @@ int launch_coarse(cm_dense *h, const float *q_dev, int nq, int k, int kind, cons
     h->timer.end(st);
     CM_HIP(hipGetLastError());
     }
-    hipLaunchKernelGGL(dense_rerank_q8_kernel, dim3(nq), dim3(256), kQRerankLds, st, w.keys, w.ups, w.cnt, c.n_wg, c.qs, k,
+    hipLaunchKernelGGL(dense_rerank_q8_kernel, dim3(nq), dim3(kQRT), kQRerankLds, st, w.keys, w.ups, w.cnt, c.n_wg, c.qs, k,
                        nq, h->C, h->ld, h->dim, q_dev, w.qsc, xh_full(h) ? h->Xh : nullptr, w.qh, w.qnorm, h->rnorm,
                        dist_dev, row_dev,
                        w.fb_mask, w.fb_count, w.fb_bound);

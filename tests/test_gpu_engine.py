@@ -157,7 +157,7 @@ def test_dense_coarse_certificate(eng, path):
     # near-duplicates of one vector (cosine gaps ~1e-8, far inside the 2E band): 600 overflow
     # K1c's 64-slot (range, query) buffers; K1s's 1024 small groups hold them, so it gets a
     # cluster wider than the re-rank band cap (1024 rows) instead; the int8 kinds get one wider
-    # than their 8192-row band
+    # than their 4096-row band
     nd = {3: 600, 4: 1500, 5: 9000, 6: 9000}[path]
     base = rng.standard_normal(dim).astype(np.float32)
     dup = base + 1e-4 * rng.standard_normal((nd, dim)).astype(np.float32)

@@ -95,7 +95,7 @@ def test_prefix_plane_growth_replanes_new_prefix_rows(data, monkeypatch):
 
 def test_prefix_plane_clusters_band_overflow_and_overflowed_groups(monkeypatch):
     """The two certificate overflows without a full f16 plane: a scattered 12k-row near-duplicate
-    cluster (int8 band > 8192 rows: the wide re-rank from the candidate buffers) and a contiguous
+    cluster (int8 band > 4096 rows: the wide re-rank from the candidate buffers) and a contiguous
     3k-row one (overflowed (group, query) buffers: their groups re-scanned on the int8 plane with the
     scan's per-row bound) -- lists equal to the fp64 oracle, finished by the wide re-rank."""
     rng = np.random.default_rng(93)

@@ -194,7 +194,7 @@ def test_q8_device_search_and_workspace(store):
 
 def test_q8_band_overflow_takes_exact_fallback():
     """Near-duplicate chunks (real corpora hold them; the synthetic bench never does): 12 000 rows
-    within 5e-4 of one base row put far more rows inside the int8 certificate than its 8192-row
+    within 5e-4 of one base row put far more rows inside the int8 certificate than its 4096-row
     band holds, so the re-rank hands those queries to the wide re-rank (every band row's exact fp64
     distance from the complete candidate buffers; round 5) -- or, with it off, to the exact fp32 K1
     pass (fb_mask), whose merge writes only their rows.  Every list -- cluster and ordinary queries in one batch -- must
