@@ -62,8 +62,11 @@ def _stores_locked(retr):
     """The vector store's collection lock, then the BM25 store's (always in this order, so two
     retrievers sharing a store cannot deadlock), held across one retrieve: concurrent callers --
     each ask_question thread building its own stores on one directory -- are serialised on the
-    handles they share (SURVEY §8(b) Threading; rag/pipeline/rag.py:531-534).  Stores without a
-    ``lock()`` (the reference's own classes) are not locked."""
+    handles they share (SURVEY §8(b) Threading; rag/pipeline/rag.py:531-534).  It also keeps a
+    deferred dense search and its exact fallback (device_batch: search_dev(defer_exact=True) ...
+    exact_fallback_dev, the shared index workspace and the kind chosen at search time) inside one
+    critical section, so no other request's search or upsert lands between them.  Stores
+    without a ``lock()`` (the reference's own classes) are not locked."""
     with contextlib.ExitStack() as stack:
         for s in (retr.vector_store, retr.bm25_store):
             lk = getattr(s, "lock", None)
