@@ -493,7 +493,8 @@ def main():
         roofs["bm25"] = _bm25_roofline(bm25, q_terms, N, bm25_ms, _pmc_traffic(args, "bm25"), args.q_terms)
         if bm25b_ms is not None:
             roofs["bm25_block"] = _bm25_block_roofline(bm25, q_terms, bm25.workspace_items(B, q_terms.numel(), K, bws),
-                                                       bm25b_ms, _pmc_traffic(args, "bm25b"), args.q_terms)
+                                                       bm25b_ms, _pmc_traffic(args, "bm25b"), args.q_terms,
+                                                       bm25.workspace_subblocks(B, q_terms.numel(), K, bws))
     # the headline roofline: the kernel with the most algorithmic work per step (K1q: 7.76 GB per launch
     # against K2a's 0.25 GB).  In-step launch times are not a fair ranking: the two run side by side and
     # whichever starts second is stretched by the other (rooflines.bm25 keeps K2a's line either way)
@@ -647,11 +648,12 @@ def _bm25_roofline(bm25, q_terms, N, ms, traffic, terms_per_query):
     return r
 
 
-def _bm25_block_roofline(bm25, q_terms, items, ms, traffic, terms_per_query):
-    """K2b (bm25_block_kernel: the head-only documents of the planned 64-doc blocks) per launch,
-    algorithmic bytes: every planned block's 64 documents read once -- one tf byte per head term of
-    its query (the dense tiles) + the 4-B length -- plus 16 B of live / allow words per block and
-    the 8-B item itself.  Planned items from the last timed step's workspace."""
+def _bm25_block_roofline(bm25, q_terms, items, ms, traffic, terms_per_query, sub_masks=None):
+    """K2b (bm25_block_kernel: the head-only documents of the planned 16-doc sub-blocks; 64-doc blocks
+    before round 6) per launch, algorithmic bytes: every planned sub-block's 16 documents read once --
+    one tf byte per head term of its query (the dense tiles) + the 4-B length -- plus 8 B of live /
+    allow words per sub-block and the item's 16 B (range word + sub-block mask).  Planned items from
+    the last timed step's workspace."""
     import numpy as np
     df, _ = bm25.term_stats()
     nh = bm25.num_head_terms
@@ -660,11 +662,16 @@ def _bm25_block_roofline(bm25, q_terms, items, ms, traffic, terms_per_query):
     nh_q = np.array([int((df[row[(row >= 0) & (row < df.shape[0])]] >= head_df).sum()) for row in qt], np.int64)
     q = (items >> np.uint64(40)).astype(np.int64)
     nblk = np.array([bin(int(x)).count("1") for x in (items & np.uint64(0xFFFF)).tolist()], np.int64)
-    bytes_ = float((nblk * (64 * (nh_q[q] + 4) + 16)).sum() + 8 * items.shape[0])
+    if sub_masks is None or sub_masks.shape[0] != items.shape[0]:
+        sub_masks = np.array([sum(0xF << (4 * b) for b in range(16) if (int(x) >> b) & 1)
+                              for x in (items & np.uint64(0xFFFF)).tolist()], np.uint64)
+    nsub = np.array([bin(int(x)).count("1") for x in sub_masks.tolist()], np.int64)
+    bytes_ = float((nsub * (16 * (nh_q[q] + 4) + 8)).sum() + 16 * items.shape[0])
     r = _roof(bytes_, 0.0, 1.0, ms)
-    r.update(traffic=traffic, kernel="K2b bm25_block_kernel (head-only documents of the planned 64-doc blocks)",
+    r.update(traffic=traffic, kernel="K2b bm25_block_kernel (head-only documents of the planned 16-doc sub-blocks)",
              avg_launch_ms=ms, algorithmic_per_launch=dict(bytes=bytes_, items=int(items.shape[0]),
-                                                           blocks=int(nblk.sum()), docs=int(nblk.sum()) * 64))
+                                                           blocks=int(nblk.sum()), subblocks=int(nsub.sum()),
+                                                           docs=int(nsub.sum()) * 16))
     return r
 
 

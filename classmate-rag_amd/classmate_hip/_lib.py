@@ -103,6 +103,7 @@ SIGNATURES = {
     "cm_bm25_set_stats": (c_int, c_vp, c_vp, c_i32, c_i64, c_i64, c_f64),
     "cm_bm25_search": (c_int, c_vp, c_vp, c_vp, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp),
     "cm_bm25_workspace_items": (c_i64, c_vp, c_i32, c_i32, c_i32, c_vp, c_vp, c_i64),
+    "cm_bm25_workspace_subblocks": (c_i64, c_vp, c_i32, c_i32, c_i32, c_vp, c_vp, c_i64),
     "cm_bm25_timing_drain_block": (c_i32, c_vp, c_vp, c_i32),
     "cm_bm25_search_idf": (c_int, c_vp, c_vp, c_vp, c_i32, c_i32, c_vp, c_vp, c_f64, c_i64, c_vp, c_vp, c_vp),
     "cm_bm25_search_workspace": (c_i64, c_vp, c_i32, c_i32, c_i32),

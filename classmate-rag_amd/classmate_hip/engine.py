@@ -381,6 +381,15 @@ class BM25Index:
             raise RuntimeError(L.last_error() or "no planned items (full path?)")
         return buf[:min(n, cap)]
 
+    def workspace_subblocks(self, nq: int, total_terms: int, k: int, workspace, cap: int = 1 << 22) -> np.ndarray:
+        """The planned items' 16-doc sub-block masks (bit 4 b + x), item for item with workspace_items."""
+        buf = np.zeros(cap, np.uint64)
+        n = int(L.fn["cm_bm25_workspace_subblocks"](self._h, int(nq), int(total_terms), int(k), L.ptr(workspace),
+                                                     L.ptr(buf), int(cap)))
+        if n < 0:
+            raise RuntimeError(L.last_error() or "no planned items (full path?)")
+        return buf[:min(n, cap)]
+
     @property
     def num_head_terms(self) -> int:
         return int(L.fn["cm_bm25_num_head_terms"](self._h))

@@ -1133,6 +1133,7 @@ struct cm_bm25 {
   DevBuf head_maxtf, range_mindl;  // pruned search: per-(head, range) max tf, per-range min length
   DevBuf blk_maxtf, blk_mindl;     // the same per 64-doc block
   DevBuf blk_maxr;                 // per (head, 64-doc block): ceil-quantised max ratio tf.2.5/(tf + K_d)
+  DevBuf blk16_maxr;               // the same per (head, 16-doc sub-block): the planner's sub-block level
   double maxr_avgdl = 0.0;         // ... at this avgdl: a valid bound for every search avgdl <= it
   int32_t path = 0;                // 0 auto (pruned), 1 full K2 scan, 2 pruned
   int32_t last_rescored = 0;       // (query, range) pairs K2 re-scored in the last host search
@@ -1283,10 +1284,15 @@ int build_head_tiles(cm_bm25 *h, const std::vector<int32_t> &df) {
     // it also bounds searches whose avgdl is somewhat larger: other shards' global statistics)
     h->maxr_avgdl = h->avgdl > 0.0 ? h->avgdl * 1.05 : 0.0;
     if (h->maxr_avgdl > 0.0) {
-      if ((rc = h->blk_maxr.ensure((size_t)h->nhead * nblk))) return rc;
+      if ((rc = h->blk_maxr.ensure((size_t)h->nhead * nblk)) || (rc = h->blk16_maxr.ensure((size_t)h->nhead * nblk * 4)))
+        return rc;
       hipLaunchKernelGGL(bm25_blk_maxratio_kernel, dim3((unsigned)ceil_div((int64_t)h->nhead * nblk, 256)),
                          dim3(256), 0, h->stream, h->headtf.as<uint8_t>(), h->npad, h->dl.as<int32_t>(), h->ndocs,
-                         nblk, h->nhead, h->maxr_avgdl, h->blk_maxr.as<uint8_t>());
+                         nblk, h->nhead, h->maxr_avgdl, h->blk_maxr.as<uint8_t>(), 64);
+      CM_HIP(hipGetLastError());
+      hipLaunchKernelGGL(bm25_blk_maxratio_kernel, dim3((unsigned)ceil_div((int64_t)h->nhead * nblk * 4, 256)),
+                         dim3(256), 0, h->stream, h->headtf.as<uint8_t>(), h->npad, h->dl.as<int32_t>(), h->ndocs,
+                         nblk * 4, h->nhead, h->maxr_avgdl, h->blk16_maxr.as<uint8_t>(), 16);
       CM_HIP(hipGetLastError());
     }
   }
@@ -1317,6 +1323,7 @@ struct BmWs {
   uint32_t *cand_row;
   uint8_t *need;  // [query groups][ranges] re-score bits (pruned search)
   uint64_t *items;  // K2b work items (pruned search)
+  uint64_t *items_sm;  // per item: its planned 16-doc sub-blocks (bit 4 b + x)
   uint8_t *qcand;   // per query term: postings walked
   int32_t *qd_code;  // [nq][kTermLanes] K2b term descriptors (bm25_qcand_kernel)
   double *qd_idf;
@@ -1351,6 +1358,8 @@ BmWs bm_ws_layout(const cm_bm25 *h, int nq, int total_terms, int k, void *base) 
   w.need = reinterpret_cast<uint8_t *>(p + off);
   off += round_up(ceil_div(std::max(nq, 1), kQPerWave) * nr, 256);
   w.items = reinterpret_cast<uint64_t *>(p + off);  // at most one item per (query, range)
+  off += round_up((int64_t)std::max(nq, 1) * nr * 8, 256);
+  w.items_sm = reinterpret_cast<uint64_t *>(p + off);
   off += round_up((int64_t)std::max(nq, 1) * nr * 8, 256);
   w.item_count = reinterpret_cast<uint32_t *>(p + off);
   off += 256;
@@ -1455,14 +1464,17 @@ int bm25_launch_core(cm_bm25 *h, const int32_t *q_terms_dev, const int32_t *q_of
                        h->range_mindl.as<int32_t>(), h->blk_maxtf.as<uint8_t>(), h->blk_mindl.as<int32_t>(),
                        (h->nhead && h->maxr_avgdl > 0.0) ? h->blk_maxr.as<uint8_t>() : (const uint8_t *)nullptr,
                        h->maxr_avgdl, nr, (int64_t)nr * (kRange / 64), avgdl, k, score_dev, row_dev, w.need, w.items,
-                       w.item_count);
+                       w.item_count,
+                       (h->nhead && h->maxr_avgdl > 0.0 && !env_knob("CM_BM25_SUB16_OFF", false))
+                           ? h->blk16_maxr.as<uint8_t>() : (const uint8_t *)nullptr,
+                       w.items_sm);
     CM_HIP(hipGetLastError());
     // K2b: head-only documents of the planned blocks, merged into the tail pass's lists
     h->timer_b.begin(st);
     hipLaunchKernelGGL(bm25_block_kernel, dim3(K2B_GRID), dim3(256), 0, st, w.items, w.item_count, w.qd_code,
                        w.qd_idf, w.qd_tb, w.bounds, nr, h->post_doc.as<int32_t>(), h->headtf.as<uint8_t>(), h->npad,
                        h->dl.as<int32_t>(), h->live.as<uint32_t>(), allow_dev, h->ndocs, avgdl, k, score_dev, nq,
-                       w.cand_key, w.cand_row);
+                       w.cand_key, w.cand_row, w.items_sm);
     h->timer_b.end(st);
     CM_HIP(hipGetLastError());
   }
@@ -1496,7 +1508,7 @@ int32_t count_rescored(cm_bm25 *h, int nq, const BmWs &w, hipStream_t st) {
 void bm25_free(cm_bm25 *h) {
   for (DevBuf *b : {&h->term_off, &h->post_doc, &h->post_tf, &h->post_pos, &h->dl, &h->live, &h->idf, &h->ws,
                     &h->qbuf, &h->obuf, &h->allow_buf, &h->tmp, &h->headtf, &h->head_id, &h->head_maxtf,
-                    &h->range_mindl, &h->blk_maxtf, &h->blk_mindl, &h->blk_maxr})
+                    &h->range_mindl, &h->blk_maxtf, &h->blk_mindl, &h->blk_maxr, &h->blk16_maxr})
     b->release();
 }
 
@@ -1936,6 +1948,24 @@ int64_t cm_bm25_workspace_items(cm_bm25 *h, int32_t nq, int32_t total_terms, int
   const int64_t m = std::min<int64_t>(n, cap);
   if (m > 0 && items_out &&
       (hipMemcpyAsync(items_out, w.items, (size_t)m * 8, hipMemcpyDeviceToHost, h->stream) != hipSuccess ||
+       hipStreamSynchronize(h->stream) != hipSuccess))
+    return -1;
+  return n;
+}
+
+int64_t cm_bm25_workspace_subblocks(cm_bm25 *h, int32_t nq, int32_t total_terms, int32_t k, const void *workspace_dev,
+                                    uint64_t *masks_out, int64_t cap) {
+  if (!h || !workspace_dev || nq <= 0 || k <= 0 || cap < 0) return -1;
+  if (h->path == 1) return -1;
+  DeviceGuard dg(h->dev);
+  const BmWs w = bm_ws_layout(h, nq, total_terms, k, const_cast<void *>(workspace_dev));
+  uint32_t n = 0;
+  if (hipMemcpyAsync(&n, w.item_count, 4, hipMemcpyDeviceToHost, h->stream) != hipSuccess ||
+      hipStreamSynchronize(h->stream) != hipSuccess)
+    return -1;
+  const int64_t m = std::min<int64_t>(n, cap);
+  if (m > 0 && masks_out &&
+      (hipMemcpyAsync(masks_out, w.items_sm, (size_t)m * 8, hipMemcpyDeviceToHost, h->stream) != hipSuccess ||
        hipStreamSynchronize(h->stream) != hipSuccess))
     return -1;
   return n;

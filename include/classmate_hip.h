@@ -228,6 +228,11 @@ int32_t cm_bm25_last_rescored(cm_bm25 *h);
  * 1024-doc range << 16 | 64-doc block mask) -- bench.py prices K2b's algorithmic bytes with them. */
 int64_t cm_bm25_workspace_items(cm_bm25 *h, int32_t nq, int32_t total_terms, int32_t k, const void *workspace_dev,
                                 uint64_t *items_out, int64_t cap);
+/* the same items' planned 16-doc sub-blocks (bit 4 b + x = sub-block x of 64-doc block b of the
+ * item's range; round 6: K2b scores only these) -- item i's mask is masks_out[i].  New: the planner
+ * refines the reference-free block plan above, so no reference interface corresponds to it. */
+int64_t cm_bm25_workspace_subblocks(cm_bm25 *h, int32_t nq, int32_t total_terms, int32_t k, const void *workspace_dev,
+                                    uint64_t *masks_out, int64_t cap);
 /* kernel timing (bench roofline): events around every search's K2 launch;
  * same contract as cm_dense_timing / cm_dense_timing_drain.              */
 int cm_bm25_timing(cm_bm25 *h, int32_t enable);
