@@ -1454,7 +1454,8 @@ int bm25_launch_core(cm_bm25 *h, const int32_t *q_terms_dev, const int32_t *q_of
                        h->nhead ? h->blk_maxtf.as<uint8_t>() : (const uint8_t *)nullptr, h->blk_mindl.as<int32_t>(),
                        h->maxr_avgdl, (int64_t)nr * (kRange / 64),
                        h->nhead ? h->head_maxtf.as<uint8_t>() : (const uint8_t *)nullptr, h->range_mindl.as<int32_t>(),
-                       bm25_debug_flags());
+                       bm25_debug_flags(),
+                       (h->nhead && h->maxr_avgdl > 0.0) ? h->blk16_maxr.as<uint8_t>() : (const uint8_t *)nullptr);
     h->timer.end(st);
     CM_HIP(hipGetLastError());
     if ((rc = launch_bm25_merge(w.cand_key, w.cand_row, nq, nr, k, score_dev, row_dev, st))) return rc;
