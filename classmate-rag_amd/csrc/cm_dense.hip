@@ -966,30 +966,7 @@ __global__ void __launch_bounds__(256, 1)
 
 // Block-wide radix select: the k-th smallest (0-based kk) of n u32 values in LDS (4 x 8-bit digits).
 __device__ inline uint32_t block_select_u32(const uint32_t *vals, int n, int kk, uint32_t *hist /*[256]*/) {
-  __shared__ uint32_t s_prefix, s_rem;
-  if (threadIdx.x == 0) {
-    s_prefix = 0;
-    s_rem = (uint32_t)kk;
-  }
-  for (int shift = 24; shift >= 0; shift -= 8) {
-    for (int b = threadIdx.x; b < 256; b += blockDim.x) hist[b] = 0;
-    __syncthreads();
-    const uint32_t prefix = s_prefix;
-    const uint32_t hmask = shift == 24 ? 0u : (0xffffffffu << (shift + 8));
-    for (int i = threadIdx.x; i < n; i += blockDim.x) {
-      const uint32_t x = vals[i];
-      if ((x & hmask) == (prefix & hmask)) atomicAdd(&hist[(x >> shift) & 255u], 1u);
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      uint32_t rem = s_rem, b = 0;
-      while (hist[b] <= rem) rem -= hist[b++];
-      s_prefix = prefix | (b << shift);
-      s_rem = rem;
-    }
-    __syncthreads();
-  }
-  return s_prefix;
+  return block_select_fn([&](int i) { return vals[i]; }, n, kk, hist);
 }
 
 // seed[q] = the k-th smallest per-group minimum + add_err x E: K1c / K1s add 2E (their minima are

@@ -7,6 +7,8 @@
 #include "cm_common.h"
 
 #include <algorithm>
+#include <cstdlib>
+#include <type_traits>
 #include <vector>
 
 namespace cm {
@@ -94,24 +96,30 @@ __global__ void __launch_bounds__(kMmrThreads) mmr_kernel(const float *__restric
 }
 
 // Same MMR for pools of <= kMmrLdsPool items (the retriever's 24): the pool and the query are
-// staged in LDS with all loads in flight, the (n + 1) x n similarity table is computed at once
-// (one exact fp64 dot per thread, rounded once to fp32 as above, so the values are the ones
-// mmr_kernel computes), and one wave runs the greedy loop on registers + shuffles with no
-// block barriers: first max wins ties (strict '>' in ascending index order).
+// staged in LDS with all loads in flight, the similarity table's distinct pairs are computed at
+// once (one fp64 dot per thread in dimension order, rounded once to fp32 as above, so the values
+// are the ones mmr_kernel computes), and one wave runs the greedy loop on registers + shuffles
+// with no block barriers: first max wins ties (strict '>' in ascending index order).
+// F64 (the rows fit LDS as doubles: pool <= 24 at dim 768): the rows are converted once while
+// staged and every product is one v_fma_f64 on two LDS doubles; otherwise the rows stay fp32 and
+// each product converts both.  fma(a, b, s) == s + a b here: the product of two fp32 values is
+// exact in fp64, so the fused and the separate forms round the same sum once.
 constexpr int kMmrLdsPool = 32;
 constexpr int kMmrLdsDim = 1024;
 
-constexpr int kMmrLdsThreads = 1024;  // 16 waves: the (n+1) n similarity pairs (600 at 24) in one pass
+constexpr int kMmrLdsThreads = 1024;  // 16 waves: the n (n + 1) / 2 + n distinct pairs (324 at 24) in one pass
+template <bool F64>
 __global__ void __launch_bounds__(kMmrLdsThreads) mmr_lds_kernel(const float *__restrict__ q, const float *__restrict__ cands,
                                                               const int32_t *__restrict__ n_valid, int pool, int dim,
                                                               int k, float lam32, float oml32,
                                                               int32_t *__restrict__ out_order) {
-  extern __shared__ __attribute__((aligned(16))) float mm_lds[];
+  extern __shared__ __attribute__((aligned(16))) unsigned char mm_raw[];
+  typedef typename std::conditional<F64, double, float>::type R;
   const int ld = dim + 1;                       // row pitch: rows start in different banks
-  float *rows = mm_lds;                         // [n + 1][ld]: pool rows, then the query
-  float *sim = mm_lds + (kMmrLdsPool + 1) * ld;  // [n + 1][kMmrLdsPool]: row n = sims_q
+  R *rows = reinterpret_cast<R *>(mm_raw);      // [n + 1][ld]: pool rows, then the query
   const int qi = blockIdx.x;
   const int n = min(n_valid ? n_valid[qi] : pool, pool);
+  float *sim = reinterpret_cast<float *>(mm_raw + (size_t)(pool + 1) * ld * sizeof(R));  // [n + 1][kMmrLdsPool]: row n = sims_q
   const int kk = min(k, n);
   for (int i = threadIdx.x; i < k; i += kMmrLdsThreads) out_order[(int64_t)qi * k + i] = -1;
   if (n <= 0) return;  // uniform
@@ -123,28 +131,38 @@ __global__ void __launch_bounds__(kMmrLdsThreads) mmr_lds_kernel(const float *__
     for (int t = threadIdx.x; t < (n + 1) * d4; t += kMmrLdsThreads) {
       const int r = t / d4, d = (t - r * d4) * 4;
       const float4 v = *reinterpret_cast<const float4 *>((r < n ? cv + (int64_t)r * dim : qv) + d);
-      float *o = rows + r * ld + d;
-      o[0] = v.x;
-      o[1] = v.y;
-      o[2] = v.z;
-      o[3] = v.w;
+      R *o = rows + r * ld + d;
+      o[0] = (R)v.x;
+      o[1] = (R)v.y;
+      o[2] = (R)v.z;
+      o[3] = (R)v.w;
     }
   } else {
     for (int t = threadIdx.x; t < (n + 1) * dim; t += kMmrLdsThreads) {
       const int r = t / dim, d = t - r * dim;
-      rows[r * ld + d] = r < n ? cv[(int64_t)r * dim + d] : qv[d];
+      rows[r * ld + d] = (R)(r < n ? cv[(int64_t)r * dim + d] : qv[d]);
     }
   }
   __syncthreads();
-  // pairs (i, j), i <= n (row n = the query), j < n, j <= i or i == n; each dot in dimension
-  // order with an fp64 accumulator (unchanged arithmetic: one pair per thread)
-  for (int p = threadIdx.x; p < (n + 1) * n; p += kMmrLdsThreads) {
-    const int i = p / n, j = p - i * n;
-    if (i < n && j > i) continue;
-    const float *a = rows + i * ld;
-    const float *b = rows + j * ld;
+  // the distinct pairs, packed: p < n (n + 1) / 2 -> (i, j), j <= i < n (row-major lower triangle);
+  // then the n query pairs (n, j).  Each dot in dimension order with an fp64 accumulator.
+  const int ntri = n * (n + 1) / 2;
+  for (int p = threadIdx.x; p < ntri + n; p += kMmrLdsThreads) {
+    int i, j;
+    if (p < ntri) {
+      i = (int)((sqrtf(8.f * (float)p + 1.f) - 1.f) * 0.5f);
+      while (i * (i + 1) / 2 > p) --i;
+      while ((i + 1) * (i + 2) / 2 <= p) ++i;
+      j = p - i * (i + 1) / 2;
+    } else {
+      i = n;
+      j = p - ntri;
+    }
+    const R *a = rows + i * ld;
+    const R *b = rows + j * ld;
     double acc = 0.0;
-    for (int d = 0; d < dim; ++d) acc += (double)a[d] * (double)b[d];
+#pragma unroll 8
+    for (int d = 0; d < dim; ++d) acc = __builtin_fma((double)a[d], (double)b[d], acc);
     const float v = (float)acc;
     sim[i * kMmrLdsPool + j] = v;
     if (i < n) sim[j * kMmrLdsPool + i] = v;
@@ -305,6 +323,94 @@ __global__ void rrf_merge_kernel(const int64_t *__restrict__ vkeys, const float 
   out_n[qi] = n_out;
 }
 
+// The same merge with one wave per query (kv + kb <= 64; rrf_merge_kernel above for longer lists):
+// lane r holds vector item r and BM25 item r.  A BM25 item's match is the first vector item with
+// its id (shuffles over the vector lanes); each vector item adds the contributions of the BM25
+// items that matched it in BM25 rank order; unmatched BM25 items take insertion positions nv, nv +
+// 1, ... in rank order (ballot prefix).  Every fused value is the same sequence of fp64 operations
+// as in rrf_merge_kernel.  The final order: an item's output position is the number of items
+// before it in the stable descending (fused, -distance) order -- what the insertion sort yields.
+constexpr int kRrfWaveCap = 64;
+__global__ void __launch_bounds__(256) rrf_merge_wave_kernel(
+    const int64_t *__restrict__ vkeys, const float *__restrict__ vdist, const int32_t *__restrict__ vn, int kv,
+    const int64_t *__restrict__ bkeys, const double *__restrict__ bscore, const int32_t *__restrict__ bn, int kb, int nq,
+    double w_vec, double w_bm25, int rrf_k, int top_k, int64_t *__restrict__ out_keys, double *__restrict__ out_fused,
+    float *__restrict__ out_vdist, double *__restrict__ out_bscore, int32_t *__restrict__ out_flags,
+    int32_t *__restrict__ out_n) {
+  __shared__ double s_f[4][kRrfWaveCap], s_v[4][kRrfWaveCap];
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int qi0 = blockIdx.x * 4 + wv;
+  const bool act = qi0 < nq;                    // wave-uniform (inactive waves still reach the barrier)
+  const int qi = act ? qi0 : 0;
+  const int nv = !act ? 0 : vn ? min(vn[qi], kv) : kv;
+  const int nb = !act ? 0 : bn ? min(bn[qi], kb) : kb;
+  const bool hv = lane < nv, hb = lane < nb;
+  const int64_t vid = hv ? vkeys[(int64_t)qi * kv + lane] : -1;
+  const int64_t bid = hb ? bkeys[(int64_t)qi * kb + lane] : -1;
+  const double bc = w_bm25 * (1.0 / (double)(rrf_k + (lane + 1)));
+  int f = -1;                                   // BM25 item lane's first matching vector item
+  for (int j = 0; j < nv; ++j) {
+    const int64_t kj = __shfl(vid, j);
+    if (f < 0 && hb && kj == bid) f = j;
+  }
+  double fv = 0.0 + w_vec * (1.0 / (double)(rrf_k + (lane + 1)));
+  int32_t srcv = lane + 1;
+  for (int r = 0; r < nb; ++r) {
+    const int fr = __shfl(f, r);
+    const double cr = __shfl(bc, r);
+    if (fr == lane) {
+      fv = fv + cr;
+      srcv |= (r + 1) << 16;
+    }
+  }
+  const bool un = hb && f < 0;                  // BM25-only item
+  const uint64_t um = __ballot(un);
+  const int upos = nv + __popcll(um & ((1ull << lane) - 1ull));
+  const int m = nv + __popcll(um);
+  const double vdv = hv ? -(double)vdist[(int64_t)qi * kv + lane] : 0.0;
+  const double fb = 0.0 + bc, vdb = -0.0;
+  if (hv) {
+    s_f[wv][lane] = fv;
+    s_v[wv][lane] = vdv;
+  }
+  if (un) {
+    s_f[wv][upos] = fb;
+    s_v[wv][upos] = vdb;
+  }
+  __syncthreads();
+  if (!act) return;
+  auto rank_of = [&](double fx, double vx, int px) {
+    int rk = 0;
+    for (int e = 0; e < m; ++e) {
+      const double fe = s_f[wv][e], ve = s_v[wv][e];
+      rk += (fe > fx || (fe == fx && (ve > vx || (ve == vx && e < px)))) ? 1 : 0;
+    }
+    return rk;
+  };
+  const int n_out = min(m, top_k);
+  auto emit = [&](int rk, int64_t key, double fx, int32_t src) {
+    if (rk >= top_k) return;
+    const int vi = (src & 0xffff) - 1, bi = (src >> 16) - 1;
+    const int64_t o = (int64_t)qi * top_k + rk;
+    out_keys[o] = key;
+    out_fused[o] = fx;
+    out_vdist[o] = vi >= 0 ? vdist[(int64_t)qi * kv + vi] : 0.f;
+    out_bscore[o] = bi >= 0 ? bscore[(int64_t)qi * kb + bi] : 0.0;
+    out_flags[o] = (vi >= 0 ? 1 : 0) | (bi >= 0 ? 2 : 0);
+  };
+  if (hv) emit(rank_of(fv, vdv, lane), vid, fv, srcv);
+  if (un) emit(rank_of(fb, vdb, upos), bid, fb, (lane + 1) << 16);
+  for (int i = n_out + lane; i < top_k; i += 64) {
+    const int64_t o = (int64_t)qi * top_k + i;
+    out_keys[o] = -1;
+    out_fused[o] = 0.0;
+    out_vdist[o] = 0.f;
+    out_bscore[o] = 0.0;
+    out_flags[o] = 0;
+  }
+  if (lane == 0) out_n[qi] = n_out;
+}
+
 // rrf_fuse over arbitrary lists (dict semantics) on one lane.
 __global__ void rrf_fuse_kernel(const int64_t *__restrict__ keys, const int32_t *__restrict__ off, int nl,
                                 const double *__restrict__ weights, int rrf_k, int64_t *__restrict__ out_keys,
@@ -450,14 +556,24 @@ int cm_mmr_dev(const float *q_dev, const float *cands_dev, const int32_t *n_vali
   const float lam32 = (float)lambd;
   const float oml32 = (float)(1.0 - lambd);
   if (pool <= kMmrLdsPool && dim <= kMmrLdsDim) {
-    const size_t lds = ((size_t)(kMmrLdsPool + 1) * (dim + 1) + (size_t)(kMmrLdsPool + 1) * kMmrLdsPool) * 4;
-    static const hipError_t attr =
-        hipFuncSetAttribute(reinterpret_cast<const void *>(&mmr_lds_kernel),
-                            hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)(((kMmrLdsPool + 1) * (kMmrLdsDim + 1) + (kMmrLdsPool + 1) * kMmrLdsPool) * 4));
+    constexpr int kMax = 160 * 1024;
+    const size_t sim_bytes = (size_t)(kMmrLdsPool + 1) * kMmrLdsPool * 4;
+    const size_t lds64 = (size_t)(pool + 1) * (dim + 1) * 8 + sim_bytes;
+    static const hipError_t attr = [] {
+      hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&mmr_lds_kernel<true>),
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, kMax);
+      return e != hipSuccess ? e
+                             : hipFuncSetAttribute(reinterpret_cast<const void *>(&mmr_lds_kernel<false>),
+                                                   hipFuncAttributeMaxDynamicSharedMemorySize, kMax);
+    }();
     CM_HIP(attr);
-    hipLaunchKernelGGL(mmr_lds_kernel, dim3(nq), dim3(kMmrLdsThreads), lds, (hipStream_t)stream, q_dev, cands_dev,
-                       n_valid_dev, pool, dim, k, lam32, oml32, order_dev);
+    if (lds64 <= (size_t)kMax)
+      hipLaunchKernelGGL(mmr_lds_kernel<true>, dim3(nq), dim3(kMmrLdsThreads), lds64, (hipStream_t)stream, q_dev,
+                         cands_dev, n_valid_dev, pool, dim, k, lam32, oml32, order_dev);
+    else
+      hipLaunchKernelGGL(mmr_lds_kernel<false>, dim3(nq), dim3(kMmrLdsThreads),
+                         (size_t)(pool + 1) * (dim + 1) * 4 + sim_bytes, (hipStream_t)stream, q_dev, cands_dev,
+                         n_valid_dev, pool, dim, k, lam32, oml32, order_dev);
     CM_HIP(hipGetLastError());
     return CM_OK;
   }
@@ -540,7 +656,15 @@ int cm_rrf_merge_dev(const int64_t *vkeys, const float *vdist, const int32_t *vn
   double *sf = c.take<double>((size_t)nq * cap);
   double *sv = c.take<double>((size_t)nq * cap);
   int32_t *ss = c.take<int32_t>((size_t)nq * cap);
-  if (cap <= kRrfLdsCap)
+  static const bool wave_on = [] {   // CM_RRF_WAVE=0: the lane-per-query kernel (A/B)
+    const char *e = getenv("CM_RRF_WAVE");
+    return !(e && e[0] == '0');
+  }();
+  if (wave_on && kv <= kRrfWaveCap && kb <= kRrfWaveCap && kv + kb <= kRrfWaveCap)
+    hipLaunchKernelGGL(rrf_merge_wave_kernel, dim3((unsigned)ceil_div(nq, 4)), dim3(256), 0, (hipStream_t)stream,
+                       vkeys, vdist, vn, kv, bkeys, bscore, bn, kb, nq, w_vec, w_bm25, rrf_k, top_k, out_keys,
+                       out_fused, out_vdist, out_bscore, out_flags, out_n);
+  else if (cap <= kRrfLdsCap)
     hipLaunchKernelGGL(rrf_merge_kernel<true>, dim3((unsigned)ceil_div(nq, 64)), dim3(64), (size_t)cap * 64 * 28,
                        (hipStream_t)stream, vkeys, vdist, vn, kv, bkeys, bscore, bn, kb, nq, w_vec, w_bm25, rrf_k,
                        top_k, out_keys, out_fused, out_vdist, out_bscore, out_flags, out_n, sk, sf, sv, ss);

@@ -726,26 +726,61 @@ def test_mmr_small_and_large_pools_match_oracle(eng, pool):
             want = orc.mmr_order(q[i], cands[i][:n], list(range(n)), k, lam)
             assert order[i][: len(want)].tolist() == want, (i, n, k)
             assert (order[i][len(want):] == -1).all()
+        if pool == 24:   # fp64 LDS rows (pool 24) and fp32 LDS rows (the same items in a 32-slot pool)
+            wide = np.zeros((nq, 32, dim), np.float32)
+            wide[:, :pool] = cands
+            assert np.array_equal(eng.mmr_order_batch(q, wide, k, lam, n_valid=nv), order)
 
 
-def test_rrf_merge_lds_and_global_paths_agree(eng):
-    """kv + kb <= 32 keeps the RRF merge lists in LDS, longer lists use global scratch: the same
-    valid items give the same fused lists (bit-identical) on both paths."""
+def _merge_ref(vk, vd, bk, bs, w_vec, w_bm25, rrf_k, top_k):
+    """HybridRetriever.retrieve's merge (rag/retrieval/fusion.py:130-167) on one query's lists."""
+    fused = orc.rrf_fuse(rank_lists=[list(vk), list(bk)], weights=[w_vec, w_bm25], rrf_k=rrf_k)
+    by_id = {}
+    for i, d in zip(vk, vd):
+        by_id.setdefault(i, [i, None, None])[1] = float(d)
+    for i, b in zip(bk, bs):
+        by_id.setdefault(i, [i, None, None])[2] = float(b)
+    items = sorted(by_id.values(), key=lambda it: (fused[it[0]], -(it[1] if it[1] is not None else 0.0)),
+                   reverse=True)[:top_k]
+    return [(it[0], fused[it[0]], it[1], it[2]) for it in items]
+
+
+def test_rrf_merge_wave_lds_and_global_paths_agree(eng):
+    """kv + kb <= 64 runs the wave-per-query RRF merge, longer lists the lane-per-query kernel on
+    global scratch: the same valid items give the same fused lists (bit-identical) on both paths,
+    equal to the reference's merge (dict order, stable sort on (fused, -distance)) -- including
+    equal distances, BM25 ids that are also vector ids, and empty lists."""
     rng = np.random.default_rng(7)
     nq = 300
-    vk = np.stack([rng.choice(60, 20, replace=False) for _ in range(nq)]).astype(np.int64)
-    bk = np.stack([rng.choice(60, 20, replace=False) for _ in range(nq)]).astype(np.int64)
-    vd = rng.random((nq, 20)).astype(np.float32)
+    vk = np.stack([rng.choice(90, 40, replace=False) for _ in range(nq)]).astype(np.int64)
+    bk = np.stack([rng.choice(90, 40, replace=False) for _ in range(nq)]).astype(np.int64)
+    vd = rng.random((nq, 40)).astype(np.float32)
     vd[:, 3] = vd[:, 2]                                     # equal distances: tie order
-    bs = rng.standard_normal((nq, 20))
+    bs = rng.standard_normal((nq, 40))
     vn = rng.integers(0, 17, nq).astype(np.int32)
     bn = rng.integers(0, 17, nq).astype(np.int32)
+    vn[:3], bn[:3] = 0, (0, 5, 0)
+    bn[3] = 0
+    bk[5, :8] = vk[5, 7::-1]                                # BM25 = reversed vector ids: every fused value ties pairwise
+    vn[5] = bn[5] = 8
     kw = dict(w_vec=1.0, w_bm25=0.7, rrf_k=60, top_k=12)
-    small = eng.rrf_merge(vk[:, :16].copy(), vd[:, :16].copy(), vn, bk[:, :16].copy(), bs[:, :16].copy(), bn, **kw)
-    large = eng.rrf_merge(vk, vd, vn, bk, bs, bn, **kw)
-    for a, b in zip(small, large):
-        assert np.array_equal(np.asarray(a), np.asarray(b))
-    assert int(np.asarray(small[-1]).max()) > 0
+    runs = [eng.rrf_merge(vk[:, :c].copy(), vd[:, :c].copy(), vn, bk[:, :c].copy(), bs[:, :c].copy(), bn, **kw)
+            for c in (16, 32, 40)]                          # wave, wave (kv + kb = 64), global
+    for other in runs[1:]:
+        for a, b in zip(runs[0], other):
+            assert np.array_equal(np.asarray(a), np.asarray(b))
+    ok, of, ov, ob, ofl, on = runs[0]
+    assert int(np.asarray(on).max()) > 0
+    for q in range(nq):
+        want = _merge_ref(vk[q, :vn[q]].tolist(), vd[q, :vn[q]], bk[q, :bn[q]].tolist(), bs[q, :bn[q]],
+                          kw["w_vec"], kw["w_bm25"], kw["rrf_k"], kw["top_k"])
+        assert on[q] == len(want), q
+        for r, (i, f, d, b) in enumerate(want):
+            assert ok[q, r] == i and of[q, r] == f, (q, r)
+            assert ofl[q, r] == (1 if d is not None else 0) | (2 if b is not None else 0)
+            assert ov[q, r] == (np.float32(d) if d is not None else 0.0)
+            assert ob[q, r] == (b if b is not None else 0.0)
+        assert (ok[q, len(want):] == -1).all()
 
 
 def _dev_queries(qs):
