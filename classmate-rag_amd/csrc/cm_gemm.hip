@@ -265,6 +265,8 @@ __global__ void __launch_bounds__(64 * NW)
   static_assert(H1 >= 1, "a row tile before the barrier");
   // threaded schedule of the second half: PCS groups of (NMF2 / PCS MFMAs, NRD / PCS reads, 1 DMA piece)
   constexpr bool THREAD = NMF2 % PCS == 0 && NRD % PCS == 0 && NMF2 / PCS >= NRD / PCS + 1;
+  // the 96 x 288 tile's counts do not divide (18 MFMAs, 12 reads, 4 pieces): spread them evenly
+  constexpr bool SPREAD = !THREAD && BNB == 18;
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -396,6 +398,8 @@ __global__ void __launch_bounds__(64 * NW)
       k10_spread<NMF2, 0, PCS, false>(std::make_integer_sequence<int, NMF2>{});                              \
     } else if constexpr (K10_SCHED == 3) {                                                                   \
       k10_spread<NMF2, NRD, PCS, true>(std::make_integer_sequence<int, NMF2>{});                             \
+    } else if constexpr (SPREAD) {                                                                           \
+      k10_spread<NMF2, NRD, PCS, false>(std::make_integer_sequence<int, NMF2>{});                            \
     } else if constexpr (THREAD) {                                                                           \
       _Pragma("unroll") for (int q_ = 0; q_ < PCS; ++q_) {                                                   \
         _Pragma("unroll") for (int r_ = 0; r_ < NRD / PCS; ++r_) {                                           \
@@ -553,10 +557,17 @@ static TileCfg pick_tile(int64_t M, int N, int n_cu) {
   // over N / (tile width) workgroups, so a 64 x 32 tile puts twice the CUs of 64 x 64 on it (the
   // per-element k order, hence every output bit, does not depend on the tile)
   if (M <= 32 && N % 32 == 0) return TileCfg{4, 2};
-  const TileCfg cands[4] = {{6, 12}, {8, 8}, {4, 8}, {4, 4}};
+  // 96 x 288 (the query batch's QKV projection, N = 2304 at M = 6144: 512 tiles = two per CU instead
+  // of three 96 x 192 ones; fewer fragment reads per MFMA and operand bytes per flop)
+  static const bool t288 = [] {
+    const char *e = getenv("CM_K10_T288");
+    return !(e && e[0] == '0');
+  }();
+  const TileCfg cands[5] = {{6, 12}, {8, 8}, {4, 8}, {4, 4}, {6, 18}};
   TileCfg best = {0, 0};
   double best_cost = 0;
   for (const TileCfg &c : cands) {
+    if (c.bnb == 18 && !t288) continue;
     if (N % (16 * c.bnb)) continue;
     const int64_t tiles = ceil_div(M, 16 * c.bmb) * (N / (16 * c.bnb));
     const double cost = (double)ceil_div(tiles, n_cu) * (c.bmb * c.bnb + 2 * (c.bmb + c.bnb));
@@ -667,6 +678,8 @@ extern "C" int cm_linear_f16x3(const void *a_planes, int64_t M, int32_t K, const
     return launch_tile<12, 12, 3, 8>(A, M, K, W, bias_dev, out_scale, N, epilogue, c_dev, next_scale, Cp, g_n_cu, st);
   if (t.bmb == 8 && t.bnb == 16)
     return launch_tile<8, 16, 3, 8>(A, M, K, W, bias_dev, out_scale, N, epilogue, c_dev, next_scale, Cp, g_n_cu, st);
+  if (t.bmb == 6 && t.bnb == 18)
+    return launch_tile<6, 18, 3, 12>(A, M, K, W, bias_dev, out_scale, N, epilogue, c_dev, next_scale, Cp, g_n_cu, st);
   if (t.bmb == 6)
     return launch_tile<6, 12, K10_S6 ? K10_S6 : (K10_W6 == 8 ? 3 : 4), K10_W6>(A, M, K, W, bias_dev, out_scale, N, epilogue, c_dev,
                                                            next_scale, Cp, g_n_cu, st);
