@@ -97,6 +97,9 @@ __device__ __forceinline__ h16x8 as_h8(i32x4 v) { return __builtin_bit_cast(h16x
 #ifndef K10_H1
 #define K10_H1 0
 #endif
+#ifndef K10_SPREAD_ALL
+#define K10_SPREAD_ALL 0     // 1: every tile whose counts do not divide gets the spread schedule (A/B knob)
+#endif
 
 // one MFMA slot of the spread schedule: the MFMA, then its share of reads and DMA pieces (EARLY:
 // one read after each of the first NR MFMAs instead of an even spread)
@@ -266,7 +269,7 @@ __global__ void __launch_bounds__(64 * NW)
   // threaded schedule of the second half: PCS groups of (NMF2 / PCS MFMAs, NRD / PCS reads, 1 DMA piece)
   constexpr bool THREAD = NMF2 % PCS == 0 && NRD % PCS == 0 && NMF2 / PCS >= NRD / PCS + 1;
   // the 96 x 288 tile's counts do not divide (18 MFMAs, 12 reads, 4 pieces): spread them evenly
-  constexpr bool SPREAD = !THREAD && BNB == 18;
+  constexpr bool SPREAD = !THREAD && (BNB == 18 || K10_SPREAD_ALL);
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
 
   const int tid = threadIdx.x, lane = tid & 63;
