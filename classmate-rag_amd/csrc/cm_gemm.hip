@@ -97,6 +97,9 @@ __device__ __forceinline__ h16x8 as_h8(i32x4 v) { return __builtin_bit_cast(h16x
 #ifndef K10_H1
 #define K10_H1 0
 #endif
+#ifndef K10_H1_6
+#define K10_H1_6 0           // > 0: row tiles before the mid-step barrier of the 96-row tiles only (A/B knob)
+#endif
 #ifndef K10_SPREAD_ALL
 #define K10_SPREAD_ALL 0     // 1: every tile whose counts do not divide gets the spread schedule (A/B knob)
 #endif
@@ -260,7 +263,8 @@ __global__ void __launch_bounds__(64 * NW)
   constexpr int PCS = (NBLK + NW - 1) / NW;           // DMA pieces per wave per stage (uniform count:
                                                       // pieces past NBLK re-load block 0 into a pad)
   constexpr int STAGE = PCS * NW * 1024;
-  constexpr int H1 = (K10_H1 > 0 && K10_H1 < WMT) ? K10_H1 : WMT / 2;   // row tiles before the mid-step barrier
+  constexpr int H1 = (BMB == 6 && K10_H1_6 > 0 && K10_H1_6 < WMT) ? K10_H1_6   // row tiles before the mid-step barrier
+                     : (K10_H1 > 0 && K10_H1 < WMT) ? K10_H1 : WMT / 2;
   constexpr int NMF2 = 3 * (WMT - H1) * WNT;          // MFMAs after it
   constexpr int NRD = 2 * (WMT + WNT);                // fragment reads per step
   static_assert(BMB % 2 == 0 && BNB % WGN == 0, "tile must split over the waves");
